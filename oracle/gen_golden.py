@@ -1,0 +1,162 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ from the REAL reference (TEST INFRASTRUCTURE ONLY).
+
+Runs oracle/_ref/ref_golden (our driver around the unmodified reference header
+/root/reference/allreduce_over_mpi/mpi_mod.hpp, built by `make -C oracle ref`)
+under MPICH's mpiexec and packs what the reference produced into small
+fixtures:
+
+  tests/golden/manifest.json   every case: parameters, per-rank sha256 of the
+                               reference output, whether all ranks agree, and
+                               which array (if any) holds the full output
+  tests/golden/allreduce.npz   full rank-0 outputs of the small allreduce cases
+  tests/golden/reduce.npz      outputs of FlexTree::reduce_sum / reduce_band
+  tests/golden/schedules.jsonl FMA-level send/recv schedules per rank
+  tests/golden/inputs.json     first draws of the input generator (pins it)
+
+Inputs are not stored: they are regenerated from (seed, rank) with
+include/ftar_inputs.h / tests/ftar_inputs.py, which inputs.json pins.
+
+Usage:  python oracle/gen_golden.py   (needs /root/reference, MPICH, ~2 min)
+"""
+import hashlib
+import itertools
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import ftar_inputs as fi  # noqa: E402
+
+REF = os.path.join(HERE, "_ref", "ref_golden")
+MPIEXEC = os.environ.get("MPIEXEC", "/opt/conda/bin/mpiexec")
+OUT = os.path.join(ROOT, "tests", "golden")
+FULL_MAX = 4099          # store full outputs up to this many elements
+SEED = 20240601
+
+# (P, FT_TOPO, FT_LONELY)
+TOPOS = [
+    (2, "1", 0), (3, "1", 0), (4, "1", 0), (5, "1", 0), (8, "1", 0),
+    (2, "2", 0), (3, "3", 0), (4, "4", 0), (4, "2,2", 0), (6, "2,3", 0), (6, "3,2", 0),
+    (8, "8", 0), (8, "2,4", 0), (8, "4,2", 0), (8, "2,2,2", 0), (9, "3,3", 0),
+    (5, "2,2", 1), (7, "2,3", 1), (7, "3,2", 1), (9, "2,4", 1), (6, "2,2", 2), (8, "3,2", 2),
+    (9, "2,2,2", 1),
+]
+SIZES = [1, 3, 7, 17, 1003, 65541]
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def run_allreduce(P, topo, lonely, dtype, op, n, seed, oop=False, repeat=1, init="random"):
+    with tempfile.TemporaryDirectory() as td:
+        prefix = os.path.join(td, "ar")
+        env = dict(os.environ, FT_TOPO=topo, FT_LONELY=str(lonely))
+        cmd = [MPIEXEC, "-n", str(P), REF, "allreduce", "--dtype", str(dtype), "--op", str(op),
+               "--n", str(n), "--seed", str(seed), "--repeat", str(repeat), "--init", init, "--out", prefix]
+        if oop:
+            cmd.append("--outofplace")
+        subprocess.run(cmd, env=env, check=True, stdout=subprocess.DEVNULL, timeout=300)
+        outs = []
+        for r in range(P):
+            with open(f"{prefix}.{r}.bin", "rb") as f:
+                outs.append(f.read())
+    return outs
+
+
+def main():
+    if not os.path.exists(REF):
+        sys.exit("build the reference driver first: make -C oracle ref")
+    os.makedirs(OUT, exist_ok=True)
+    cases, arrays = [], {}
+
+    def add_case(P, topo, lonely, dtype, op, n, seed, oop=False, repeat=1, init="random"):
+        outs = run_allreduce(P, topo, lonely, dtype, op, n, seed, oop, repeat, init)
+        cid = f"ar_P{P}_t{topo.replace(',', '-')}_l{lonely}_{fi.DTYPES[dtype][0]}_op{op}_n{n}" + \
+              ("_oop" if oop else "") + (f"_rep{repeat}" if repeat > 1 else "") + ("_lin" if init != "random" else "")
+        shas = [sha(o) for o in outs]
+        c = dict(id=cid, P=P, topo=topo, lonely=lonely, dtype=dtype, op=op, n=n, seed=seed,
+                 outofplace=oop, repeat=repeat, init=init, sha256=shas, all_equal=len(set(shas)) == 1)
+        if n <= FULL_MAX:
+            if c["all_equal"]:
+                arrays[cid] = np.frombuffer(outs[0], dtype=fi.np_dtype(dtype)).copy()
+            else:
+                for r, o in enumerate(outs):
+                    arrays[f"{cid}__r{r}"] = np.frombuffer(o, dtype=fi.np_dtype(dtype)).copy()
+            c["stored"] = True
+        else:
+            a = np.frombuffer(outs[0], dtype=fi.np_dtype(dtype))
+            c["stored"] = False
+            c["head"] = a[:16].tolist()
+            c["tail"] = a[-16:].tolist()
+        cases.append(c)
+        print(cid, "all_equal" if c["all_equal"] else "RANKS DIFFER", flush=True)
+
+    # 1. fp32 sum, every topology x size, in place (benchmark.cpp:161)
+    for (P, topo, lonely), n in itertools.product(TOPOS, SIZES):
+        add_case(P, topo, lonely, 6, 0, n, SEED)
+    # 2. out-of-place (sendbuf != MPI_IN_PLACE) at a ragged size
+    for P, topo, lonely in TOPOS:
+        add_case(P, topo, lonely, 6, 0, 1003, SEED + 1, oop=True)
+    # 3. every reference datatype / op on three schedules
+    for (P, topo, lonely), dt in itertools.product([(4, "1", 0), (4, "2,2", 0), (5, "2,2", 1)], [0, 1, 2, 3, 4, 5, 7, 8]):
+        add_case(P, topo, lonely, dt, 0, 1003, SEED + 2)
+        if dt not in (7, 8):
+            add_case(P, topo, lonely, dt, 1, 1003, SEED + 3)
+    # 4. repeated in-place calls (benchmark.cpp --repeat semantics)
+    for P, topo, lonely in [(4, "1", 0), (4, "2,2", 0), (8, "8", 0)]:
+        add_case(P, topo, lonely, 6, 0, 1003, SEED + 4, repeat=3)
+    # 5. the benchmark.cpp workload itself: data[i] = i*0.1f, C1 = P2 ring 2^20
+    add_case(2, "1", 0, 6, 0, 1 << 20, 0, init="linear")
+    add_case(8, "8", 0, 6, 0, 1 << 16, 0, init="linear")
+
+    np.savez_compressed(os.path.join(OUT, "allreduce.npz"), **arrays)
+
+    # reduce_sum / reduce_band directly
+    red = {}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "r.bin")
+        specs = [(6, 0, k, 1003) for k in range(1, 21)] + [(dt, 0, 3, 1003) for dt in (0, 1, 2, 3, 4, 5, 7, 8)] + \
+                [(dt, 1, k, 1003) for dt in (0, 1, 2, 3, 4, 5) for k in (1, 2, 3, 7)] + [(6, 0, 2, 0), (6, 0, 5, 1)]
+        for dt, op, k, n in specs:
+            subprocess.run([REF, "reduce", "--dtype", str(dt), "--op", str(op), "--k", str(k), "--n", str(n),
+                            "--seed", str(SEED + 7), "--out", path], check=True, stdout=subprocess.DEVNULL)
+            rid = f"red_{fi.DTYPES[dt][0]}_op{op}_k{k}_n{n}"
+            with open(path, "rb") as f:
+                red[rid] = np.frombuffer(f.read(), dtype=fi.np_dtype(dt)).copy()
+            cases.append(dict(id=rid, kind="reduce", dtype=dt, op=op, k=k, n=n, seed=SEED + 7))
+    np.savez_compressed(os.path.join(OUT, "reduce.npz"), **red)
+
+    # schedules
+    with open(os.path.join(OUT, "schedules.jsonl"), "w") as f:
+        for (P, topo, lonely), n in itertools.product([t for t in TOPOS if t[1] != "1"], [3, 27, 1003]):
+            out = subprocess.run([REF, "schedule", "--P", str(P), "--topo", topo, "--lonely", str(lonely), "--n", str(n)],
+                                 check=True, capture_output=True, text=True).stdout
+            for line in out.strip().splitlines():
+                d = json.loads(line)
+                d.update(P=P, topo=topo, lonely=lonely, n=n)
+                f.write(json.dumps(d, separators=(",", ":")) + "\n")
+
+    # generator pin
+    pins = []
+    for dt in range(10):
+        for seed, stream in [(1, 0), (SEED, 3)]:
+            pins.append(dict(dtype=dt, seed=seed, stream=stream, values=fi.fill(dt, seed, stream, 8).tolist()))
+    with open(os.path.join(OUT, "inputs.json"), "w") as f:
+        json.dump(dict(raw_seed1_stream0=[int(x) for x in fi.raw(1, 0, 4)], fills=pins), f)
+
+    with open(os.path.join(OUT, "manifest.json"), "w") as f:
+        json.dump(dict(generator="oracle/gen_golden.py", reference="mpi_mod.hpp via oracle/ref_golden.cpp, MPICH 3.3.2",
+                       cases=cases), f, indent=0)
+    print(len(cases), "cases written")
+
+
+if __name__ == "__main__":
+    main()
