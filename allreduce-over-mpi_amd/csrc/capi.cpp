@@ -1,0 +1,252 @@
+// C ABI: version/errors, the one-device reduce, topology parsing, the
+// re-fitted cost model and schedule introspection.  Communicator and
+// AllReduce entry points live in engine.cpp.
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <sstream>
+
+#include "ftar_internal.h"
+
+namespace ftar {
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+void set_error(const std::string& msg, const char* file, int line) {
+  g_last_error = msg + " (" + file + ":" + std::to_string(line) + ")";
+  if (getenv("FTAR_DEBUG")) fprintf(stderr, "[ftar] %s\n", g_last_error.c_str());
+}
+const char* last_error() { return g_last_error.c_str(); }
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// cost model.  The reference (cost_model/CostModel.h:1-80) scores a width list
+// with per-layer latency `lo`, memory steps `o` and (P-1)/P*s*bo for a
+// 16-host MPI cluster; it never sees that one tree stage of width w talks to
+// w-1 peers AT ONCE.  On an MI355X node every peer is its own xGMI link, so
+// here a stage of width w on data D moves D/w to each of w-1 peers in
+// parallel, then reduces w+1 streams through HBM:
+//   stage(w, D) = 2*alpha + 2*(D/w)/link + (w+1)*(D/w)/hbm,   D /= w per stage
+//   ring        = 2(P-1)*alpha + 2(P-1)*(S/P)/link + 3(P-1)*(S/P)/hbm
+// alpha = one p2p group (launch + handshake), link = one peer's unidirectional
+// xGMI bandwidth, hbm = achieved reduce bandwidth.  Defaults are MI355X
+// figures (DESIGN.md §Cost model); FTAR_COST_{ALPHA_US,LINK_GBPS,HBM_GBPS}
+// override them.
+// ---------------------------------------------------------------------------
+struct CostConsts {
+  double alpha = 20e-6, link = 48e9, hbm = 5.0e12;
+  CostConsts() {
+    if (const char* e = getenv("FTAR_COST_ALPHA_US")) alpha = atof(e) * 1e-6;
+    if (const char* e = getenv("FTAR_COST_LINK_GBPS")) link = atof(e) * 1e9;
+    if (const char* e = getenv("FTAR_COST_HBM_GBPS")) hbm = atof(e) * 1e9;
+  }
+};
+
+double model_cost(const Topology& t, int P, size_t bytes) {
+  CostConsts k;
+  const double S = (double)bytes;
+  if (P <= 1) return 0.0;
+  if (t.ring) {
+    const double blk = S / P;
+    return 2.0 * (P - 1) * k.alpha + 2.0 * (P - 1) * blk / k.link + 3.0 * (P - 1) * blk / k.hbm;
+  }
+  double D = S, cost = 0.0;
+  for (size_t w : t.widths) {
+    const double piece = D / (double)w;
+    cost += 2.0 * k.alpha + 2.0 * piece / k.link + (double)(w + 1) * piece / k.hbm;
+    D = piece;
+  }
+  if (t.lonely) cost += 4.0 * k.alpha + 2.0 * (S / P) / k.link;  // lonely exchange stages
+  return cost;
+}
+
+// every ordered factorization of n into factors >= 2 (cost_model/GetWidth.h:10-47)
+void factorizations(size_t n, std::vector<size_t>& cur, std::vector<std::vector<size_t>>& out) {
+  if (n == 1) {
+    if (!cur.empty()) out.push_back(cur);
+    return;
+  }
+  for (size_t f = 2; f <= n; ++f)
+    if (n % f == 0) {
+      cur.push_back(f);
+      factorizations(n / f, cur, out);
+      cur.pop_back();
+    }
+}
+
+}  // namespace
+}  // namespace ftar
+
+extern "C" {
+
+const char* ftar_version(void) {
+  static char v[64];
+  snprintf(v, sizeof v, "ftar %d.%d (gfx950)", FTAR_VERSION_MAJOR, FTAR_VERSION_MINOR);
+  return v;
+}
+
+const char* ftar_status_string(ftar_status_t s) {
+  switch (s) {
+    case FTAR_SUCCESS: return "success";
+    case FTAR_ERR_INVALID_ARG: return "invalid argument";
+    case FTAR_ERR_UNSUPPORTED: return "unsupported dtype/op";
+    case FTAR_ERR_INVALID_TOPO: return "invalid FT_TOPO/FT_LONELY";
+    case FTAR_ERR_HIP: return "HIP error";
+    case FTAR_ERR_RCCL: return "RCCL error";
+    case FTAR_ERR_INTERNAL: return "internal error";
+    case FTAR_ERR_TIMEOUT: return "timeout";
+  }
+  return "unknown";
+}
+
+const char* ftar_last_error(void) { return ftar::last_error(); }
+
+size_t ftar_dtype_size(ftar_dtype_t dt) { return ftar::dtype_size(dt); }
+
+ftar_status_t ftar_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                          void* stream) {
+  return ftar::launch_reduce(srcs, k, dst, count, dtype, op, static_cast<hipStream_t>(stream));
+}
+
+// get_stages (mpi_mod.hpp:1419-1486), minus its two bugs: an unset FT_TOPO
+// is reported (the reference exit(1)s for every P > 1) and a trailing comma
+// does not repeat the last width (the reference's `while(!ss.eof())` does).
+ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nranks, ftar_topo_t* out) {
+  if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  ftar_topo_t t{};
+  if (ft_lonely && *ft_lonely) t.lonely = atoi(ft_lonely);
+  if (!ft_topo || !*ft_topo) {
+    if (nranks == 1) {
+      t.nstages = 1;
+      t.stages[0] = 1;
+      *out = t;
+      return FTAR_SUCCESS;
+    }
+    return FTAR_ERR_INVALID_TOPO;
+  }
+  std::string s(ft_topo);
+  for (char& ch : s)
+    if (ch == ',') ch = ' ';
+  std::istringstream is(s);
+  long w;
+  while (is >> w) {
+    if (t.nstages >= FTAR_MAX_STAGES || w <= 0) return FTAR_ERR_INVALID_TOPO;
+    if (w == 1) {  // any 1 => ring
+      ftar_topo_t r{};
+      r.nstages = 1;
+      r.stages[0] = 1;
+      r.ring = 1;
+      *out = r;
+      return FTAR_SUCCESS;
+    }
+    t.stages[t.nstages++] = (int)w;
+  }
+  if (!is.eof() || t.nstages == 0) return FTAR_ERR_INVALID_TOPO;
+  ftar::Topology chk;
+  ftar_status_t st = ftar::to_topology(&t, nranks, &chk);
+  if (st != FTAR_SUCCESS) return st;
+  *out = t;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
+  if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  ftar::Topology best;
+  best.ring = true;
+  best.widths = {1};
+  if (nranks > 1) {
+    double best_cost = ftar::model_cost(best, nranks, bytes);
+    std::vector<size_t> cur;
+    std::vector<std::vector<size_t>> cands;
+    ftar::factorizations((size_t)nranks, cur, cands);
+    for (auto& c : cands) {
+      if (c.size() > FTAR_MAX_STAGES) continue;
+      ftar::Topology t;
+      t.widths = c;
+      double cost = ftar::model_cost(t, nranks, bytes);
+      if (cost < best_cost) {
+        best_cost = cost;
+        best = t;
+      }
+    }
+  }
+  ftar::from_topology(best, out);
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out) {
+  ftar_status_t st = ftar_topo_parse(getenv("FT_TOPO"), getenv("FT_LONELY"), nranks, out);
+  if (st == FTAR_SUCCESS) return st;
+  if (getenv("FT_TOPO") && *getenv("FT_TOPO")) return st;  // set but invalid: report it
+  return ftar_topo_choose(nranks, bytes, out);
+}
+
+double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes) {
+  ftar::Topology t;
+  if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -1.0;
+  return ftar::model_cost(t, nranks, bytes);
+}
+
+int ftar_topo_format(const ftar_topo_t* topo, char* buf, size_t buflen) {
+  if (!topo) return -1;
+  ftar::Topology t;
+  std::string s;
+  if (topo->ring) s = "ring";
+  else {
+    for (int i = 0; i < topo->nstages; ++i) s += (i ? "," : "") + std::to_string(topo->stages[i]);
+    if (topo->lonely) s += "+" + std::to_string(topo->lonely);
+  }
+  if (buf && buflen) snprintf(buf, buflen, "%s", s.c_str());
+  return (int)s.size();
+}
+
+ftar_status_t ftar_get_unique_id(ftar_unique_id_t* id) {
+  if (!id) return FTAR_ERR_INVALID_ARG;
+  static_assert(sizeof(ftar_unique_id_t) == sizeof(ncclUniqueId), "unique id size");
+  ncclUniqueId u;
+  ncclResult_t r = ncclGetUniqueId(&u);
+  if (r != ncclSuccess) {
+    ftar::set_error(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r), __FILE__, __LINE__);
+    return FTAR_ERR_RCCL;
+  }
+  memcpy(id, &u, sizeof(u));
+  return FTAR_SUCCESS;
+}
+
+static long emit(const std::string& s, char* buf, size_t buflen) {
+  if (buf && buflen) {
+    size_t m = std::min(s.size(), buflen - 1);
+    memcpy(buf, s.data(), m);
+    buf[m] = 0;
+  }
+  return (long)s.size();
+}
+
+long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, char* buf, size_t buflen) {
+  ftar::Topology t;
+  if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -FTAR_ERR_INVALID_TOPO;
+  std::string s;
+  ftar_status_t st = ftar::schedule_json(t, nranks, rank, count, &s);
+  if (st != FTAR_SUCCESS) return -(long)st;
+  return emit(s, buf, buflen);
+}
+
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, size_t esz, char* buf,
+                    size_t buflen) {
+  (void)esz;
+  ftar::Topology t;
+  if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -FTAR_ERR_INVALID_TOPO;
+  ftar::Plan p;
+  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p);
+  if (st != FTAR_SUCCESS) return -(long)st;
+  return emit(p.json(), buf, buflen);
+}
+
+}  // extern "C"

@@ -1,0 +1,303 @@
+// FlexTree AllReduce engine: runs a rank's plan on two HIP streams.
+//
+// Reference execution (mpi_mod.hpp:1550-1644, :1689-1715): per stage post all
+// Isend/Irecv, MPI_Waitall the receives, reduce on 14 OpenMP threads,
+// MPI_Waitall the sends, MPI_Barrier — no overlap between communication and
+// reduction, a global barrier every stage, host buffers.
+//
+// Here (device-resident, nothing blocks the host):
+//   comm stream : the stage's transfers, cut into pieces of `chunk` elements
+//                 (piece c of every block of the stage = one p2p group);
+//   reduce stream: the reduce kernel for piece c starts as soon as piece c of
+//                 the stage's receives has landed (event), while piece c+1 is
+//                 still on the wire;
+//   cross-stage : piece c of stage s+1's transfers waits only for piece c of
+//                 the latest reducing stage (what it sends, or the scratch it
+//                 overwrites two stages later, depends on nothing else);
+//   scratch     : compact, two halves alternating per stage, grow-only, HBM.
+// The caller's stream is joined at entry and at exit with events, so the call
+// is stream-ordered like any other HIP operation.
+#include <algorithm>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "ftar_internal.h"
+
+struct ftar_comm {
+  int rank = 0, nranks = 1, device = 0;
+  std::unique_ptr<ftar::Transport> tp;
+  hipStream_t comm_s = nullptr, red_s = nullptr;
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  size_t chunk_bytes = 0;
+  bool auto_topo = true;
+  ftar::Topology topo;
+  std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
+  std::vector<hipEvent_t> events;
+  std::mutex mu;
+};
+
+namespace ftar {
+
+namespace {
+constexpr size_t kDefaultChunkBytes = 16u << 20;
+
+ftar_status_t grow_events(ftar_comm* c, size_t n) {
+  while (c->events.size() < n) {
+    hipEvent_t e;
+    FTAR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->events.push_back(e);
+  }
+  return FTAR_SUCCESS;
+}
+}  // namespace
+
+ftar_status_t comm_setup(ftar_comm* c) {
+  FTAR_CHECK_HIP(hipSetDevice(c->device));
+  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
+  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
+  const char* cb = getenv("FTAR_CHUNK_BYTES");
+  c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
+  if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
+  ftar_topo_t t;
+  if (ftar_topo_parse(getenv("FT_TOPO"), getenv("FT_LONELY"), c->nranks, &t) == FTAR_SUCCESS) {
+    c->auto_topo = false;
+    return to_topology(&t, c->nranks, &c->topo);
+  }
+  c->auto_topo = true;
+  return FTAR_SUCCESS;
+}
+
+void comm_teardown(ftar_comm* c) {
+  (void)hipSetDevice(c->device);
+  if (c->comm_s) (void)hipStreamSynchronize(c->comm_s);
+  if (c->red_s) (void)hipStreamSynchronize(c->red_s);
+  c->tp.reset();
+  for (auto e : c->events) (void)hipEventDestroy(e);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->comm_s) (void)hipStreamDestroy(c->comm_s);
+  if (c->red_s) (void)hipStreamDestroy(c->red_s);
+}
+
+ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                        const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream) {
+  if (!c || !recvbuf) return FTAR_ERR_INVALID_ARG;
+  if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
+  const size_t esz = dtype_size(dt);
+  std::lock_guard<std::mutex> g(c->mu);
+  FTAR_CHECK_HIP(hipSetDevice(c->device));
+  if (sendbuf == recvbuf) sendbuf = nullptr;
+  if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
+    if (sendbuf && count) FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, hipMemcpyDeviceToDevice, stream));
+    return FTAR_SUCCESS;
+  }
+  if (count == 0) return FTAR_SUCCESS;
+
+  Topology t;
+  if (topo) {
+    FTAR_RETURN_IF(to_topology(topo, c->nranks, &t));
+  } else if (!c->auto_topo) {
+    t = c->topo;
+  } else {
+    ftar_topo_t ch;
+    FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
+    FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
+  }
+  const std::string key = t.key() + "/" + std::to_string(count);
+  auto it = c->plans.find(key);
+  if (it == c->plans.end()) {
+    auto p = std::make_shared<Plan>();
+    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get()));
+    if (c->plans.size() > 64) c->plans.clear();
+    it = c->plans.emplace(key, p).first;
+  }
+  const Plan& plan = *it->second;
+  if (plan.max_k > FTAR_MAX_K) return FTAR_ERR_UNSUPPORTED;
+
+  const size_t need = 2 * plan.scratch_half * esz;
+  if (need > c->scratch_bytes) {
+    if (c->scratch) {  // work of earlier calls may still read it
+      FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
+      FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
+      FTAR_CHECK_HIP(hipFree(c->scratch));
+      c->scratch = nullptr;
+      c->scratch_bytes = 0;
+    }
+    FTAR_CHECK_HIP(hipMalloc(&c->scratch, need));
+    c->scratch_bytes = need;
+  }
+
+  size_t chunk = std::max<size_t>(1, (c->chunk_bytes / esz) & ~size_t(63));
+  if (chunk == 0) chunk = 64;
+  const size_t nchunks = std::max<size_t>(1, (plan.split + chunk - 1) / chunk);
+  const size_t nst = plan.stages.size();
+  FTAR_RETURN_IF(grow_events(c, 2 * nst * nchunks + 3));
+  hipEvent_t* ev = c->events.data();
+  auto ev_x = [&](size_t s, size_t k) { return ev[3 + (s * nchunks + k) * 2]; };
+  auto ev_r = [&](size_t s, size_t k) { return ev[3 + (s * nchunks + k) * 2 + 1]; };
+
+  char* bufs[3] = {static_cast<char*>(const_cast<void*>(sendbuf ? sendbuf : recvbuf)), static_cast<char*>(recvbuf),
+                   static_cast<char*>(c->scratch)};
+  Transport* tp = c->tp.get();
+
+  FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev[0], 0));
+
+  long last_red = -1;
+  std::vector<const void*> srcs;
+  for (size_t s = 0; s < nst; ++s) {
+    const Stage& st = plan.stages[s];
+    const bool moves = !st.sends.empty() || !st.recvs.empty();
+    for (size_t k = 0; k < nchunks; ++k) {
+      const size_t lo = k * chunk;
+      if (moves) {
+        if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, k), 0));
+        FTAR_RETURN_IF(tp->group_start());
+        for (const Transfer& x : st.sends)
+          if (x.len > lo)
+            FTAR_RETURN_IF(tp->send(bufs[x.buf] + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz, x.peer,
+                                    c->comm_s));
+        for (const Transfer& x : st.recvs)
+          if (x.len > lo)
+            FTAR_RETURN_IF(tp->recv(bufs[x.buf] + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz, x.peer,
+                                    c->comm_s));
+        FTAR_RETURN_IF(tp->group_end());
+      }
+      if (!st.reduces.empty()) {
+        FTAR_CHECK_HIP(hipEventRecord(ev_x(s, k), c->comm_s));
+        FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev_x(s, k), 0));
+        for (const ReduceItem& r : st.reduces) {
+          if (r.len <= lo) continue;
+          srcs.clear();
+          srcs.push_back(bufs[r.own_buf] + (r.off + lo) * esz);
+          for (size_t so : r.scratch_offs) srcs.push_back(bufs[BUF_SCRATCH] + (so + lo) * esz);
+          FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), bufs[BUF_DST] + (r.off + lo) * esz,
+                                       std::min(chunk, r.len - lo), dt, op, c->red_s));
+        }
+        FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
+      }
+    }
+    if (!st.reduces.empty()) last_red = (long)s;
+  }
+  FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[2], c->red_s));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[2], 0));
+  return FTAR_SUCCESS;
+}
+
+}  // namespace ftar
+
+// ============================================================================
+// C ABI: communicators and AllReduce
+// ============================================================================
+extern "C" {
+
+ftar_status_t ftar_comm_init_rank(ftar_comm_t* comm, int nranks, ftar_unique_id_t id, int rank, int device) {
+  if (!comm || nranks <= 0 || rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
+  std::unique_ptr<ftar_comm> c(new ftar_comm);
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  FTAR_CHECK_HIP(hipSetDevice(device));
+  ftar_status_t st = FTAR_SUCCESS;
+  c->tp = ftar::make_rccl_transport(nranks, id, rank, &st);
+  if (st != FTAR_SUCCESS) return st;
+  st = ftar::comm_setup(c.get());
+  if (st != FTAR_SUCCESS) {
+    ftar::comm_teardown(c.get());
+    return st;
+  }
+  *comm = c.release();
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* devices) {
+  if (!comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  auto hub = ftar::make_local_hub(nranks);
+  std::vector<ftar_comm*> made;
+  for (int r = 0; r < nranks; ++r) {
+    auto* c = new ftar_comm;
+    c->rank = r;
+    c->nranks = nranks;
+    c->device = devices ? devices[r] : 0;
+    c->tp = ftar::make_local_transport(hub, r);
+    ftar_status_t st = ftar::comm_setup(c);
+    if (st != FTAR_SUCCESS) {
+      ftar::comm_teardown(c);
+      delete c;
+      for (auto* m : made) {
+        ftar::comm_teardown(m);
+        delete m;
+      }
+      return st;
+    }
+    made.push_back(c);
+  }
+  for (int r = 0; r < nranks; ++r) comms[r] = made[r];
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_destroy(ftar_comm_t comm) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  ftar::comm_teardown(comm);
+  delete comm;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_rank(ftar_comm_t comm, int* rank) {
+  if (!comm || !rank) return FTAR_ERR_INVALID_ARG;
+  *rank = comm->rank;
+  return FTAR_SUCCESS;
+}
+ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size) {
+  if (!comm || !size) return FTAR_ERR_INVALID_ARG;
+  *size = comm->nranks;
+  return FTAR_SUCCESS;
+}
+ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device) {
+  if (!comm || !device) return FTAR_ERR_INVALID_ARG;
+  *device = comm->device;
+  return FTAR_SUCCESS;
+}
+ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : ftar::kDefaultChunkBytes;
+  return FTAR_SUCCESS;
+}
+ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes) {
+  if (!comm || !bytes) return FTAR_ERR_INVALID_ARG;
+  *bytes = comm->chunk_bytes;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                             const ftar_topo_t* topo, ftar_comm_t comm, void* stream) {
+  return ftar::allreduce(sendbuf, recvbuf, count, dtype, op, topo, comm, static_cast<hipStream_t>(stream));
+}
+
+ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
+                                   ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
+                                   int nranks, void* const* streams) {
+  if (!recvbufs || !comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  std::vector<ftar_status_t> st(nranks, FTAR_SUCCESS);
+  std::vector<std::thread> th;
+  for (int r = 0; r < nranks; ++r)
+    th.emplace_back([&, r] {
+      hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;
+      st[r] = ftar::allreduce(sendbufs ? sendbufs[r] : nullptr, recvbufs[r], count, dtype, op, topo, comms[r], s);
+      if (st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
+          hipStreamSynchronize(s) != hipSuccess)
+        st[r] = FTAR_ERR_HIP;
+    });
+  for (auto& t : th) t.join();
+  for (int r = 0; r < nranks; ++r)
+    if (st[r] != FTAR_SUCCESS) return st[r];
+  return FTAR_SUCCESS;
+}
+
+}  // extern "C"

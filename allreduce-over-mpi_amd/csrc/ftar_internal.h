@@ -1,0 +1,111 @@
+// Internal declarations of libftar (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ftar.h"
+
+namespace ftar {
+
+#define FTAR_CHECK_HIP(expr)                                                                   \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) {                                                                    \
+      ::ftar::set_error(std::string(#expr) + ": " + hipGetErrorString(_e), __FILE__, __LINE__); \
+      return FTAR_ERR_HIP;                                                                     \
+    }                                                                                          \
+  } while (0)
+
+#define FTAR_RETURN_IF(st)          \
+  do {                              \
+    ftar_status_t _s = (st);        \
+    if (_s != FTAR_SUCCESS) return _s; \
+  } while (0)
+
+void set_error(const std::string& msg, const char* file, int line);
+const char* last_error();
+
+// ---------------------------------------------------------------------------
+// topology (mpi_mod.hpp:1419-1486)
+// ---------------------------------------------------------------------------
+struct Topology {
+  std::vector<size_t> widths;  // bottom-up stage widths (tree); {1} for ring
+  size_t lonely = 0;
+  bool ring = false;
+  std::string key() const;
+};
+ftar_status_t to_topology(const ftar_topo_t* t, int nranks, Topology* out);
+void from_topology(const Topology& t, ftar_topo_t* out);
+
+// ---------------------------------------------------------------------------
+// schedule (mpi_mod.hpp:80-766) lowered to an executable plan
+// ---------------------------------------------------------------------------
+enum BufId : int { BUF_SRC = 0, BUF_DST = 1, BUF_SCRATCH = 2 };
+
+struct Transfer {
+  int peer;
+  int buf;     // BufId
+  size_t off;  // elements into buf
+  size_t len;  // elements (> 0)
+};
+
+struct ReduceItem {
+  size_t off;                        // element offset of the block in dst (and own)
+  size_t len;                        // elements (> 0)
+  int own_buf;                       // BUF_SRC or BUF_DST
+  std::vector<size_t> scratch_offs;  // peers' partials, in reduction order
+};
+
+struct Stage {
+  std::vector<Transfer> sends, recvs;
+  std::vector<ReduceItem> reduces;
+};
+
+struct Plan {
+  int rank = 0, nranks = 1;
+  size_t count = 0, split = 0;
+  std::vector<Stage> stages;
+  size_t scratch_half = 0;  // elements per scratch half (stages alternate halves)
+  int max_k = 0;
+  std::string json() const;
+};
+
+// FMA-level schedule (for tests/introspection), JSON shaped like the reference dump.
+ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t count, std::string* out);
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out);
+
+// ---------------------------------------------------------------------------
+// reduce kernels (reduce_kernels.hip)
+// ---------------------------------------------------------------------------
+// srcs: host array of k device pointers. k == 1 copies.
+ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                            hipStream_t stream);
+bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op);
+size_t dtype_size(ftar_dtype_t dt);
+
+// ---------------------------------------------------------------------------
+// transports (transport.cpp)
+// ---------------------------------------------------------------------------
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual ftar_status_t group_start() = 0;
+  virtual ftar_status_t send(const void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+  virtual ftar_status_t group_end() = 0;
+  virtual const char* name() const = 0;
+};
+
+std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_t& id, int rank,
+                                               ftar_status_t* st);
+struct LocalHub;
+std::shared_ptr<LocalHub> make_local_hub(int nranks);
+std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank);
+
+}  // namespace ftar

@@ -1,0 +1,377 @@
+// k-way element-wise reduce for gfx950 (MI355X).
+//
+// Replaces FlexTree::reduce_sum<T>/reduce_band<T> (allreduce_over_mpi/mpi_mod.hpp:812-1251)
+// and the reference's never-wired GPU twin reduce_sum_1..20 (vector_add/reduce_sum_gpu.h:4-316).
+//
+//   dst[i] = src0[i] OP src1[i] OP ... OP src{k-1}[i]      strictly left to right
+//
+// Design (bandwidth-bound: (k+1)*n*sizeof(T) bytes, ~0 flops per byte, no MFMA):
+//   * 16 B per lane per access (global_load_dwordx4 / global_store_dwordx4),
+//     one wave instruction = 1 KiB contiguous per source: fully coalesced;
+//   * each lane keeps U vectors of every source in flight before combining
+//     (K*U outstanding 16-B loads per lane) to cover HBM latency at any
+//     occupancy; one-shot grid of ceil(nvec / (256*U)) workgroups (>> 256 CUs);
+//   * source pointers travel in the kernarg segment (no device-side pointer
+//     table, no extra dependent load); K is a template parameter for 2..8;
+//   * unaligned heads/tails (block offsets need not be 16-B aligned) are done
+//     element-wise by workgroup 0 in the same launch; sources whose alignment
+//     differs from dst's take a dword-granular kernel instead;
+//   * arithmetic follows the reference's C++ semantics bit for bit:
+//       float/double in their own precision (no FMA: pure adds),
+//       narrow integers wrap (promotion + truncating store == modular add),
+//       bool sum = OR of non-zero, bf16 (extension) = fp32 accumulate + one RNE.
+#include <hip/hip_runtime.h>
+
+#include "ftar_internal.h"
+
+namespace ftar {
+namespace {
+
+constexpr int kThreads = 256;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+// ---------------------------------------------------------------------------
+// element traits: scalar (S*) and 16-byte vector (V*) forms of one (dtype, op)
+// ---------------------------------------------------------------------------
+struct F32Sum {
+  using S = float;
+  using SA = float;
+  using VA = f32x4;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return a + x; }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return __builtin_bit_cast(f32x4, x); }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a + __builtin_bit_cast(f32x4, x); }
+  __device__ static u32x4 v_fin(VA a) { return __builtin_bit_cast(u32x4, a); }
+};
+struct F64Sum {
+  using S = double;
+  using SA = double;
+  using VA = f64x2;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return a + x; }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return __builtin_bit_cast(f64x2, x); }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a + __builtin_bit_cast(f64x2, x); }
+  __device__ static u32x4 v_fin(VA a) { return __builtin_bit_cast(u32x4, a); }
+};
+struct BF16Sum {
+  using S = unsigned short;
+  using SA = float;
+  struct VA {
+    f32x4 lo, hi;
+  };
+  __device__ static SA s_init(S x) { return bf16_to_f32(x); }
+  __device__ static SA s_comb(SA a, S x) { return a + bf16_to_f32(x); }
+  __device__ static S s_fin(SA a) { return f32_to_bf16(a); }
+  __device__ static f32x4 unpack(unsigned a, unsigned b) {
+    f32x4 r;
+    r.x = __uint_as_float(a << 16);
+    r.y = __uint_as_float(a & 0xffff0000u);
+    r.z = __uint_as_float(b << 16);
+    r.w = __uint_as_float(b & 0xffff0000u);
+    return r;
+  }
+  __device__ static VA v_init(u32x4 x) { return {unpack(x.x, x.y), unpack(x.z, x.w)}; }
+  __device__ static VA v_comb(VA a, u32x4 x) {
+    VA b = v_init(x);
+    return {a.lo + b.lo, a.hi + b.hi};
+  }
+  __device__ static unsigned pack(float lo, float hi) {
+    return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+  }
+  __device__ static u32x4 v_fin(VA a) {
+    return u32x4{pack(a.lo.x, a.lo.y), pack(a.lo.z, a.lo.w), pack(a.hi.x, a.hi.y), pack(a.hi.z, a.hi.w)};
+  }
+};
+// modular integer sums on packed lanes (SWAR for 8/16-bit lanes)
+template <class S_, unsigned HI>
+struct SwarSum {
+  using S = S_;
+  using SA = S_;
+  using VA = u32x4;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return (S)(a + x); }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return x; }
+  __device__ static VA v_comb(VA a, u32x4 b) {
+    const u32x4 lo = (a & ~HI) + (b & ~HI);  // carries stay inside each lane
+    return lo ^ ((a ^ b) & HI);
+  }
+  __device__ static u32x4 v_fin(VA a) { return a; }
+};
+using U8Sum = SwarSum<unsigned char, 0x80808080u>;
+using U16Sum = SwarSum<unsigned short, 0x80008000u>;
+struct U32Sum {
+  using S = unsigned;
+  using SA = unsigned;
+  using VA = u32x4;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return a + x; }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return x; }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a + x; }
+  __device__ static u32x4 v_fin(VA a) { return a; }
+};
+struct U64Sum {
+  using S = unsigned long long;
+  using SA = unsigned long long;
+  using VA = u64x2;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return a + x; }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return __builtin_bit_cast(u64x2, x); }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a + __builtin_bit_cast(u64x2, x); }
+  __device__ static u32x4 v_fin(VA a) { return __builtin_bit_cast(u32x4, a); }
+};
+// bool "sum": the reference adds 0/1 ints and stores sum != 0 -> logical OR
+struct BoolSum {
+  using S = unsigned char;
+  using SA = unsigned char;
+  using VA = u32x4;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return a | x; }
+  __device__ static S s_fin(SA a) { return a != 0; }
+  __device__ static VA v_init(u32x4 x) { return x; }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a | x; }
+  __device__ static u32x4 v_fin(VA a) {
+    const u32x4 nz = ((a & 0x7f7f7f7fu) + 0x7f7f7f7fu) | a;  // bit 7 of each byte = byte != 0
+    return (nz >> 7) & 0x01010101u;
+  }
+};
+template <class S_>
+struct Band {
+  using S = S_;
+  using SA = S_;
+  using VA = u32x4;
+  __device__ static SA s_init(S x) { return x; }
+  __device__ static SA s_comb(SA a, S x) { return (S)(a & x); }
+  __device__ static S s_fin(SA a) { return a; }
+  __device__ static VA v_init(u32x4 x) { return x; }
+  __device__ static VA v_comb(VA a, u32x4 x) { return a & x; }
+  __device__ static u32x4 v_fin(VA a) { return a; }
+};
+
+template <int K>
+struct Srcs {
+  const void* p[K];
+};
+
+// ---------------------------------------------------------------------------
+// vector kernel: K sources (K == 0: runtime k <= FTAR_MAX_K), U vectors per lane.
+// Element range [head, head + nvec*VE) is vectorised; workgroup 0 also does the
+// `head` leading and `tail` trailing elements element-wise.
+// ---------------------------------------------------------------------------
+template <class Tr, int K, int U, bool NT>
+__global__ void __launch_bounds__(kThreads)
+    reduce_vec_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, void* __restrict__ dst, size_t nvec, int head,
+                      int tail) {
+  using S = typename Tr::S;
+  constexpr int KK = K > 0 ? K : FTAR_MAX_K;
+  const int k = K > 0 ? K : kr;
+  constexpr int VE = 16 / sizeof(S);
+  const size_t v0 = (size_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {
+    const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
+    typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
+    for (int j = 1; j < k; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
+    static_cast<S*>(dst)[e] = Tr::s_fin(a);
+  }
+
+  const u32x4* s0 = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[0]) + head);
+  u32x4* d = reinterpret_cast<u32x4*>(static_cast<S*>(dst) + head);
+  if (v0 + (U - 1) * kThreads < nvec) {  // full tile: no per-vector guards
+    typename Tr::VA acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = Tr::v_init(ld16<NT>(s0 + v0 + u * kThreads));
+    if constexpr (K > 0) {
+      u32x4 x[KK > 1 ? KK - 1 : 1][U];
+#pragma unroll
+      for (int j = 1; j < KK; ++j) {
+        const u32x4* sj = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[j - 1][u] = ld16<NT>(sj + v0 + u * kThreads);
+      }
+#pragma unroll
+      for (int j = 1; j < KK; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = Tr::v_comb(acc[u], x[j - 1][u]);
+    } else {
+      for (int j = 1; j < k; ++j) {
+        const u32x4* sj = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head);
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld16<NT>(sj + v0 + u * kThreads);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = Tr::v_comb(acc[u], x[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st16<NT>(d + v0 + u * kThreads, Tr::v_fin(acc[u]));
+  } else {  // last workgroup: guarded
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t v = v0 + u * kThreads;
+      if (v >= nvec) break;
+      typename Tr::VA a = Tr::v_init(ld16<NT>(s0 + v));
+      for (int j = 1; j < k; ++j)
+        a = Tr::v_comb(a, ld16<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head) + v));
+      st16<NT>(d + v, Tr::v_fin(a));
+    }
+  }
+}
+
+// element-wise fallback for sources not co-aligned with dst
+template <class Tr>
+__global__ void __launch_bounds__(kThreads)
+    reduce_elem_kernel(Srcs<FTAR_MAX_K> src, int k, void* __restrict__ dst, size_t n) {
+  using S = typename Tr::S;
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < n; e += stride) {
+    typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
+    for (int j = 1; j < k; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
+    static_cast<S*>(dst)[e] = Tr::s_fin(a);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch
+// ---------------------------------------------------------------------------
+template <int K>
+constexpr int unroll_for() {
+  return K == 2 ? 4 : (K > 0 && K <= 4) ? 2 : 1;
+}
+
+template <class Tr, int K>
+hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
+  constexpr int KK = K > 0 ? K : FTAR_MAX_K;
+  constexpr int U = K > 0 ? unroll_for<K>() : 2;
+  Srcs<KK> a{};
+  for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
+  const size_t per_block = (size_t)U * kThreads;
+  size_t blocks = (nvec + per_block - 1) / per_block;
+  if (blocks == 0) blocks = 1;  // head/tail only
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((reduce_vec_kernel<Tr, K, U, false>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, dst,
+                     nvec, head, tail);
+  return hipGetLastError();
+}
+
+template <class Tr>
+hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hipStream_t s, bool hot) {
+  using S = typename Tr::S;
+  constexpr size_t VE = 16 / sizeof(S);
+  const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
+  bool co_aligned = (mis % sizeof(S)) == 0;
+  for (int j = 0; j < k && co_aligned; ++j) co_aligned = (reinterpret_cast<uintptr_t>(srcs[j]) & 15) == mis;
+  if (!co_aligned) {
+    Srcs<FTAR_MAX_K> a{};
+    for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
+    size_t blocks = (count + kThreads - 1) / kThreads;
+    blocks = blocks > 8192 ? 8192 : blocks;
+    hipLaunchKernelGGL((reduce_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, dst, count);
+    return hipGetLastError();
+  }
+  size_t head = mis ? (16 - mis) / sizeof(S) : 0;
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / VE;
+  const size_t tail = count - head - nvec * VE;
+  if (hot) {
+    switch (k) {
+      case 2: return launch_k<Tr, 2>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 3: return launch_k<Tr, 3>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 4: return launch_k<Tr, 4>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 5: return launch_k<Tr, 5>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 6: return launch_k<Tr, 6>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 7: return launch_k<Tr, 7>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 8: return launch_k<Tr, 8>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      default: break;
+    }
+  } else if (k == 2) {
+    return launch_k<Tr, 2>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+  }
+  return launch_k<Tr, 0>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+}
+
+}  // namespace
+
+size_t dtype_size(ftar_dtype_t dt) {
+  switch (dt) {
+    case FTAR_UINT8: case FTAR_INT8: case FTAR_BOOL: return 1;
+    case FTAR_UINT16: case FTAR_INT16: case FTAR_BFLOAT16: return 2;
+    case FTAR_INT32: case FTAR_FLOAT32: return 4;
+    case FTAR_INT64: case FTAR_FLOAT64: return 8;
+  }
+  return 0;
+}
+
+bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
+  if (dtype_size(dt) == 0) return false;
+  if (op == FTAR_SUM) return true;
+  if (op == FTAR_BAND)  // mpi_mod.hpp:1389-1396: integer types only
+    return dt == FTAR_UINT8 || dt == FTAR_INT8 || dt == FTAR_UINT16 || dt == FTAR_INT16 || dt == FTAR_INT32 ||
+           dt == FTAR_INT64;
+  return false;
+}
+
+ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                            hipStream_t s) {
+  if (k < 1 || k > FTAR_MAX_K || !srcs || !dst) return FTAR_ERR_INVALID_ARG;
+  if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
+  if (count == 0) return FTAR_SUCCESS;
+  for (int j = 0; j < k; ++j)
+    if (!srcs[j]) return FTAR_ERR_INVALID_ARG;
+  if (k == 1) {  // vector_add/reduce_sum.h:36-47: a copy
+    if (srcs[0] != dst) FTAR_CHECK_HIP(hipMemcpyAsync(dst, srcs[0], count * dtype_size(dt), hipMemcpyDeviceToDevice, s));
+    return FTAR_SUCCESS;
+  }
+  hipError_t e = hipErrorInvalidValue;
+  if (op == FTAR_SUM) {
+    switch (dt) {
+      case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, true); break;
+      case FTAR_BFLOAT16: e = launch_tr<BF16Sum>(srcs, k, dst, count, s, true); break;
+      case FTAR_FLOAT64: e = launch_tr<F64Sum>(srcs, k, dst, count, s, false); break;
+      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum>(srcs, k, dst, count, s, false); break;
+      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<U16Sum>(srcs, k, dst, count, s, false); break;
+      case FTAR_INT32: e = launch_tr<U32Sum>(srcs, k, dst, count, s, false); break;
+      case FTAR_INT64: e = launch_tr<U64Sum>(srcs, k, dst, count, s, false); break;
+      case FTAR_BOOL: e = launch_tr<BoolSum>(srcs, k, dst, count, s, false); break;
+    }
+  } else {
+    switch (dt) {
+      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<Band<unsigned char>>(srcs, k, dst, count, s, false); break;
+      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<Band<unsigned short>>(srcs, k, dst, count, s, false); break;
+      case FTAR_INT32: e = launch_tr<Band<unsigned>>(srcs, k, dst, count, s, false); break;
+      case FTAR_INT64: e = launch_tr<Band<unsigned long long>>(srcs, k, dst, count, s, false); break;
+      default: return FTAR_ERR_UNSUPPORTED;
+    }
+  }
+  FTAR_CHECK_HIP(e);
+  return FTAR_SUCCESS;
+}
+
+}  // namespace ftar

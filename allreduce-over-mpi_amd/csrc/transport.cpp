@@ -1,0 +1,238 @@
+// Transports of the FlexTree engine: point-to-point, stream-ordered byte moves.
+//
+// The reference moves every block with MPI_Isend/MPI_Irecv, tag 0, matched in
+// posting order per peer pair, and then blocks in MPI_Waitall + MPI_Barrier
+// (mpi_mod.hpp:1254-1305, :1576-1595, :1696-1712).  Here a stage's moves are
+// one group of non-blocking, stream-ordered p2p operations; completion is a
+// stream event, never a host wait or a barrier.
+//
+//   RcclTransport   one process per GPU: ncclSend/ncclRecv inside
+//                   ncclGroupStart/End over xGMI (the product path).
+//   LocalTransport  N ranks inside one process (one host thread per rank):
+//                   the receiver enqueues a device copy from the sender's
+//                   buffer on its own stream, ordered after the sender's
+//                   "ready" event; the sender's stream then waits for the
+//                   receiver's "copied" event.  Same per-pair FIFO matching,
+//                   same stream semantics as RCCL p2p, so the engine code
+//                   above it is identical; used to run multi-rank schedules
+//                   on a single GPU (tests) and in single-process groups.
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <mutex>
+
+#include "ftar_internal.h"
+
+namespace ftar {
+
+// ---------------------------------------------------------------------------
+// RCCL
+// ---------------------------------------------------------------------------
+namespace {
+
+#define FTAR_CHECK_NCCL(expr)                                                                       \
+  do {                                                                                              \
+    ncclResult_t _r = (expr);                                                                       \
+    if (_r != ncclSuccess) {                                                                        \
+      ::ftar::set_error(std::string(#expr) + ": " + ncclGetErrorString(_r), __FILE__, __LINE__);    \
+      return FTAR_ERR_RCCL;                                                                         \
+    }                                                                                               \
+  } while (0)
+
+class RcclTransport final : public Transport {
+ public:
+  explicit RcclTransport(ncclComm_t c) : comm_(c) {}
+  ~RcclTransport() override {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  ftar_status_t group_start() override {
+    FTAR_CHECK_NCCL(ncclGroupStart());
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    FTAR_CHECK_NCCL(ncclSend(buf, bytes, ncclUint8, peer, comm_, s));
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    FTAR_CHECK_NCCL(ncclRecv(buf, bytes, ncclUint8, peer, comm_, s));
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t group_end() override {
+    FTAR_CHECK_NCCL(ncclGroupEnd());
+    return FTAR_SUCCESS;
+  }
+  const char* name() const override { return "rccl"; }
+
+ private:
+  ncclComm_t comm_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_t& id, int rank, ftar_status_t* st) {
+  static_assert(sizeof(ftar_unique_id_t) == sizeof(ncclUniqueId), "unique id size");
+  ncclUniqueId uid;
+  memcpy(&uid, &id, sizeof(uid));
+  ncclComm_t c = nullptr;
+  ncclResult_t r = ncclCommInitRank(&c, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r), __FILE__, __LINE__);
+    *st = FTAR_ERR_RCCL;
+    return nullptr;
+  }
+  *st = FTAR_SUCCESS;
+  return std::unique_ptr<Transport>(new RcclTransport(c));
+}
+
+// ---------------------------------------------------------------------------
+// in-process ranks
+// ---------------------------------------------------------------------------
+struct LocalHub {
+  struct Posted {
+    const void* buf;
+    size_t bytes;
+    hipEvent_t ready = nullptr;  // sender-side data ready
+    hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
+    bool taken = false;
+    ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
+      if (ready) (void)hipEventDestroy(ready);
+      if (done) (void)hipEventDestroy(done);
+    }
+  };
+  explicit LocalHub(int n) : nranks(n) {}
+  int nranks;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::map<std::pair<int, int>, std::deque<std::shared_ptr<Posted>>> wire;  // (from, to)
+};
+
+std::shared_ptr<LocalHub> make_local_hub(int nranks) { return std::make_shared<LocalHub>(nranks); }
+
+namespace {
+
+class LocalTransport final : public Transport {
+  struct Op {
+    bool is_send;
+    void* buf;
+    size_t bytes;
+    int peer;
+    hipStream_t s;
+  };
+
+ public:
+  LocalTransport(std::shared_ptr<LocalHub> h, int rank) : hub_(std::move(h)), rank_(rank) {}
+  ftar_status_t group_start() override {
+    ++depth_;
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    ops_.push_back({true, const_cast<void*>(buf), bytes, peer, s});
+    return depth_ ? FTAR_SUCCESS : flush();
+  }
+  ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    ops_.push_back({false, buf, bytes, peer, s});
+    return depth_ ? FTAR_SUCCESS : flush();
+  }
+  ftar_status_t group_end() override {
+    if (depth_ <= 0) return FTAR_ERR_INVALID_ARG;
+    if (--depth_ == 0) return flush();
+    return FTAR_SUCCESS;
+  }
+  const char* name() const override { return "local"; }
+
+ private:
+  static ftar_status_t event(hipEvent_t* e) {
+    FTAR_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return FTAR_SUCCESS;
+  }
+
+  ftar_status_t flush() {
+    std::vector<Op> ops;
+    ops.swap(ops_);
+    // 1. publish every send, with an event marking its data ready on the sender's stream
+    std::vector<std::shared_ptr<LocalHub::Posted>> mine;
+    for (auto& o : ops) {
+      if (!o.is_send) continue;
+      if (o.peer == rank_ || o.peer < 0 || o.peer >= hub_->nranks) return FTAR_ERR_INVALID_ARG;
+      auto p = std::make_shared<LocalHub::Posted>();
+      p->buf = o.buf;
+      p->bytes = o.bytes;
+      p->ready = nullptr;
+      FTAR_RETURN_IF(event(&p->ready));
+      FTAR_CHECK_HIP(hipEventRecord(p->ready, o.s));
+      mine.push_back(p);
+      std::lock_guard<std::mutex> g(hub_->mu);
+      hub_->wire[{rank_, o.peer}].push_back(p);
+    }
+    hub_->cv.notify_all();
+    // 2. complete every receive in posting order (per-pair FIFO, like MPI/RCCL)
+    for (auto& o : ops) {
+      if (o.is_send) continue;
+      std::shared_ptr<LocalHub::Posted> p;
+      {
+        std::unique_lock<std::mutex> g(hub_->mu);
+        auto& q = hub_->wire[{o.peer, rank_}];
+        if (!hub_->cv.wait_for(g, std::chrono::seconds(120), [&] { return !q.empty(); })) {
+          set_error("local transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
+          return FTAR_ERR_TIMEOUT;
+        }
+        p = q.front();
+        q.pop_front();
+      }
+      if (p->bytes != o.bytes) {
+        set_error("local transport: message size mismatch", __FILE__, __LINE__);
+        return FTAR_ERR_INTERNAL;
+      }
+      FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
+      if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
+      hipEvent_t done = nullptr;
+      FTAR_RETURN_IF(event(&done));
+      if (hipEventRecord(done, o.s) != hipSuccess) {
+        (void)hipEventDestroy(done);
+        set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
+        return FTAR_ERR_HIP;
+      }
+      {
+        std::lock_guard<std::mutex> g(hub_->mu);
+        p->done = done;
+        p->taken = true;
+      }
+      hub_->cv.notify_all();
+    }
+    // 3. the sender's stream may not move on (and overwrite the source) before the copy
+    size_t i = 0;
+    for (auto& o : ops) {
+      if (!o.is_send) continue;
+      auto& p = mine[i++];
+      hipEvent_t done;
+      {
+        std::unique_lock<std::mutex> g(hub_->mu);
+        if (!hub_->cv.wait_for(g, std::chrono::seconds(120), [&] { return p->taken; })) {
+          set_error("local transport: send to rank " + std::to_string(o.peer) + " never received", __FILE__,
+                    __LINE__);
+          return FTAR_ERR_TIMEOUT;
+        }
+        done = p->done;
+      }
+      FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, done, 0));
+    }
+    return FTAR_SUCCESS;
+  }
+
+  std::shared_ptr<LocalHub> hub_;
+  int rank_;
+  int depth_ = 0;
+  std::vector<Op> ops_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank) {
+  return std::unique_ptr<Transport>(new LocalTransport(std::move(hub), rank));
+}
+
+}  // namespace ftar

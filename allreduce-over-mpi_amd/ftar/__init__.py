@@ -1,0 +1,327 @@
+"""ftar — Python host binding of libftar.so (the MI355X FlexTree AllReduce).
+
+A thin ctypes layer over the C ABI in include/ftar.h.  It mirrors the
+reference's call surface (allreduce_over_mpi/mpi_mod.hpp:1723-1778):
+
+    MPI_Allreduce_FT(sendbuf, recvbuf, count, datatype, op, comm)
+        -> ftar.allreduce(sendbuf, recvbuf, count, dtype, op, comm, stream=...)
+
+with MPI_IN_PLACE == `sendbuf=None`, MPI datatypes/ops mapped to DTYPE/OP,
+and FT_TOPO / FT_LONELY read from the environment exactly like get_stages
+(mpi_mod.hpp:1419-1486) — or passed explicitly as `topo="2,4"`, `lonely=1`.
+
+Buffers are device pointers (ints) or objects with `data_ptr()` (torch
+tensors).  There is no CPU fallback: if libftar.so is missing this module
+raises at import time.
+"""
+import ctypes
+import json
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FTAR_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libftar.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libftar.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                      "or `make -C allreduce-over-mpi_amd/csrc`")
+
+_lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+
+# ---- enums (include/ftar.h) -------------------------------------------------
+DTYPE = {"u8": 0, "i8": 1, "u16": 2, "i16": 3, "i32": 4, "i64": 5, "f32": 6, "f64": 7, "bool": 8, "bf16": 9}
+# MPI names used by the reference (mpi_mod.hpp:1365-1375)
+MPI_DTYPE = {"MPI_UINT8_T": 0, "MPI_INT8_T": 1, "MPI_UINT16_T": 2, "MPI_INT16_T": 3, "MPI_INT32_T": 4,
+             "MPI_INT64_T": 5, "MPI_LONG_LONG": 5, "MPI_LONG_LONG_INT": 5, "MPI_FLOAT": 6, "MPI_DOUBLE": 7,
+             "MPI_C_BOOL": 8}
+OP = {"sum": 0, "band": 1, "MPI_SUM": 0, "MPI_BAND": 1}
+STATUS = {0: "success", 1: "invalid argument", 2: "unsupported dtype/op", 3: "invalid FT_TOPO/FT_LONELY",
+          4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout"}
+MAX_STAGES = 16
+_TORCH_DTYPE_NAMES = {"torch.float32": "f32", "torch.float64": "f64", "torch.bfloat16": "bf16", "torch.int32": "i32",
+                      "torch.int64": "i64", "torch.int16": "i16", "torch.int8": "i8", "torch.uint8": "u8",
+                      "torch.bool": "bool", "torch.uint16": "u16"}
+
+
+class FtarError(RuntimeError):
+    def __init__(self, status, what=""):
+        detail = _lib.ftar_last_error().decode()
+        super().__init__(f"{what}: {STATUS.get(status, status)}" + (f" ({detail})" if detail else ""))
+        self.status = status
+
+
+class Topo(ctypes.Structure):
+    _fields_ = [("nstages", ctypes.c_int), ("stages", ctypes.c_int * MAX_STAGES), ("lonely", ctypes.c_int),
+                ("ring", ctypes.c_int)]
+
+    def __str__(self):
+        buf = ctypes.create_string_buffer(128)
+        _lib.ftar_topo_format(ctypes.byref(self), buf, 128)
+        return buf.value.decode()
+
+    @property
+    def widths(self):
+        return [self.stages[i] for i in range(self.nstages)]
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+_vp, _sz, _int = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+_lib.ftar_version.restype = ctypes.c_char_p
+_lib.ftar_status_string.restype = ctypes.c_char_p
+_lib.ftar_last_error.restype = ctypes.c_char_p
+_lib.ftar_dtype_size.restype = _sz
+_lib.ftar_dtype_size.argtypes = [_int]
+_lib.ftar_reduce.argtypes = [ctypes.POINTER(_vp), _int, _vp, _sz, _int, _int, _vp]
+_lib.ftar_topo_parse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, _int, ctypes.POINTER(Topo)]
+_lib.ftar_topo_from_env.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
+_lib.ftar_topo_choose.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
+_lib.ftar_topo_cost.argtypes = [ctypes.POINTER(Topo), _int, _sz]
+_lib.ftar_topo_cost.restype = ctypes.c_double
+_lib.ftar_topo_format.argtypes = [ctypes.POINTER(Topo), ctypes.c_char_p, _sz]
+_lib.ftar_get_unique_id.argtypes = [ctypes.POINTER(UniqueId)]
+_lib.ftar_comm_init_rank.argtypes = [ctypes.POINTER(_vp), _int, UniqueId, _int, _int]
+_lib.ftar_comm_init_local.argtypes = [ctypes.POINTER(_vp), _int, ctypes.POINTER(_int)]
+_lib.ftar_comm_destroy.argtypes = [_vp]
+_lib.ftar_comm_set_chunk_bytes.argtypes = [_vp, _sz]
+_lib.ftar_comm_get_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
+_lib.ftar_allreduce.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(Topo), _vp, _vp]
+_lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int, ctypes.POINTER(Topo),
+                                      ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
+_lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
+_lib.ftar_schedule_json.restype = ctypes.c_long
+_lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _sz, ctypes.c_char_p, _sz]
+_lib.ftar_plan_json.restype = ctypes.c_long
+
+
+def lib():
+    return _lib
+
+
+def version():
+    return _lib.ftar_version().decode()
+
+
+def _check(st, what):
+    if st != 0:
+        raise FtarError(st, what)
+
+
+def _dt(dtype):
+    if isinstance(dtype, int):
+        return dtype
+    s = str(dtype)
+    if s in DTYPE:
+        return DTYPE[s]
+    if s in MPI_DTYPE:
+        return MPI_DTYPE[s]
+    if s in _TORCH_DTYPE_NAMES:
+        return DTYPE[_TORCH_DTYPE_NAMES[s]]
+    raise ValueError(f"unknown dtype {dtype!r}")
+
+
+def _op(op):
+    return op if isinstance(op, int) else OP[op]
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(f"not a device pointer: {type(x)}")
+
+
+def _stream(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return s
+    if hasattr(s, "cuda_stream"):
+        return s.cuda_stream
+    raise TypeError(f"not a stream: {type(s)}")
+
+
+def dtype_size(dtype):
+    return _lib.ftar_dtype_size(_dt(dtype))
+
+
+# ---- L3: one-device reduce ----------------------------------------------------
+def reduce(srcs, dst, count, dtype="f32", op="sum", stream=None):
+    """dst[i] = srcs[0][i] op srcs[1][i] op ... (left to right), enqueued on `stream`."""
+    arr = (_vp * len(srcs))(*[_ptr(s) for s in srcs])
+    _check(_lib.ftar_reduce(arr, len(srcs), _ptr(dst), count, _dt(dtype), _op(op), _stream(stream)), "ftar_reduce")
+
+
+# ---- topology -------------------------------------------------------------------
+def topo(spec=None, lonely=0, nranks=None):
+    """Topo from "2,4" / [2,4] / "ring" (+ lonely count), validated for nranks if given."""
+    if isinstance(spec, Topo):
+        return spec
+    if spec in ("ring", 1, "1"):
+        spec = "1"
+    if isinstance(spec, (list, tuple)):
+        spec = ",".join(str(x) for x in spec)
+    if nranks is None:
+        t = Topo()
+        ws = [int(x) for x in str(spec).split(",") if x.strip()]
+        if 1 in ws:
+            t.nstages, t.stages[0], t.ring = 1, 1, 1
+            return t
+        t.nstages = len(ws)
+        for i, w in enumerate(ws):
+            t.stages[i] = w
+        t.lonely = int(lonely)
+        return t
+    t = Topo()
+    _check(_lib.ftar_topo_parse(str(spec).encode(), str(lonely).encode(), nranks, ctypes.byref(t)), f"topo {spec}+{lonely}")
+    return t
+
+
+def topo_parse(ft_topo, ft_lonely, nranks):
+    t = Topo()
+    st = _lib.ftar_topo_parse(None if ft_topo is None else ft_topo.encode(),
+                              None if ft_lonely is None else str(ft_lonely).encode(), nranks, ctypes.byref(t))
+    _check(st, "ftar_topo_parse")
+    return t
+
+
+def topo_from_env(nranks, nbytes):
+    t = Topo()
+    _check(_lib.ftar_topo_from_env(nranks, nbytes, ctypes.byref(t)), "ftar_topo_from_env")
+    return t
+
+
+def topo_choose(nranks, nbytes):
+    t = Topo()
+    _check(_lib.ftar_topo_choose(nranks, nbytes, ctypes.byref(t)), "ftar_topo_choose")
+    return t
+
+
+def topo_cost(t, nranks, nbytes):
+    return _lib.ftar_topo_cost(ctypes.byref(topo(t)), nranks, nbytes)
+
+
+def schedule_json(t, nranks, rank, count):
+    t = topo(t)
+    n = _lib.ftar_schedule_json(ctypes.byref(t), nranks, rank, count, None, 0)
+    if n < 0:
+        raise FtarError(-n, "ftar_schedule_json")
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib.ftar_schedule_json(ctypes.byref(t), nranks, rank, count, buf, n + 1)
+    return json.loads(buf.value.decode())
+
+
+def plan_json(t, nranks, rank, count, esz=4):
+    t = topo(t)
+    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, esz, None, 0)
+    if n < 0:
+        raise FtarError(-n, "ftar_plan_json")
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, esz, buf, n + 1)
+    return json.loads(buf.value.decode())
+
+
+# ---- communicators -------------------------------------------------------------
+def get_unique_id():
+    u = UniqueId()
+    _check(_lib.ftar_get_unique_id(ctypes.byref(u)), "ftar_get_unique_id")
+    return ctypes.string_at(ctypes.addressof(u), 128)
+
+
+class Comm:
+    """One rank's communicator (RCCL over xGMI, or a rank of a local group)."""
+
+    def __init__(self, handle, rank, nranks, device, group=None):
+        self.handle, self.rank, self.nranks, self.device, self._group = handle, rank, nranks, device, group
+
+    @classmethod
+    def init_rank(cls, nranks, unique_id, rank, device):
+        u = UniqueId()
+        ctypes.memmove(ctypes.addressof(u), unique_id, 128)
+        h = _vp()
+        _check(_lib.ftar_comm_init_rank(ctypes.byref(h), nranks, u, rank, device), "ftar_comm_init_rank")
+        return cls(h.value, rank, nranks, device)
+
+    @classmethod
+    def init_local(cls, nranks, devices=None):
+        hs = (_vp * nranks)()
+        devs = (_int * nranks)(*(devices or [0] * nranks))
+        _check(_lib.ftar_comm_init_local(hs, nranks, devs), "ftar_comm_init_local")
+        comms = [cls(hs[r], r, nranks, devs[r]) for r in range(nranks)]
+        group = LocalGroup(comms)
+        for c in comms:
+            c._group = group
+        return group
+
+    @property
+    def chunk_bytes(self):
+        v = _sz()
+        _check(_lib.ftar_comm_get_chunk_bytes(self.handle, ctypes.byref(v)), "chunk_bytes")
+        return v.value
+
+    @chunk_bytes.setter
+    def chunk_bytes(self, b):
+        _check(_lib.ftar_comm_set_chunk_bytes(self.handle, b), "chunk_bytes")
+
+    def allreduce(self, sendbuf, recvbuf, count, dtype="f32", op="sum", topo_=None, lonely=0, stream=None):
+        t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
+        st = _lib.ftar_allreduce(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), t, self.handle,
+                                 _stream(stream))
+        _check(st, "ftar_allreduce")
+
+    def destroy(self):
+        if self.handle:
+            _check(_lib.ftar_comm_destroy(self.handle), "ftar_comm_destroy")
+            self.handle = None
+
+
+class LocalGroup:
+    """All ranks of an in-process group (ftar_comm_init_local)."""
+
+    def __init__(self, comms):
+        self.comms = comms
+
+    def __len__(self):
+        return len(self.comms)
+
+    def __getitem__(self, i):
+        return self.comms[i]
+
+    def set_chunk_bytes(self, b):
+        for c in self.comms:
+            c.chunk_bytes = b
+
+    def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None):
+        P = len(self.comms)
+        t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
+        sb = None if sendbufs is None else (_vp * P)(*[_ptr(x) for x in sendbufs])
+        rb = (_vp * P)(*[_ptr(x) for x in recvbufs])
+        hs = (_vp * P)(*[c.handle for c in self.comms])
+        ss = None if streams is None else (_vp * P)(*[_stream(s) for s in streams])
+        st = _lib.ftar_allreduce_group(sb, rb, count, _dt(dtype), _op(op), t, hs, P, ss)
+        _check(st, "ftar_allreduce_group")
+
+    def destroy(self):
+        for c in self.comms:
+            c.destroy()
+
+
+# ---- the reference's call surface ---------------------------------------------
+MPI_IN_PLACE = None
+
+
+def MPI_Allreduce_FT(sendbuf, recvbuf, count, datatype, op, comm, stream=None):
+    """Drop-in for MPI_Allreduce_FT (mpi_mod.hpp:1724) on device buffers.
+
+    sendbuf=MPI_IN_PLACE (None) reduces recvbuf in place; datatype/op accept the
+    reference's MPI names ("MPI_FLOAT", "MPI_SUM"); the topology comes from
+    FT_TOPO/FT_LONELY at communicator creation (or the cost model).  Returns 0
+    like the reference; raises FtarError where the reference would exit(1).
+    """
+    comm.allreduce(sendbuf, recvbuf, count, datatype, op, stream=stream)
+    return 0

@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Benchmark of the FlexTree AllReduce hot path on MI355X (BASELINE.json metric).
+
+  N = 1  (default) : the per-chunk k-way reduce-sum kernel alone, fp32,
+                     k sources of 2^26 elements (256 MiB each) -> dst
+                     (BASELINE configs[1]; the reference's vector_add.cu
+                     harness, vector_add/vector_add.cu:49-170).
+                     value = algorithmic HBM bytes (k+1)*n*4 per second.
+  N > 1 (torchrun) : one process per GPU, RCCL p2p over xGMI, device-resident
+                     fp32 bucket AllReduce (configs[2..3]; the reference's
+                     benchmark.cpp harness, benchmark.cpp:155-167), default
+                     2^28 elements (1 GiB) per rank, topology FT_TOPO/FT_LONELY
+                     or the re-fitted cost model.
+                     value = N * bucket bytes / t (aggregate algorithmic bandwidth).
+
+Prints ONE JSON line on rank 0.  Inputs are synthetic (splitmix64 fp32 in
+[-1, 1) at N=1, torch.rand at N>1) and resident in HBM before timing starts.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "allreduce-over-mpi_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+XGMI_LINK_GBPS = 76.8           # one xGMI link, one direction (153.6 GB/s bidirectional)
+XGMI_LINKS = 7
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--k", type=int, default=2, help="N=1: number of source buckets")
+    ap.add_argument("--n", type=int, default=0, help="elements per bucket (default 2^26 at N=1, 2^28 at N>1)")
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--topo", default=None, help="N>1: FT_TOPO string (default: env FT_TOPO, else cost model)")
+    ap.add_argument("--lonely", type=int, default=0)
+    ap.add_argument("--chunk-bytes", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
+    return ap.parse_args()
+
+
+def pmc_traffic(workload):
+    """Per-launch HBM bytes measured with rocprofv3 --pmc (profiles/pmc_summary.json), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get(workload, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(k, n, seconds):
+    """The reference's reduce_sum<float> (mpi_mod.hpp:812, 14 OpenMP threads) on this host,
+    built from the unmodified header into oracle/_ref/ref_golden; else the oracle port."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
+    ncpu = os.cpu_count() or 1
+    if os.path.exists(ref):
+        try:
+            out = subprocess.run([ref, "bench", "--k", str(k), "--n", str(n), "--seconds", str(seconds)],
+                                 capture_output=True, text=True, timeout=seconds * 6 + 120, check=True).stdout
+            d = json.loads(out.strip().splitlines()[-1])
+            return {"value": round(d["GBps_best"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+                    "sample": f"FlexTree::reduce_sum<float> k={k} n={n} fp32, best of {d['iters']} calls in ~{seconds:.0f}s "
+                              f"(mean {d['GBps_mean']:.2f} GB/s), host nproc={ncpu}"}
+        except Exception as e:  # fall through to the port
+            sys.stderr.write(f"reference cpu baseline failed: {e}\n")
+    import numpy as np
+    import oracle_lib
+    from ftar import inputs as fi
+    m = min(n, 1 << 24)
+    xs = [fi.fill("f32", 0x5EED, j, m) for j in range(k)]
+    out = np.empty(m, np.float32)
+    best, iters, t_end = 1e30, 0, time.time() + seconds
+    while time.time() < t_end or iters == 0:
+        t0 = time.perf_counter()
+        oracle_lib.reduce(6, 0, xs, out=out)
+        best = min(best, time.perf_counter() - t0)
+        iters += 1
+    return {"value": round((k + 1) * m * 4 / best / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle reduce k={k} n={m} fp32 single thread, best of {iters}, host nproc={ncpu}"}
+
+
+def bench_single(a):
+    import numpy as np
+    import torch
+
+    import ftar
+    from ftar import inputs as fi
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    k, n = a.k, a.n or (1 << 26)
+    esz = ftar.dtype_size(a.dtype)
+    srcs = []
+    for j in range(k):
+        x = fi.fill(a.dtype, 0x5EED, j, n)
+        srcs.append(torch.from_numpy(x.view(np.uint8)).to(dev))
+    dst = torch.empty(n * esz, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream()
+    ptrs = [s.data_ptr() for s in srcs]
+
+    def step():
+        ftar.reduce(ptrs, dst.data_ptr(), n, a.dtype, "sum", stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(a.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / a.steps          # one kernel per step, same stream
+    algo_bytes = (k + 1) * n * esz
+    gbps = algo_bytes / (ms * 1e-3) / 1e9
+
+    # spot check against the oracle (first and last 64 Ki elements)
+    check = "skipped"
+    if a.dtype == "f32":
+        import oracle_lib
+        m = 1 << 16
+        host = [fi.fill("f32", 0x5EED, j, n) for j in range(k)]
+        got = dst.view(torch.float32).cpu().numpy()
+        ok = True
+        for sl in (slice(0, m), slice(n - m, n)):
+            exp = oracle_lib.reduce(6, 0, [h[sl] for h in host])
+            ok &= bool(np.array_equal(got[sl].view(np.uint32), exp.view(np.uint32)))
+        check = "bit-exact" if ok else "MISMATCH"
+
+    workload = f"reduce_k{k}_{a.dtype}_n{n}"
+    res = {
+        "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
+        "value": round(gbps, 2), "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(ms, 5), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": a.dtype, "data": "synthetic (splitmix64 uniform [-1,1), HBM-resident)",
+        "config": {"workload": "1xMI355X local k-way reduce-sum kernel (BASELINE configs[1])", "k": k,
+                   "elements_per_bucket": n, "bucket_bytes": n * esz, "algorithmic_bytes_per_step": algo_bytes},
+        "roofline": {"bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(workload)},
+        "check": check, "wall_s": round(wall, 4),
+    }
+    if a.sweep:
+        sweep = {}
+        for kk in range(1, 17):
+            extra = [torch.empty_like(srcs[0]).copy_(srcs[j % k]) for j in range(kk)]
+            pp = [e.data_ptr() for e in extra]
+            ftar.reduce(pp, dst.data_ptr(), n, a.dtype, "sum", stream=stream)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(5):
+                ftar.reduce(pp, dst.data_ptr(), n, a.dtype, "sum", stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) / 5
+            sweep[kk] = {"ms": round(t, 4), "GBps": round((kk + 1) * n * esz / (t * 1e-3) / 1e9, 1)}
+            del extra
+        res["k_sweep"] = sweep
+    if not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(k, n, a.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+def bench_distributed(a):
+    import torch
+    import torch.distributed as dist
+
+    import ftar
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    uid = [ftar.get_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = ftar.Comm.init_rank(world, uid[0], rank, local)
+    if a.chunk_bytes:
+        comm.chunk_bytes = a.chunk_bytes
+    n = a.n or (1 << 28)
+    esz = ftar.dtype_size(a.dtype)
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    x = (torch.rand(n, generator=gen, device=dev, dtype=torch.float32) * 2 - 1).to(tdt)
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+    if a.topo:
+        topo = ftar.topo(a.topo, a.lonely, nranks=world)
+    else:
+        topo = ftar.topo_from_env(world, n * esz)
+
+    def step():
+        comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    tmax = torch.tensor([t1 - t0], dtype=torch.float64)
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    ms = tmax.item() / a.steps * 1e3
+
+    # correctness: identical on every rank, and within (P-1) * 2^-24 * sum|x| of the fp64 sum on a sample
+    idx = torch.linspace(0, n - 1, 4096, device=dev).long()
+    mine = y[idx].float().cpu()
+    xs = x[idx].float().cpu()
+    allx = [torch.empty_like(xs) for _ in range(world)]
+    ally = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allx, xs)
+    dist.all_gather(ally, mine)
+    ref64 = sum(t.double() for t in allx)
+    absum = sum(t.double().abs() for t in allx)
+    eps = 2.0 ** -24 if a.dtype == "f32" else 2.0 ** -8
+    tol = (world - 1) * eps * absum + 1e-30
+    ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
+
+    bucket = n * esz
+    algbw = bucket / (ms * 1e-3) / 1e9
+    busbw = algbw * 2 * (world - 1) / world
+    links = 1 if topo.ring else min(XGMI_LINKS, world - 1)
+    peak = links * XGMI_LINK_GBPS
+    if rank == 0:
+        res = {
+            "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
+            "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
+            "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
+                       "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo),
+                       "chunk_bytes": comm.chunk_bytes, "parallelism": f"dp{world}"},
+            "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
+            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
+                         "frac": round(busbw / peak, 4), "traffic": None,
+                         "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
+            "check": "ok" if ok else "MISMATCH",
+        }
+        print(json.dumps(res), flush=True)
+    comm.destroy()
+    dist.destroy_process_group()
+
+
+def main():
+    a = parse()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        bench_distributed(a)
+    else:
+        bench_single(a)
+
+
+if __name__ == "__main__":
+    main()

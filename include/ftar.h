@@ -1,0 +1,157 @@
+/*
+ * ftar.h — C ABI of the MI355X-native FlexTree AllReduce (libftar.so).
+ *
+ * Plain pointers, sizes and enums only: no torch, no C++ types.  Every entry
+ * point returns an ftar_status_t instead of exit()ing like the reference.
+ * Device buffers are HBM pointers on the communicator's device; streams are
+ * hipStream_t passed as void* so this header needs no HIP include.
+ *
+ * What each entry point replaces in the reference (DictXiong/AllReduce-Over-MPI):
+ *
+ *   ftar_reduce            FlexTree::reduce_sum<T> / reduce_band<T>
+ *                            allreduce_over_mpi/mpi_mod.hpp:812-1031, :1034-1251
+ *                          reduce_sum_gpu<T> + reduce_sum_1..20 kernels
+ *                            vector_add/reduce_sum_gpu.h:4-316
+ *   ftar_topo_parse        FlexTree::get_stages (FT_TOPO / FT_LONELY)
+ *                            allreduce_over_mpi/mpi_mod.hpp:1419-1486
+ *   ftar_topo_choose       cost_model getWidth + CostModel (argmin width list)
+ *                            cost_model/GetWidth.h:42-47, cost_model/CostModel.h:82-120
+ *   ftar_comm_init_rank    the MPI communicator the reference runs on (MPI_Comm_size/
+ *                            rank, mpi_mod.hpp:781-809); transport = RCCL p2p
+ *   ftar_allreduce         MPI_Allreduce_FT / static MPI_Allreduce
+ *                            allreduce_over_mpi/mpi_mod.hpp:1723-1778
+ *                          (ring_allreduce :1673-1719, tree_allreduce :1510-1671)
+ *   ftar_schedule_json     Send/Recv_Operations + FMA_Send/Recv_Operations
+ *                            allreduce_over_mpi/mpi_mod.hpp:258-766 (introspection)
+ *
+ * Results are bit-identical to the reference's CPU path for the same inputs
+ * and FT_TOPO/FT_LONELY (same association order), see DESIGN.md §Parity.
+ */
+#ifndef FTAR_H
+#define FTAR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FTAR_VERSION_MAJOR 0
+#define FTAR_VERSION_MINOR 1
+#define FTAR_MAX_STAGES 16
+#define FTAR_MAX_K 64 /* max sources of one reduce (reference: 20, mpi_mod.hpp:811) */
+
+typedef enum {
+  FTAR_UINT8 = 0,   /* MPI_UINT8_T */
+  FTAR_INT8 = 1,    /* MPI_INT8_T */
+  FTAR_UINT16 = 2,  /* MPI_UINT16_T */
+  FTAR_INT16 = 3,   /* MPI_INT16_T */
+  FTAR_INT32 = 4,   /* MPI_INT32_T */
+  FTAR_INT64 = 5,   /* MPI_INT64_T, MPI_LONG_LONG(_INT) */
+  FTAR_FLOAT32 = 6, /* MPI_FLOAT */
+  FTAR_FLOAT64 = 7, /* MPI_DOUBLE */
+  FTAR_BOOL = 8,    /* MPI_C_BOOL: sum of bools == logical OR */
+  FTAR_BFLOAT16 = 9 /* extension: fp32 accumulate, one RNE rounding per reduce */
+} ftar_dtype_t;
+
+typedef enum {
+  FTAR_SUM = 0,  /* MPI_SUM */
+  FTAR_BAND = 1  /* MPI_BAND (integer types only, as in the reference) */
+} ftar_op_t;
+
+typedef enum {
+  FTAR_SUCCESS = 0,
+  FTAR_ERR_INVALID_ARG = 1,
+  FTAR_ERR_UNSUPPORTED = 2,   /* dtype/op pair the reference rejects too */
+  FTAR_ERR_INVALID_TOPO = 3,  /* reference: "invalid FT_TOPO" + exit(1) */
+  FTAR_ERR_HIP = 4,
+  FTAR_ERR_RCCL = 5,
+  FTAR_ERR_INTERNAL = 6,
+  FTAR_ERR_TIMEOUT = 7
+} ftar_status_t;
+
+/* Topology = FT_TOPO stage widths (bottom-up) + FT_LONELY count.  ring != 0
+ * selects the ring schedule (reference: any width 1 in FT_TOPO). */
+typedef struct {
+  int nstages;
+  int stages[FTAR_MAX_STAGES];
+  int lonely;
+  int ring;
+} ftar_topo_t;
+
+typedef struct ftar_comm* ftar_comm_t;
+typedef struct {
+  char internal[128];
+} ftar_unique_id_t; /* == ncclUniqueId */
+
+const char* ftar_version(void);
+const char* ftar_status_string(ftar_status_t s);
+/* Detail of the last failure on the calling thread ("" if none). */
+const char* ftar_last_error(void);
+size_t ftar_dtype_size(ftar_dtype_t dt);
+
+/* ---- L3: k-way element-wise reduce on one device -------------------------
+ * dst[i] = srcs[0][i] (+|&) srcs[1][i] (+|&) ... left to right, i < count.
+ * srcs: HOST array of k device pointers; dst may alias srcs[0] (in place).
+ * k == 1 copies (vector_add/reduce_sum.h:36-47).  stream: hipStream_t. */
+ftar_status_t ftar_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dtype,
+                          ftar_op_t op, void* stream);
+
+/* ---- topology ------------------------------------------------------------
+ * ftar_topo_parse: FT_TOPO / FT_LONELY strings (NULL = unset) for nranks.
+ * Unlike the reference (mpi_mod.hpp:1447-1475, which exit(1)s when FT_TOPO
+ * is unset and P > 1), an unset FT_TOPO returns FTAR_ERR_INVALID_TOPO so the
+ * caller can fall back to ftar_topo_choose. */
+ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nranks, ftar_topo_t* out);
+/* FT_TOPO/FT_LONELY from the environment, else ftar_topo_choose(nranks, bytes). */
+ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out);
+/* Cost-model choice among all ordered factorizations of nranks (plus ring),
+ * constants re-fitted for MI355X xGMI (DESIGN.md §Cost model). */
+ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out);
+/* Model cost (seconds) of one topology for a bucket of `bytes`. */
+double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes);
+/* Writes "w0,w1,..+L" / "ring" into buf; returns needed length. */
+int ftar_topo_format(const ftar_topo_t* topo, char* buf, size_t buflen);
+
+/* ---- communicators -------------------------------------------------------- */
+ftar_status_t ftar_get_unique_id(ftar_unique_id_t* id);
+/* One process per GPU over RCCL p2p (xGMI). Collective across nranks. */
+ftar_status_t ftar_comm_init_rank(ftar_comm_t* comm, int nranks, ftar_unique_id_t id, int rank, int device);
+/* nranks communicators inside ONE process (thread transport: stream-ordered
+ * device copies).  All ranks may share one device (test mode on a 1-GPU box).
+ * Each ftar_allreduce on them must be issued from its own host thread, or via
+ * ftar_allreduce_group. */
+ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* devices);
+ftar_status_t ftar_comm_destroy(ftar_comm_t comm);
+ftar_status_t ftar_comm_rank(ftar_comm_t comm, int* rank);
+ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size);
+ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device);
+/* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = default. */
+ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes);
+ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
+
+/* ---- AllReduce (device resident) -------------------------------------------
+ * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
+ * communicator's topology (FT_TOPO/FT_LONELY from the environment at init,
+ * else the cost-model choice).  Enqueued on `stream`; returns once enqueued. */
+ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                             const ftar_topo_t* topo, ftar_comm_t comm, void* stream);
+/* Drive every rank of an ftar_comm_init_local group from this one call
+ * (one internal host thread per rank); blocks until all ranks are done. */
+ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
+                                   ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
+                                   int nranks, void* const* streams);
+
+/* ---- introspection (tests) -------------------------------------------------
+ * FMA-level schedule of `rank` (same JSON shape as the reference dump in
+ * tests/golden/schedules.jsonl). Returns needed length, or <0 on error. */
+long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, char* buf, size_t buflen);
+/* Executable plan summary: stages, transfers, reduces, scratch bytes (JSON). */
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, size_t esz, char* buf,
+                    size_t buflen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FTAR_H */

@@ -32,6 +32,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "allreduce-over-mpi_amd"))
 import ftar_inputs as fi  # noqa: E402
 
 REF = os.path.join(HERE, "_ref", "ref_golden")

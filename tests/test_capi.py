@@ -1,0 +1,104 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+entry point include/ftar.h declares, and its host logic (topology parsing,
+cost model, error reporting) behaves like the reference's get_stages."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(ROOT, "include", "ftar.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ftar_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    import ftar
+    names = header_functions()
+    assert len(names) >= 20
+    missing = [n for n in names if not hasattr(ftar.lib(), n)]
+    assert not missing, missing
+
+
+def test_version_and_status_strings():
+    import ftar
+    assert "gfx950" in ftar.version()
+    assert ftar.lib().ftar_status_string(3) == b"invalid FT_TOPO/FT_LONELY"
+
+
+@pytest.mark.parametrize("dt,size", [("u8", 1), ("i8", 1), ("u16", 2), ("i16", 2), ("i32", 4), ("i64", 8),
+                                     ("f32", 4), ("f64", 8), ("bool", 1), ("bf16", 2)])
+def test_dtype_sizes(dt, size):
+    import ftar
+    assert ftar.dtype_size(dt) == size
+
+
+@pytest.mark.parametrize("spec,lonely,P,expect", [
+    ("1", "", 8, "ring"), ("2,1", "", 8, "ring"), ("8", "", 8, "8"), ("2,4", "", 8, "2,4"), ("2,2,2", "", 8, "2,2,2"),
+    ("2,2", "1", 5, "2,2+1"), ("3,2", "2", 8, "3,2+2"), ("2,4,", "", 8, "2,4"),
+])
+def test_topo_parse_valid(spec, lonely, P, expect):
+    import ftar
+    assert str(ftar.topo_parse(spec, lonely, P)) == expect
+
+
+@pytest.mark.parametrize("spec,lonely,P", [
+    ("3", "", 4),        # product != P (mpi_mod.hpp:1471)
+    ("4", "1", 5),       # lonely needs >= 2 stages
+    (None, None, 4),     # unset FT_TOPO with P > 1 (reference: exit(1))
+    ("", None, 4),
+    ("2,x", None, 4),
+])
+def test_topo_parse_invalid(spec, lonely, P):
+    import ftar
+    with pytest.raises(ftar.FtarError):
+        ftar.topo_parse(spec, lonely, P)
+
+
+def test_topo_parse_single_rank_defaults():
+    import ftar
+    t = ftar.topo_parse(None, None, 1)
+    assert t.nstages == 1
+
+
+def test_cost_model_prefers_all_links_on_8_gpus():
+    """One stage of width 8 drives all 7 xGMI links at once; a ring drives one."""
+    import ftar
+    big = 1 << 30
+    t = ftar.topo_choose(8, big)
+    assert str(t) == "8"
+    assert ftar.topo_cost("8", 8, big) < ftar.topo_cost("2,4", 8, big) < ftar.topo_cost("ring", 8, big)
+    assert str(ftar.topo_choose(2, big)) in ("2", "ring")  # the same exchange at P=2
+    # every candidate is a valid factorization of P
+    for P in range(2, 17):
+        t = ftar.topo_choose(P, 1 << 20)
+        if not t.ring:
+            prod = 1
+            for w in t.widths:
+                prod *= w
+            assert prod == P
+
+
+def test_topo_from_env(monkeypatch):
+    import ftar
+    monkeypatch.setenv("FT_TOPO", "2,2")
+    monkeypatch.setenv("FT_LONELY", "1")
+    assert str(ftar.topo_from_env(5, 1 << 20)) == "2,2+1"
+    monkeypatch.setenv("FT_TOPO", "3")
+    with pytest.raises(ftar.FtarError):
+        ftar.topo_from_env(5, 1 << 20)
+    monkeypatch.delenv("FT_TOPO")
+    monkeypatch.delenv("FT_LONELY")
+    assert str(ftar.topo_from_env(8, 1 << 30)) == "8"
+
+
+def test_reduce_argument_errors_without_gpu():
+    """Argument validation happens before any device work."""
+    import ftar
+    with pytest.raises(ftar.FtarError):
+        ftar.reduce([], 1234, 10)                      # k = 0
+    with pytest.raises(ftar.FtarError):
+        ftar.reduce([1024, 2048], 4096, 10, "f32", "band")   # BAND on float: unsupported (mpi_mod.hpp:1397)

@@ -1,0 +1,117 @@
+"""Parity of the device-resident FlexTree AllReduce (ftar_allreduce) with the reference.
+
+All P ranks run in this one process on cuda:0 (ftar_comm_init_local: one host
+thread per rank, each with its own comm/reduce streams; transfers are
+stream-ordered device copies matched per peer pair exactly like RCCL p2p).
+The plan executor, the pipelining and the HIP reduce kernel are the product's;
+only the byte mover differs from the multi-GPU RCCL path.
+
+  * every reference golden case (ring, trees, lonely ranks, out-of-place,
+    every dtype/op, repeated calls): bit-exact per rank;
+  * tiny pipeline chunks (many pieces per block) and larger buckets: bit-exact
+    against the pinned oracle;
+  * an RCCL communicator of one rank (the 1-GPU box cannot host more).
+"""
+import numpy as np
+import pytest
+
+import ftar_inputs as fi
+import golden_cases as gc
+import oracle_lib
+from gpu_util import filled_dev, from_dev, to_dev
+
+pytestmark = pytest.mark.gpu
+
+_groups = {}
+
+
+def group(P):
+    import ftar
+    if P not in _groups:
+        _groups[P] = ftar.Comm.init_local(P)
+    return _groups[P]
+
+
+def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1):
+    g = group(len(ins))
+    g.set_chunk_bytes(chunk_bytes)
+    n = ins[0].size
+    send = [to_dev(x) for x in ins]
+    if outofplace:
+        recv = [filled_dev(x.nbytes) for x in ins]
+    else:
+        recv = send
+    for it in range(repeat):
+        sb = [p for _, p in send] if outofplace else None
+        g.allreduce(sb, [p for _, p in recv], n, dtype, op, topo_=topo, lonely=lonely)
+        if outofplace and it + 1 < repeat:
+            send, recv = recv, send
+    return [from_dev(t, ins[0].dtype, n) for t, _ in recv]
+
+
+@pytest.mark.parametrize("case", gc.allreduce_cases(max_n=70000), ids=lambda c: c["id"])
+def test_allreduce_matches_reference_golden(case):
+    ins = gc.case_inputs(case)
+    outs = run_group(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                     repeat=case["repeat"])
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
+@pytest.mark.parametrize("P,topo,lonely", [(2, "1", 0), (4, "1", 0), (8, "1", 0), (4, "2,2", 0), (8, "8", 0),
+                                           (8, "2,2,2", 0), (8, "4,2", 0), (5, "2,2", 1), (8, "3,2", 2)])
+@pytest.mark.parametrize("chunk_bytes", [256, 4096])
+def test_allreduce_pipelined_pieces(P, topo, lonely, chunk_bytes):
+    """Many pieces per block: exercises the per-piece comm->reduce->comm event chain and the scratch halves."""
+    n = 100_003
+    ins = [fi.fill("f32", 31, r, n) for r in range(P)]
+    outs = run_group(ins, topo, lonely, chunk_bytes=chunk_bytes)
+    ref = oracle_lib.allreduce(ins, topo, lonely)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+
+
+@pytest.mark.parametrize("P,topo", [(8, "8"), (8, "1"), (4, "2,2")])
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_allreduce_larger_bucket(P, topo, dt):
+    n = (1 << 22) + 13
+    ins = [fi.fill(dt, 5, r, n) for r in range(P)]
+    outs = run_group(ins, topo, dtype=fi.BY_NAME[dt], chunk_bytes=1 << 20)
+    ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint8), ref[r].view(np.uint8))
+
+
+def test_allreduce_default_topology_is_cost_model_choice():
+    import ftar
+    P, n = 8, 1 << 16
+    ins = [fi.fill("f32", 8, r, n) for r in range(P)]
+    outs = run_group(ins, None)
+    chosen = str(ftar.topo_choose(P, n * 4))
+    ref = oracle_lib.allreduce(ins, "1" if chosen == "ring" else chosen)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+
+
+def test_allreduce_zero_count_and_unsupported():
+    import ftar
+    g = group(2)
+    t, p = filled_dev(16)
+    g.allreduce(None, [p, p], 0, "f32")
+    with pytest.raises(ftar.FtarError):
+        g.allreduce(None, [p, p], 4, "f32", "band")
+
+
+def test_rccl_single_rank_comm():
+    """RCCL communicator bring-up (P=1 on this box): copy semantics of MPI_Allreduce_FT at P<=1."""
+    import ftar
+    uid = ftar.get_unique_id()
+    comm = ftar.Comm.init_rank(1, uid, 0, 0)
+    try:
+        x = fi.fill("f32", 1, 0, 1000)
+        s, sp = to_dev(x)
+        d, dp = filled_dev(x.nbytes)
+        assert ftar.MPI_Allreduce_FT(sp, dp, 1000, "MPI_FLOAT", "MPI_SUM", comm) == 0
+        np.testing.assert_array_equal(from_dev(d, np.float32, 1000), x)
+    finally:
+        comm.destroy()
