@@ -26,6 +26,15 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"libftar.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
                       "or `make -C allreduce-over-mpi_amd/csrc`")
 
+# One HIP runtime per process: torch ships its own libamdhip64/librccl with the
+# same sonames (libamdhip64.so.7, librccl.so.1) as the ROCm ones libftar links.
+# Loading torch first makes libftar's DT_NEEDED entries bind to those copies
+# instead of mapping a second runtime next to torch's.
+try:
+    import torch  # noqa: F401
+except ImportError:  # standalone use: libftar loads /opt/rocm's runtime
+    pass
+
 _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
 
 # ---- enums (include/ftar.h) -------------------------------------------------

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session: smoke, GPU tests, bench, rocprof. Every GPU step has its
+# own time limit; a fault/abort/timeout (exit >= 124) stops the script there.
+# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests bench prof pmc sweep
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+steps=("$@"); [ ${#steps[@]} -eq 0 ] && steps=(smoke tests bench prof)
+run() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/summary.log
+  local t0=$(date +%s)
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a gpurun_out/summary.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name: stopping"; exit $rc; fi
+  return 0
+}
+for s in "${steps[@]}"; do
+  case $s in
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    sweep) run bench_sweep 600 python bench.py --steps 20 --warmup 5 --sweep --no-cpu-baseline ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
