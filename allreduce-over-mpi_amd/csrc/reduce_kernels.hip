@@ -8,9 +8,10 @@
 // Design (bandwidth-bound: (k+1)*n*sizeof(T) bytes, ~0 flops per byte, no MFMA):
 //   * 16 B per lane per access (global_load_dwordx4 / global_store_dwordx4),
 //     one wave instruction = 1 KiB contiguous per source: fully coalesced;
-//   * each lane keeps U vectors of every source in flight before combining
-//     (K*U outstanding 16-B loads per lane) to cover HBM latency at any
-//     occupancy; one-shot grid of ceil(nvec / (256*U)) workgroups (>> 256 CUs);
+//   * each lane keeps U=2 vectors of every source in flight before combining
+//     (2K outstanding 16-B loads per lane); loads carry the nontemporal hint
+//     (streamed once), stores do not (the next ring step sends that block);
+//     one-shot grid of ceil(nvec / 512) workgroups of 256 (>> 256 CUs);
 //   * source pointers travel in the kernarg segment (no device-side pointer
 //     table, no extra dependent load); K is a template parameter for 2..8;
 //   * unaligned heads/tails (block offsets need not be 16-B aligned) are done
@@ -185,17 +186,19 @@ struct Srcs {
 // Element range [head, head + nvec*VE) is vectorised; workgroup 0 also does the
 // `head` leading and `tail` trailing elements element-wise.
 // ---------------------------------------------------------------------------
-template <class Tr, int K, int U, bool NT>
-__global__ void __launch_bounds__(kThreads)
+template <class Tr, int K, int U, bool NTL, bool NTS, int BS = kThreads>
+__global__ void __launch_bounds__(BS)
     reduce_vec_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, void* __restrict__ dst, size_t nvec, int head,
                       int tail) {
   using S = typename Tr::S;
   constexpr int KK = K > 0 ? K : FTAR_MAX_K;
   const int k = K > 0 ? K : kr;
   constexpr int VE = 16 / sizeof(S);
-  const size_t v0 = (size_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+  constexpr int kThreads = BS;
+  const size_t tile_stride = (size_t)gridDim.x * (U * kThreads);
+  size_t v0 = (size_t)blockIdx.x * (U * kThreads) + threadIdx.x;
 
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {  // unaligned head / short tail
     const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
     typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
     for (int j = 1; j < k; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
@@ -204,17 +207,17 @@ __global__ void __launch_bounds__(kThreads)
 
   const u32x4* s0 = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[0]) + head);
   u32x4* d = reinterpret_cast<u32x4*>(static_cast<S*>(dst) + head);
-  if (v0 + (U - 1) * kThreads < nvec) {  // full tile: no per-vector guards
+  for (; v0 + (U - 1) * kThreads < nvec; v0 += tile_stride) {  // full tiles: no per-vector guards
     typename Tr::VA acc[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] = Tr::v_init(ld16<NT>(s0 + v0 + u * kThreads));
+    for (int u = 0; u < U; ++u) acc[u] = Tr::v_init(ld16<NTL>(s0 + v0 + u * kThreads));
     if constexpr (K > 0) {
       u32x4 x[KK > 1 ? KK - 1 : 1][U];
 #pragma unroll
       for (int j = 1; j < KK; ++j) {
         const u32x4* sj = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head);
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[j - 1][u] = ld16<NT>(sj + v0 + u * kThreads);
+        for (int u = 0; u < U; ++u) x[j - 1][u] = ld16<NTL>(sj + v0 + u * kThreads);
       }
 #pragma unroll
       for (int j = 1; j < KK; ++j)
@@ -225,23 +228,23 @@ __global__ void __launch_bounds__(kThreads)
         const u32x4* sj = reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head);
         u32x4 x[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = ld16<NT>(sj + v0 + u * kThreads);
+        for (int u = 0; u < U; ++u) x[u] = ld16<NTL>(sj + v0 + u * kThreads);
 #pragma unroll
         for (int u = 0; u < U; ++u) acc[u] = Tr::v_comb(acc[u], x[u]);
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) st16<NT>(d + v0 + u * kThreads, Tr::v_fin(acc[u]));
-  } else {  // last workgroup: guarded
+    for (int u = 0; u < U; ++u) st16<NTS>(d + v0 + u * kThreads, Tr::v_fin(acc[u]));
+  }
+  // the one partial tile (if any): guarded
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t v = v0 + u * kThreads;
-      if (v >= nvec) break;
-      typename Tr::VA a = Tr::v_init(ld16<NT>(s0 + v));
-      for (int j = 1; j < k; ++j)
-        a = Tr::v_comb(a, ld16<NT>(reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head) + v));
-      st16<NT>(d + v, Tr::v_fin(a));
-    }
+  for (int u = 0; u < U; ++u) {
+    const size_t v = v0 + u * kThreads;
+    if (v >= nvec) break;
+    typename Tr::VA a = Tr::v_init(ld16<NTL>(s0 + v));
+    for (int j = 1; j < k; ++j)
+      a = Tr::v_comb(a, ld16<NTL>(reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head) + v));
+    st16<NTS>(d + v, Tr::v_fin(a));
   }
 }
 
@@ -261,24 +264,36 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 // host-side launch
 // ---------------------------------------------------------------------------
+// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32):
+// nontemporal loads + plain stores, 2 vectors per lane, 256-thread workgroups
+// is the best of the variants at k = 2 (6.96 TB/s) and among the best at k = 8;
+// nontemporal STORES cost 6-8 % (they also evict what the next ring step sends).
 template <int K>
 constexpr int unroll_for() {
-  return K == 2 ? 4 : (K > 0 && K <= 4) ? 2 : 1;
+  return K == 2 ? 4 : (K > 0 && K <= 4) ? 2 : 1;  // variant-0 baseline (kept for A/B)
+}
+constexpr int kUnroll = 2;
+constexpr bool kNtLoads = true, kNtStores = false;
+
+template <class Tr, int K, int U, bool NTL, bool NTS, int BS>
+hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s,
+                      size_t max_blocks) {
+  constexpr int KK = K > 0 ? K : FTAR_MAX_K;
+  Srcs<KK> a{};
+  for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
+  const size_t per_block = (size_t)U * BS;
+  size_t blocks = (nvec + per_block - 1) / per_block;
+  if (blocks == 0) blocks = 1;  // head/tail only
+  if (max_blocks && blocks > max_blocks) blocks = max_blocks;  // grid-stride over the rest
+  if (blocks > 0x7fffffffull) blocks = 0x7fffffffull;
+  hipLaunchKernelGGL((reduce_vec_kernel<Tr, K, U, NTL, NTS, BS>), dim3((unsigned)blocks), dim3(BS), 0, s, a, k, dst,
+                     nvec, head, tail);
+  return hipGetLastError();
 }
 
 template <class Tr, int K>
 hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
-  constexpr int KK = K > 0 ? K : FTAR_MAX_K;
-  constexpr int U = K > 0 ? unroll_for<K>() : 2;
-  Srcs<KK> a{};
-  for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
-  const size_t per_block = (size_t)U * kThreads;
-  size_t blocks = (nvec + per_block - 1) / per_block;
-  if (blocks == 0) blocks = 1;  // head/tail only
-  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((reduce_vec_kernel<Tr, K, U, false>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, dst,
-                     nvec, head, tail);
-  return hipGetLastError();
+  return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kThreads>(srcs, k, dst, nvec, head, tail, s, 0);
 }
 
 template <class Tr>
@@ -317,6 +332,40 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
   return launch_k<Tr, 0>(srcs, k, dst, nvec, (int)head, (int)tail, s);
 }
 
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// A/B variants of the fp32 kernel for tools/kbench.py (not part of ftar.h).
+// ---------------------------------------------------------------------------
+namespace {
+template <int K>
+hipError_t f32_variant(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
+  constexpr int U0 = unroll_for<K>();
+  constexpr int U2 = U0 * 2;
+  switch (v) {
+    case 0: return launch_cfg<F32Sum, K, U0, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 1: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 2: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 3: return launch_cfg<F32Sum, K, U0, false, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 4: return launch_cfg<F32Sum, K, U2, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 5: return launch_cfg<F32Sum, K, U2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 6: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 2048);
+    case 7: return launch_cfg<F32Sum, K, U0, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 2048);
+    case 8: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 9: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 10: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 8192);
+    case 11: return launch_cfg<F32Sum, K, U0, false, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 12: return launch_cfg<F32Sum, K, U2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 13: return launch_cfg<F32Sum, K, U0, true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 14: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 15: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 8192);
+    case 16: return launch_cfg<F32Sum, K, U0, true, false, 1024>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 17: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
+    case 18: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 19: return launch_cfg<F32Sum, K, U2 * 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+  }
+  return hipErrorInvalidValue;
+}
 }  // namespace
 
 size_t dtype_size(ftar_dtype_t dt) {
@@ -375,3 +424,14 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
 }
 
 }  // namespace ftar
+
+extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, const void* const* srcs, int k, void* dst,
+                                                   size_t count, void* stream) {
+  if ((count & 3) || (reinterpret_cast<uintptr_t>(dst) & 15)) return FTAR_ERR_INVALID_ARG;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  if (k == 2) e = ftar::f32_variant<2>(variant, srcs, k, dst, count / 4, s);
+  else if (k == 8) e = ftar::f32_variant<8>(variant, srcs, k, dst, count / 4, s);
+  else return FTAR_ERR_INVALID_ARG;
+  return e == hipSuccess ? FTAR_SUCCESS : FTAR_ERR_HIP;
+}
