@@ -185,9 +185,8 @@ def bench_distributed(a):
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    uid = [ftar.get_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    comm = ftar.Comm.init_rank(world, uid[0], rank, local)
+    import ftar.dist
+    comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
     if a.chunk_bytes:
         comm.chunk_bytes = a.chunk_bytes
     n = a.n or (1 << 28)
