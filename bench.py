@@ -37,8 +37,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--k", type=int, default=2, help="N=1: number of source buckets")
-    ap.add_argument("--n", type=int, default=0, help="elements per bucket (default 2^26 at N=1, 2^28 at N>1)")
+    ap.add_argument("--sources", dest="k", type=int, default=2, help="N=1: number of source buckets k")
+    ap.add_argument("--elements", dest="n", type=int, default=0, help="elements per bucket (default 2^26 at N=1, 2^28 at N>1)")
     ap.add_argument("--dtype", default="f32")
     ap.add_argument("--topo", default=None, help="N>1: FT_TOPO string (default: env FT_TOPO, else cost model)")
     ap.add_argument("--lonely", type=int, default=0)
@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
+    ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     return ap.parse_args()
 
 
@@ -236,8 +237,8 @@ def bench_distributed(a):
 
     bucket = n * esz
     algbw = bucket / (ms * 1e-3) / 1e9
-    busbw = algbw * 2 * (world - 1) / world
-    links = 1 if topo.ring else min(XGMI_LINKS, world - 1)
+    busbw = algbw * 2 * (world - 1) / world if world > 1 else algbw
+    links = max(1, 1 if topo.ring else min(XGMI_LINKS, world - 1))
     peak = links * XGMI_LINK_GBPS
     if rank == 0:
         res = {
@@ -261,7 +262,7 @@ def bench_distributed(a):
 
 def main():
     a = parse()
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.force_dist:
         bench_distributed(a)
     else:
         bench_single(a)
