@@ -1,0 +1,209 @@
+// MPI_Allreduce_FT on MI355X: the reference's host-buffer entry point
+// (allreduce_over_mpi/mpi_mod.hpp:1723-1778) re-expressed over libftar.
+//
+//   reference                               here
+//   get_stages() every call (:1732)         FT_TOPO/FT_LONELY read once per communicator
+//   FlexTree_Context (:1734)                ftar plan cache (per topology, count)
+//   P <= 1 -> memcpy (:1739-1746)           same, on the host
+//   static grow-only host recv_buffer       grow-only DEVICE buffer per communicator
+//   (:1489-1507, never freed)               (freed by MPI_Allreduce_FT_finalize)
+//   ring/tree over MPI_Isend/Irecv          H2D -> ftar_allreduce (RCCL p2p + HIP reduce) -> D2H
+//   + 14-thread OpenMP reduce
+//   MPI_Comm_split every call, leaked       nothing per call; RCCL comm built once
+//   (:1541-1548)
+// The caller's buffers are page-locked on first use (hipHostRegister, cached)
+// so the copies run at PCIe DMA speed; set FTAR_MPI_REGISTER=0 to disable.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "ftar_mpi.h"
+
+namespace {
+
+struct Entry {
+  ftar_comm_t comm = nullptr;
+  int rank = 0, size = 1, device = 0;
+  hipStream_t stream = nullptr;
+  void* dbuf = nullptr;
+  size_t dbuf_bytes = 0;
+};
+
+std::mutex g_mu;
+std::map<MPI_Comm, Entry> g_entries;
+std::map<void*, size_t> g_registered;
+
+int pick_device(MPI_Comm comm) {
+  if (const char* e = getenv("FTAR_DEVICE")) return atoi(e);
+  MPI_Comm node;
+  int local = 0;
+  if (MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node) == MPI_SUCCESS) {
+    MPI_Comm_rank(node, &local);
+    MPI_Comm_free(&node);
+  }
+  int n = 1;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) n = 1;
+  return local % n;
+}
+
+int entry_for(MPI_Comm comm, Entry** out) {
+  auto it = g_entries.find(comm);
+  if (it != g_entries.end()) {
+    *out = &it->second;
+    return MPI_SUCCESS;
+  }
+  Entry e;
+  MPI_Comm_rank(comm, &e.rank);
+  MPI_Comm_size(comm, &e.size);
+  e.device = pick_device(comm);
+  if (e.size > 1) {
+    ftar_unique_id_t id;
+    memset(&id, 0, sizeof id);
+    int ok = e.rank == 0 ? ftar_get_unique_id(&id) == FTAR_SUCCESS : 1;
+    MPI_Bcast(&ok, 1, MPI_INT, 0, comm);
+    if (!ok) return MPI_ERR_OTHER;
+    MPI_Bcast(&id, (int)sizeof id, MPI_BYTE, 0, comm);
+    if (ftar_comm_init_rank(&e.comm, e.size, id, e.rank, e.device) != FTAR_SUCCESS) return MPI_ERR_OTHER;
+  }
+  *out = &g_entries.emplace(comm, e).first->second;
+  return MPI_SUCCESS;
+}
+
+// device + stream on first GPU use (a 1-rank communicator's host path never needs them)
+int ensure_stream(Entry* e) {
+  if (hipSetDevice(e->device) != hipSuccess) return MPI_ERR_OTHER;
+  if (!e->stream && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return MPI_ERR_OTHER;
+  return MPI_SUCCESS;
+}
+
+void maybe_register(const void* p, size_t bytes) {
+  static const bool on = !getenv("FTAR_MPI_REGISTER") || atoi(getenv("FTAR_MPI_REGISTER")) != 0;
+  if (!on || !p || !bytes) return;
+  void* key = const_cast<void*>(p);
+  auto it = g_registered.find(key);
+  if (it != g_registered.end() && it->second >= bytes) return;
+  if (it != g_registered.end()) {
+    (void)hipHostUnregister(key);
+    g_registered.erase(it);
+  }
+  if (hipHostRegister(key, bytes, hipHostRegisterDefault) == hipSuccess) g_registered[key] = bytes;
+  else (void)hipGetLastError();  // pageable copies still work
+}
+
+}  // namespace
+
+extern "C" {
+
+int ftar_mpi_dtype(MPI_Datatype d, ftar_dtype_t* out) {
+  // handle_reduce's dispatch list, mpi_mod.hpp:1365-1375
+  if (d == MPI_UINT8_T) *out = FTAR_UINT8;
+  else if (d == MPI_INT8_T) *out = FTAR_INT8;
+  else if (d == MPI_UINT16_T) *out = FTAR_UINT16;
+  else if (d == MPI_INT16_T) *out = FTAR_INT16;
+  else if (d == MPI_INT32_T) *out = FTAR_INT32;
+  else if (d == MPI_INT64_T || d == MPI_LONG_LONG_INT || d == MPI_LONG_LONG) *out = FTAR_INT64;
+  else if (d == MPI_FLOAT) *out = FTAR_FLOAT32;
+  else if (d == MPI_DOUBLE) *out = FTAR_FLOAT64;
+  else if (d == MPI_C_BOOL) *out = FTAR_BOOL;
+  else return MPI_ERR_TYPE;
+  return MPI_SUCCESS;
+}
+
+int ftar_mpi_op(MPI_Op op, ftar_op_t* out) {
+  if (op == MPI_SUM) *out = FTAR_SUM;
+  else if (op == MPI_BAND) *out = FTAR_BAND;
+  else return MPI_ERR_OP;
+  return MPI_SUCCESS;
+}
+
+int MPI_Allreduce_FT_comm(MPI_Comm comm, ftar_comm_t* out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  Entry* e;
+  int rc = entry_for(comm, &e);
+  if (rc == MPI_SUCCESS) *out = e->comm;
+  return rc;
+}
+
+int MPI_Allreduce_FT(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                     MPI_Comm comm) {
+  ftar_dtype_t dt;
+  ftar_op_t fo;
+  if (ftar_mpi_dtype(datatype, &dt) != MPI_SUCCESS) return MPI_ERR_TYPE;
+  if (ftar_mpi_op(op, &fo) != MPI_SUCCESS) return MPI_ERR_OP;
+  if (count < 0 || (!recvbuf && count)) return MPI_ERR_ARG;
+  std::lock_guard<std::mutex> g(g_mu);
+  Entry* e;
+  int rc = entry_for(comm, &e);
+  if (rc != MPI_SUCCESS) return rc;
+  const size_t bytes = (size_t)count * ftar_dtype_size(dt);
+  const void* src = sendbuf == MPI_IN_PLACE ? recvbuf : sendbuf;
+  if (e->size <= 1) {  // mpi_mod.hpp:1739-1746
+    if (src != recvbuf && bytes) memcpy(recvbuf, src, bytes);
+    return MPI_SUCCESS;
+  }
+  if ((rc = ensure_stream(e)) != MPI_SUCCESS) return rc;
+  if (bytes > e->dbuf_bytes) {
+    if (e->dbuf) (void)hipFree(e->dbuf);
+    e->dbuf = nullptr;
+    e->dbuf_bytes = 0;
+    if (hipMalloc(&e->dbuf, bytes) != hipSuccess) return MPI_ERR_NO_MEM;
+    e->dbuf_bytes = bytes;
+  }
+  maybe_register(src, bytes);
+  maybe_register(recvbuf, bytes);
+  if (bytes && hipMemcpyAsync(e->dbuf, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    return MPI_ERR_OTHER;
+  if (ftar_allreduce(nullptr, e->dbuf, (size_t)count, dt, fo, nullptr, e->comm, e->stream) != FTAR_SUCCESS)
+    return MPI_ERR_OTHER;
+  if (bytes && hipMemcpyAsync(recvbuf, e->dbuf, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+    return MPI_ERR_OTHER;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return MPI_ERR_OTHER;
+  return MPI_SUCCESS;
+}
+
+int MPI_Allreduce_FT_device(const void* sendbuf, void* recvbuf, int count, MPI_Datatype datatype, MPI_Op op,
+                            MPI_Comm comm, void* stream) {
+  ftar_dtype_t dt;
+  ftar_op_t fo;
+  if (ftar_mpi_dtype(datatype, &dt) != MPI_SUCCESS) return MPI_ERR_TYPE;
+  if (ftar_mpi_op(op, &fo) != MPI_SUCCESS) return MPI_ERR_OP;
+  if (count < 0) return MPI_ERR_ARG;
+  std::lock_guard<std::mutex> g(g_mu);
+  Entry* e;
+  int rc = entry_for(comm, &e);
+  if (rc != MPI_SUCCESS) return rc;
+  if ((rc = ensure_stream(e)) != MPI_SUCCESS) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  const void* src = sendbuf == MPI_IN_PLACE ? nullptr : sendbuf;
+  if (e->size <= 1) {
+    if (src && src != recvbuf && count &&
+        hipMemcpyAsync(recvbuf, src, (size_t)count * ftar_dtype_size(dt), hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return MPI_ERR_OTHER;
+  } else if (ftar_allreduce(src, recvbuf, (size_t)count, dt, fo, nullptr, e->comm, s) != FTAR_SUCCESS) {
+    return MPI_ERR_OTHER;
+  }
+  if (!stream && hipStreamSynchronize(s) != hipSuccess) return MPI_ERR_OTHER;
+  return MPI_SUCCESS;
+}
+
+int MPI_Allreduce_FT_finalize(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& kv : g_entries) {
+    Entry& e = kv.second;
+    (void)hipSetDevice(e.device);
+    if (e.stream) (void)hipStreamSynchronize(e.stream);
+    if (e.comm) ftar_comm_destroy(e.comm);
+    if (e.dbuf) (void)hipFree(e.dbuf);
+    if (e.stream) (void)hipStreamDestroy(e.stream);
+  }
+  g_entries.clear();
+  for (auto& kv : g_registered) (void)hipHostUnregister(kv.first);
+  g_registered.clear();
+  return MPI_SUCCESS;
+}
+
+}  // extern "C"

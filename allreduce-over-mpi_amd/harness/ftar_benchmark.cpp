@@ -1,0 +1,197 @@
+// ftar_benchmark — the reference's MPI benchmark harness on the MI355X path.
+//
+// Same command line and the same measurement as
+// allreduce_over_mpi/benchmark.cpp:31-244:
+//   --size N        elements (fp32), default 35            (:42, :71-77)
+//   --repeat R      timed calls, default 1                  (:78-84)
+//   --to-file       per-repeat times -> {tag.}{P}.{n}.{topo}.ar_test.{unix}.txt (:218-238)
+//   --comm-type T   flextree|ftar (MPI_Allreduce_FT) or mpi (library MPI_Allreduce) (:90-101)
+//   --tag S, --version, --check                            (:102-118)
+// data[i] = i * 0.1f on every rank, in place; MPI_Barrier + MPI_Wtime around
+// every call; prints "CHECK <rank>: data[9..23]" per rank and
+// "DONE, average time: <avg>, min time: <min>" (:125-240).
+// Extras: --device (time the device-resident entry, buffers already in HBM),
+// --warmup W (untimed calls first; the reference's first call pays one-time
+// setup), and one JSON summary line on rank 0.
+// --check is two-sided here: the reference only flags results that are too
+// LARGE (benchmark.cpp:201), so NaN/zero results pass there.
+#include <hip/hip_runtime_api.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ftar_mpi.h"
+
+static void die(int rank, const std::string& msg) {
+  fprintf(stderr, "[rank %d] %s\n", rank, msg.c_str());
+  MPI_Abort(MPI_COMM_WORLD, 1);
+}
+
+int main(int argc, char** argv) {
+  int provided = 0, rank = 0, P = 1;
+  MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);  // benchmark.cpp:50
+  MPI_Comm_size(MPI_COMM_WORLD, &P);
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+
+  size_t data_len = 35;
+  int repeat = 1, warmup = 0;
+  bool to_file = false, check = false, device = false;
+  std::string tag, comm_type = "flextree";
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) die(rank, "missing value for " + a);
+      return argv[++i];
+    };
+    if (a == "--size") data_len = strtoull(next().c_str(), nullptr, 0);
+    else if (a == "--repeat") repeat = atoi(next().c_str());
+    else if (a == "--warmup") warmup = atoi(next().c_str());
+    else if (a == "--to-file") to_file = true;
+    else if (a == "--comm-type") comm_type = next();
+    else if (a == "--tag") tag = next();
+    else if (a == "--check") check = true;
+    else if (a == "--device") device = true;
+    else if (a == "--version") {
+      if (rank == 0) printf("ftar_benchmark: %s\n", ftar_version());
+      MPI_Finalize();
+      return 0;
+    } else die(rank, "unknown parameter: " + a);
+  }
+  if (comm_type == "ftar") comm_type = "flextree";
+  if (comm_type != "flextree" && comm_type != "mpi") die(rank, "unknown comm type: " + comm_type);
+  if (device && comm_type == "mpi") die(rank, "--device needs --comm-type flextree");
+
+  std::vector<float> data(data_len);
+  const float base = 0.1f;
+  for (size_t i = 0; i < data_len; ++i) data[i] = i * base;  // benchmark.cpp:125-129
+
+  ftar_topo_t topo;
+  const bool have_topo = ftar_topo_from_env(P, data_len * sizeof(float), &topo) == FTAR_SUCCESS;
+  char topo_s[128] = "?";
+  if (have_topo) ftar_topo_format(&topo, topo_s, sizeof topo_s);
+
+  float* dptr = nullptr;
+  if (device) {
+    ftar_comm_t fc;
+    if (MPI_Allreduce_FT_comm(MPI_COMM_WORLD, &fc) != MPI_SUCCESS) die(rank, "communicator setup failed");
+    int dev = 0;
+    if (fc) ftar_comm_device(fc, &dev);
+    if (hipSetDevice(dev) != hipSuccess || hipMalloc(&dptr, data_len * sizeof(float) + 4) != hipSuccess)
+      die(rank, "hipMalloc failed");
+    if (hipMemcpy(dptr, data.data(), data_len * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      die(rank, "hipMemcpy failed");
+  }
+  MPI_Barrier(MPI_COMM_WORLD);
+  if (rank == 0) {
+    printf("configuration:\n  - total_peers: %d\n  - data_size: %zu\n  - repeat: %d\n  - to_file: %s\n"
+           "  - check_validity: %s\n  - communication method: %s%s\n  - FlexTree topo: %s\n  - library: %s\n",
+           P, data_len, repeat, to_file ? "true" : "false", check ? "true" : "false", comm_type.c_str(),
+           device ? " (device-resident)" : " (host buffers)", topo_s, ftar_version());
+    fflush(stdout);
+  }
+
+  auto one_call = [&]() -> int {
+    if (comm_type == "mpi") return MPI_Allreduce(MPI_IN_PLACE, data.data(), (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+    if (device) return MPI_Allreduce_FT_device(MPI_IN_PLACE, dptr, (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD, nullptr);
+    return MPI_Allreduce_FT(MPI_IN_PLACE, data.data(), (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+  };
+
+  // warm-up calls change the data (in place, x P each); restart from i*0.1 afterwards
+  for (int i = 0; i < warmup; ++i)
+    if (one_call() != MPI_SUCCESS) die(rank, "allreduce failed (warmup)");
+  if (warmup) {
+    for (size_t i = 0; i < data_len; ++i) data[i] = i * base;
+    if (device && hipMemcpy(dptr, data.data(), data_len * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      die(rank, "hipMemcpy failed");
+  }
+
+  std::vector<double> times;
+  double sum_time = 0, min_time = 1e30;
+  for (int i = 0; i < repeat; ++i) {  // benchmark.cpp:157-167
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t1 = MPI_Wtime();
+    if (one_call() != MPI_SUCCESS) die(rank, "allreduce failed");
+    const double t2 = MPI_Wtime();
+    times.push_back(t2 - t1);
+    sum_time += t2 - t1;
+    min_time = std::min(min_time, t2 - t1);
+  }
+  if (device && hipMemcpy(data.data(), dptr, data_len * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+    die(rank, "hipMemcpy failed");
+
+  // validity: expected i * 0.1 * P^repeat (benchmark.cpp:195-210), two-sided
+  size_t bad = 0, first_bad = 0;
+  if (check) {
+    const double scale = std::pow((double)P, repeat);
+    for (size_t i = 0; i < data_len; ++i) {
+      const double exp = (double)(i * base) * scale;
+      const double tol = std::max(0.01, 4.0 * P * repeat * std::fabs(exp) * 1.2e-7);
+      if (!(std::fabs((double)data[i] - exp) <= tol)) {
+        if (!bad) first_bad = i;
+        ++bad;
+      }
+    }
+  }
+  for (int r = 0; r <= P; ++r) {  // ordered CHECK lines (benchmark.cpp:188-213)
+    MPI_Barrier(MPI_COMM_WORLD);
+    if (r == rank + 1) {
+      printf("CHECK %d: ", rank);
+      for (size_t i = 9; i < 24 && i < data_len; ++i) printf("%g ", data[i]);
+      if (check) {
+        if (!bad) printf("(test passed)");
+        else printf("(test FAILED: %zu wrong, first at %zu)", bad, first_bad);
+      }
+      printf("\n");
+      fflush(stdout);
+    }
+  }
+  size_t bad_all = 0;
+  MPI_Allreduce(&bad, &bad_all, 1, MPI_UNSIGNED_LONG, MPI_SUM, MPI_COMM_WORLD);
+  double max_min = 0, max_avg = 0, avg = repeat ? sum_time / repeat : 0;
+  MPI_Allreduce(&min_time, &max_min, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+  MPI_Allreduce(&avg, &max_avg, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+
+  if (device) (void)hipFree(dptr);
+  MPI_Allreduce_FT_finalize();
+  MPI_Finalize();
+
+  if (rank == 0 && to_file) {  // benchmark.cpp:218-238
+    std::ostringstream ss;
+    if (!tag.empty()) ss << tag << ".";
+    ss << P << "." << data_len << ".";
+    if (comm_type == "flextree") {
+      if (have_topo && !topo.ring) {
+        for (int i = 0; i < topo.nstages; ++i) ss << topo.stages[i] << "-";
+        ss << "+" << topo.lonely;
+      } else {
+        ss << "1-+0";
+      }
+    } else {
+      ss << "mpi";
+    }
+    ss << ".ar_test." << time(nullptr) << ".txt";
+    std::ofstream f(ss.str());
+    for (double t : times) f << t << "\n";
+  }
+  if (rank == 0) {
+    const double bytes = (double)data_len * sizeof(float);
+    const double tmin = max_min > 0 ? max_min : 1e-30;
+    printf("\nDONE, average time: %g, min time: %g\n", sum_time / std::max(1, repeat), min_time);
+    printf("{\"harness\":\"ftar_benchmark\",\"comm_type\":\"%s\",\"resident\":\"%s\",\"P\":%d,\"count\":%zu,"
+           "\"topo\":\"%s\",\"repeat\":%d,\"warmup\":%d,\"min_s\":%.6e,\"avg_s\":%.6e,\"algbw_GBps_min\":%.3f,"
+           "\"busbw_GBps_min\":%.3f,\"check\":\"%s\"}\n",
+           comm_type.c_str(), device ? "device" : "host", P, data_len, topo_s, repeat, warmup, max_min, max_avg,
+           bytes / tmin / 1e9, P > 1 ? bytes / tmin / 1e9 * 2.0 * (P - 1) / P : bytes / tmin / 1e9,
+           check ? (bad_all ? "FAILED" : "passed") : "off");
+  }
+  return bad_all ? 2 : 0;
+}

@@ -18,6 +18,8 @@
 //              FMA_Send/FMA_Recv operations (mpi_mod.hpp:627-766).
 //   reduce     --dtype D --op O --k K --n N --seed S --out FILE
 //              calls FlexTree::reduce_sum / reduce_band directly.
+//   arbench    --n N --repeat R   (under mpiexec, FT_TOPO set): the reference
+//              MPI path timed like benchmark.cpp (C1 = P2 ring 2^20 fp32).
 //   bench      --k K --n N --seconds T
 //              times FlexTree::reduce_sum<float> (the cpu_baseline, kind
 //              "reference"); prints one JSON line.
@@ -161,6 +163,41 @@ static int mode_allreduce(int argc, char** argv) {
   return 0;
 }
 
+// benchmark.cpp:125-167 semantics with the reference's own MPI_Allreduce_FT:
+// data[i] = i*0.1f, in place, MPI_Barrier + MPI_Wtime around each call.
+static int mode_arbench(int argc, char** argv) {
+  MPI_Init(&argc, &argv);
+  int rank, P;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &P);
+  size_t n = strtoull(arg(argc, argv, "--n", "1048576"), 0, 10);
+  int repeat = atoi(arg(argc, argv, "--repeat", "20"));
+  std::vector<float> data(n);
+  const float base = 0.1;
+  for (size_t i = 0; i < n; ++i) data[i] = i * base;
+  double sum = 0, mn = 1e30, first = 0;
+  for (int it = 0; it < repeat; ++it) {
+    MPI_Barrier(MPI_COMM_WORLD);
+    double t1 = MPI_Wtime();
+    MPI_Allreduce(MPI_IN_PLACE, data.data(), (int)n, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+    double t2 = MPI_Wtime();
+    if (it == 0) first = t2 - t1;
+    else sum += t2 - t1;  // mean excludes the first call (OMP team + buffer setup)
+    mn = std::min(mn, t2 - t1);
+  }
+  double mx_min = 0, mean = repeat > 1 ? sum / (repeat - 1) : first, mx_mean = 0;
+  MPI_Reduce(&mn, &mx_min, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+  MPI_Reduce(&mean, &mx_mean, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+  if (rank == 0) {
+    const char* topo = getenv("FT_TOPO");
+    printf("{\"kind\":\"reference\",\"P\":%d,\"n\":%zu,\"topo\":\"%s\",\"repeat\":%d,\"min_s\":%.6e,"
+           "\"mean_s\":%.6e,\"first_s\":%.6e,\"algbw_GBps_min\":%.4f,\"threads_per_rank\":14}\n",
+           P, n, topo ? topo : "", repeat, mx_min, mx_mean, first, n * 4.0 / mx_min / 1e9);
+  }
+  MPI_Finalize();
+  return 0;
+}
+
 static std::string json_ops(const std::vector<std::vector<FMA_Operation>>& v) {
   std::string s = "[";
   for (size_t i = 0; i < v.size(); ++i) {
@@ -249,6 +286,7 @@ int main(int argc, char** argv) {
   if (m == "schedule") return mode_schedule(argc, argv);
   if (m == "reduce") return mode_reduce(argc, argv);
   if (m == "bench") return mode_bench(argc, argv);
+  if (m == "arbench") return mode_arbench(argc, argv);
   fprintf(stderr, "unknown mode %s\n", m.c_str());
   return 1;
 }

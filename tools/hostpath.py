@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Host-memory end-to-end rate of the AllReduce path (DESIGN.md §Host path).
+
+The reference's buffers live in host memory (MPI send/recv buffers,
+benchmark.cpp:125-131); MPI_Allreduce_FT here does H2D -> device AllReduce ->
+D2H.  Measured on one MI355X: pinned H2D and D2H of one bucket, the device
+AllReduce of P in-process ranks, and the whole host->host call, per bucket size.
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "allreduce-over-mpi_amd"))
+import torch  # noqa: E402
+import ftar  # noqa: E402
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    best = 1e30
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    return best
+
+
+dev = torch.device("cuda:0")
+out = []
+for n in (1 << 20, 1 << 26, 1 << 28):
+    nbytes = n * 4
+    h = torch.rand(n).pin_memory()
+    hp = torch.empty(n).pin_memory()
+    hpg = torch.empty(n)                # pageable
+    d = torch.empty(n, device=dev)
+    t_h2d = timeit(lambda: d.copy_(h, non_blocking=True))
+    t_d2h = timeit(lambda: hp.copy_(d, non_blocking=True))
+    t_d2h_pageable = timeit(lambda: hpg.copy_(d))
+    row = {"bytes": nbytes, "h2d_GBps": round(nbytes / t_h2d / 1e9, 2), "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
+           "d2h_pageable_GBps": round(nbytes / t_d2h_pageable / 1e9, 2)}
+    for P, topo in ((2, "2"), (8, "8")):
+        if n > (1 << 26) and P > 2:
+            continue
+        g = ftar.Comm.init_local(P)
+        ds = [torch.rand(n, device=dev) for _ in range(P)]
+        hs = [torch.rand(n).pin_memory() for _ in range(P)]
+        t_dev = timeit(lambda: g.allreduce(None, ds, n, "f32", topo_=topo))
+
+        def e2e():
+            for r in range(P):
+                ds[r].copy_(hs[r], non_blocking=True)
+            g.allreduce(None, ds, n, "f32", topo_=topo, streams=[torch.cuda.current_stream()] * P)
+            for r in range(P):
+                hs[r].copy_(ds[r], non_blocking=True)
+        t_e2e = timeit(e2e)
+        row[f"P{P}_device_ms"] = round(t_dev * 1e3, 3)
+        row[f"P{P}_host_e2e_ms"] = round(t_e2e * 1e3, 3)
+        g.destroy()
+        del ds, hs
+    out.append(row)
+    print(json.dumps(row), flush=True)
