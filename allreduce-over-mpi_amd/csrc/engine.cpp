@@ -280,6 +280,15 @@ ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
   return ftar::allreduce(sendbuf, recvbuf, count, dtype, op, topo, comm, static_cast<hipStream_t>(stream));
 }
 
+ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                                  ftar_comm_t comm, void* stream) {
+  if (!comm || !recvbuf) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  return comm->tp->native_allreduce(sendbuf == recvbuf ? nullptr : sendbuf, recvbuf, count, dtype, op,
+                                    static_cast<hipStream_t>(stream));
+}
+
 ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
                                    ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
                                    int nranks, void* const* streams) {

@@ -100,6 +100,12 @@ class Transport {
   virtual ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) = 0;
   virtual ftar_status_t group_end() = 0;
   virtual const char* name() const = 0;
+  // The transport library's own collective, for comparison (RCCL only).
+  virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                                         hipStream_t s) {
+    (void)send; (void)recv; (void)count; (void)dt; (void)op; (void)s;
+    return FTAR_ERR_UNSUPPORTED;
+  }
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_t& id, int rank,

@@ -66,6 +66,23 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "rccl"; }
+  ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                                 hipStream_t s) override {
+    ncclDataType_t t;
+    switch (dt) {
+      case FTAR_UINT8: t = ncclUint8; break;
+      case FTAR_INT8: t = ncclInt8; break;
+      case FTAR_INT32: t = ncclInt32; break;
+      case FTAR_INT64: t = ncclInt64; break;
+      case FTAR_FLOAT32: t = ncclFloat32; break;
+      case FTAR_FLOAT64: t = ncclFloat64; break;
+      case FTAR_BFLOAT16: t = ncclBfloat16; break;
+      default: return FTAR_ERR_UNSUPPORTED;
+    }
+    if (op != FTAR_SUM) return FTAR_ERR_UNSUPPORTED;
+    FTAR_CHECK_NCCL(ncclAllReduce(send ? send : recv, recv, count, t, ncclSum, comm_, s));
+    return FTAR_SUCCESS;
+  }
 
  private:
   ncclComm_t comm_;

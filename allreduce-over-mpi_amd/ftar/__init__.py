@@ -97,6 +97,7 @@ _lib.ftar_comm_destroy.argtypes = [_vp]
 _lib.ftar_comm_set_chunk_bytes.argtypes = [_vp, _sz]
 _lib.ftar_comm_get_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
 _lib.ftar_allreduce.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(Topo), _vp, _vp]
+_lib.ftar_rccl_allreduce.argtypes = [_vp, _vp, _sz, _int, _int, _vp, _vp]
 _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int, ctypes.POINTER(Topo),
                                       ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
@@ -282,6 +283,12 @@ class Comm:
         st = _lib.ftar_allreduce(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), t, self.handle,
                                  _stream(stream))
         _check(st, "ftar_allreduce")
+
+    def rccl_allreduce(self, sendbuf, recvbuf, count, dtype="f32", op="sum", stream=None):
+        """RCCL's own ncclAllReduce on this communicator (comparison yardstick)."""
+        st = _lib.ftar_rccl_allreduce(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), self.handle,
+                                      _stream(stream))
+        _check(st, "ftar_rccl_allreduce")
 
     def destroy(self):
         if self.handle:

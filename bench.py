@@ -175,21 +175,34 @@ def bench_single(a):
     print(json.dumps(res), flush=True)
 
 
+def _factorizations(n):
+    out = []
+
+    def rec(m, cur):
+        if m == 1:
+            if cur:
+                out.append(list(cur))
+            return
+        for f in range(2, m + 1):
+            if m % f == 0:
+                rec(m // f, cur + [f])
+    rec(n, [])
+    return out
+
+
 def bench_distributed(a):
     import torch
     import torch.distributed as dist
 
     import ftar
+    import ftar.dist
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    import ftar.dist
     comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
-    if a.chunk_bytes:
-        comm.chunk_bytes = a.chunk_bytes
     n = a.n or (1 << 28)
     esz = ftar.dtype_size(a.dtype)
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
@@ -198,30 +211,69 @@ def bench_distributed(a):
     x = (torch.rand(n, generator=gen, device=dev, dtype=torch.float32) * 2 - 1).to(tdt)
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream()
+    bucket = n * esz
+
+    def timed(fn, steps, warmup):
+        """barrier + sync on both sides of `steps` calls; max over ranks (ms per call)."""
+        for _ in range(warmup):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item() / max(1, steps) * 1e3
+
+    def run_with(topo, chunk):
+        comm.chunk_bytes = chunk
+        return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
+
+    # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
     if a.topo:
-        topo = ftar.topo(a.topo, a.lonely, nranks=world)
+        default_topo = ftar.topo(a.topo, a.lonely, nranks=world)
     else:
-        topo = ftar.topo_from_env(world, n * esz)
+        default_topo = ftar.topo_from_env(world, bucket)
+    default_chunk = a.chunk_bytes or comm.chunk_bytes
 
-    def step():
-        comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
+    # BASELINE configs[3]: "chunk size swept" -- every factorization of P and the ring, x chunk sizes
+    sweep = []
+    cands = [str(default_topo)] + (["1"] if world > 1 else []) + [",".join(map(str, f)) for f in _factorizations(world)]
+    seen = set()
+    for tp in cands:
+        t = ftar.topo("1" if tp == "ring" else tp, 0 if "+" not in tp else int(tp.split("+")[1]))
+        key = str(t)
+        if key in seen:
+            continue
+        seen.add(key)
+        for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
+            ms_ = timed(run_with(t, chunk), steps=min(5, a.steps), warmup=1)
+            sweep.append({"topology": key, "chunk_bytes": chunk, "ms": round(ms_, 4),
+                          "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
+    best = min(sweep, key=lambda r: r["ms"])
+    best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
 
-    for _ in range(a.warmup):
-        step()
+    # headline: the swept-best (topology, chunk), K timed steps after W warmup
+    ms = timed(run_with(best_topo, best["chunk_bytes"]), a.steps, a.warmup)
+    ms_default = timed(run_with(default_topo, default_chunk), min(a.steps, 10), 1)
+    comm.chunk_bytes = best["chunk_bytes"]
+    comm.allreduce(x, y, n, a.dtype, "sum", topo_=best_topo, stream=stream)
     torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    t1 = time.perf_counter()
-    tmax = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    ms = tmax.item() / a.steps * 1e3
 
-    # correctness: identical on every rank, and within (P-1) * 2^-24 * sum|x| of the fp64 sum on a sample
+    # RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
+    try:
+        y2 = torch.empty_like(x)
+        ms_rccl = timed(lambda: comm.rccl_allreduce(x, y2, n, a.dtype, "sum", stream=stream), min(a.steps, 10), 2)
+        del y2
+    except Exception as e:  # noqa: BLE001
+        ms_rccl = None
+        sys.stderr.write(f"rccl yardstick failed: {e}\n")
+
+    # correctness: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
     idx = torch.linspace(0, n - 1, 4096, device=dev).long()
     mine = y[idx].float().cpu()
     xs = x[idx].float().cpu()
@@ -235,10 +287,12 @@ def bench_distributed(a):
     tol = (world - 1) * eps * absum + 1e-30
     ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
 
-    bucket = n * esz
-    algbw = bucket / (ms * 1e-3) / 1e9
-    busbw = algbw * 2 * (world - 1) / world if world > 1 else algbw
-    links = max(1, 1 if topo.ring else min(XGMI_LINKS, world - 1))
+    def bws(m):
+        alg = bucket / (m * 1e-3) / 1e9
+        return alg, (alg * 2 * (world - 1) / world if world > 1 else alg)
+
+    algbw, busbw = bws(ms)
+    links = max(1, 1 if best_topo.ring else min(XGMI_LINKS, world - 1))
     peak = links * XGMI_LINK_GBPS
     if rank == 0:
         res = {
@@ -247,12 +301,18 @@ def bench_distributed(a):
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
             "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
-                       "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo),
-                       "chunk_bytes": comm.chunk_bytes, "parallelism": f"dp{world}"},
+                       "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
+                       "chunk_bytes": best["chunk_bytes"], "selection": "best of sweep (FT_TOPO x chunk)",
+                       "parallelism": f"dp{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
                          "frac": round(busbw / peak, 4), "traffic": None,
                          "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
+            "default_config": {"topology": str(default_topo), "chunk_bytes": default_chunk, "ms": round(ms_default, 4),
+                               "busbw_GBps": round(bws(ms_default)[1], 2)},
+            "rccl_native_allreduce": None if ms_rccl is None else
+            {"ms": round(ms_rccl, 4), "busbw_GBps": round(bws(ms_rccl)[1], 2)},
+            "sweep": sweep,
             "check": "ok" if ok else "MISMATCH",
         }
         print(json.dumps(res), flush=True)

@@ -143,6 +143,13 @@ ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* rec
                                    ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
                                    int nranks, void* const* streams);
 
+/* ---- diagnostics ---------------------------------------------------------------
+ * RCCL's own ncclAllReduce on the communicator's RCCL comm (ring/tree of the
+ * vendor library, reduction inside RCCL): the yardstick bench.py reports next
+ * to ftar at N > 1.  FTAR_ERR_UNSUPPORTED on local (in-process) groups. */
+ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                                  ftar_comm_t comm, void* stream);
+
 /* ---- introspection (tests) -------------------------------------------------
  * FMA-level schedule of `rank` (same JSON shape as the reference dump in
  * tests/golden/schedules.jsonl). Returns needed length, or <0 on error. */
