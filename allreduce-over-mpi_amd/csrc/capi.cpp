@@ -181,6 +181,31 @@ ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
   return FTAR_SUCCESS;
 }
 
+int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out) {
+  // the reference's getWidth(P) order (cost_model/GetWidth.h:10-47): ordered
+  // factorizations, smallest first factor first; its {1,P}/{P,1} pair is the ring.
+  if (nranks <= 0) return -FTAR_ERR_INVALID_ARG;
+  std::vector<size_t> cur;
+  std::vector<std::vector<size_t>> cands;
+  ftar::factorizations((size_t)nranks, cur, cands);
+  int n = 0;
+  for (auto& c : cands) {
+    ftar::Topology t;
+    if (c.size() == 1) {  // the width-P single stage is listed as [1,P],[P,1] by the reference: ring first
+      ftar::Topology r;
+      r.ring = true;
+      r.widths = {1};
+      if (out && n < max_out) ftar::from_topology(r, &out[n]);
+      ++n;
+    }
+    if (c.size() > FTAR_MAX_STAGES) continue;
+    t.widths = c;
+    if (out && n < max_out) ftar::from_topology(t, &out[n]);
+    ++n;
+  }
+  return n;
+}
+
 ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out) {
   ftar_status_t st = ftar_topo_parse(getenv("FT_TOPO"), getenv("FT_LONELY"), nranks, out);
   if (st == FTAR_SUCCESS) return st;

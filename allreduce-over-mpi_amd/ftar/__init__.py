@@ -87,6 +87,7 @@ _lib.ftar_reduce.argtypes = [ctypes.POINTER(_vp), _int, _vp, _sz, _int, _int, _v
 _lib.ftar_topo_parse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, _int, ctypes.POINTER(Topo)]
 _lib.ftar_topo_from_env.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
 _lib.ftar_topo_choose.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
+_lib.ftar_topo_candidates.argtypes = [_int, ctypes.POINTER(Topo), _int]
 _lib.ftar_topo_cost.argtypes = [ctypes.POINTER(Topo), _int, _sz]
 _lib.ftar_topo_cost.restype = ctypes.c_double
 _lib.ftar_topo_format.argtypes = [ctypes.POINTER(Topo), ctypes.c_char_p, _sz]
@@ -210,6 +211,15 @@ def topo_choose(nranks, nbytes):
     t = Topo()
     _check(_lib.ftar_topo_choose(nranks, nbytes, ctypes.byref(t)), "ftar_topo_choose")
     return t
+
+
+def topo_candidates(nranks):
+    n = _lib.ftar_topo_candidates(nranks, None, 0)
+    if n < 0:
+        raise FtarError(-n, "ftar_topo_candidates")
+    arr = (Topo * max(1, n))()
+    _lib.ftar_topo_candidates(nranks, arr, n)
+    return [arr[i] for i in range(n)]
 
 
 def topo_cost(t, nranks, nbytes):

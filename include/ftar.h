@@ -109,6 +109,11 @@ ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out);
 /* Cost-model choice among all ordered factorizations of nranks (plus ring),
  * constants re-fitted for MI355X xGMI (DESIGN.md §Cost model). */
 ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out);
+/* The candidate set the cost model scores, in the reference's getWidth order
+ * (cost_model/GetWidth.h:42-47; its [1,P]/[P,1] entries = the ring), plus the
+ * single-stage width-P tree right after the ring (getWidth omits it; FT_TOPO=P
+ * is valid).  Writes up to max_out entries, returns the total count (<0 = error). */
+int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out);
 /* Model cost (seconds) of one topology for a bucket of `bytes`. */
 double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes);
 /* Writes "w0,w1,..+L" / "ring" into buf; returns needed length. */

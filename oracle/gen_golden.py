@@ -13,6 +13,7 @@ fixtures:
   tests/golden/reduce.npz      outputs of FlexTree::reduce_sum / reduce_band
   tests/golden/schedules.jsonl FMA-level send/recv schedules per rank
   tests/golden/inputs.json     first draws of the input generator (pins it)
+  tests/golden/getwidth.json   the cost model's candidate width lists, P = 1..24
 
 Inputs are not stored: they are regenerated from (seed, rank) with
 include/ftar_inputs.h / tests/ftar_inputs.py, which inputs.json pins.
@@ -144,6 +145,12 @@ def main():
                 d = json.loads(line)
                 d.update(P=P, topo=topo, lonely=lonely, n=n)
                 f.write(json.dumps(d, separators=(",", ":")) + "\n")
+
+    # cost-model candidate lists: getWidth(P) of the reference (cost_model/GetWidth.h:42-47)
+    gw = subprocess.run([os.path.join(HERE, "_ref", "ref_getwidth"), "1", "24"], check=True,
+                        capture_output=True, text=True).stdout
+    with open(os.path.join(OUT, "getwidth.json"), "w") as f:
+        f.write(gw)
 
     # generator pin
     pins = []

@@ -102,3 +102,24 @@ def test_reduce_argument_errors_without_gpu():
         ftar.reduce([], 1234, 10)                      # k = 0
     with pytest.raises(ftar.FtarError):
         ftar.reduce([1024, 2048], 4096, 10, "f32", "band")   # BAND on float: unsupported (mpi_mod.hpp:1397)
+
+
+def test_cost_model_candidates_match_reference_getwidth():
+    """The candidate set is the reference's getWidth(P) (tests/golden/getwidth.json, dumped from
+    cost_model/GetWidth.h), its [1,P]/[P,1] entries being the ring, plus the single-stage
+    width-P tree that getWidth never lists although FT_TOPO=P is valid (mpi_mod.hpp:1440-1468)
+    and is the all-links schedule on an MI355X node."""
+    import json
+    import ftar
+    with open(os.path.join(ROOT, "tests", "golden", "getwidth.json")) as f:
+        ref = json.load(f)
+    for P in range(2, 25):
+        exp = []
+        for w in ref[str(P)]:
+            key = "ring" if 1 in w else ",".join(map(str, w))
+            if not exp or exp[-1] != key:
+                exp.append(key)
+                if key == "ring":
+                    exp.append(str(P))
+        got = [str(t) for t in ftar.topo_candidates(P)]
+        assert got == exp, (P, got, exp)
