@@ -117,7 +117,7 @@ def test_cost_model_candidates_match_reference_getwidth():
         exp = []
         for w in ref[str(P)]:
             key = "ring" if 1 in w else ",".join(map(str, w))
-            if not exp or exp[-1] != key:
+            if key not in exp:
                 exp.append(key)
                 if key == "ring":
                     exp.append(str(P))
