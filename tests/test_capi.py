@@ -123,3 +123,17 @@ def test_cost_model_candidates_match_reference_getwidth():
                     exp.append(str(P))
         got = [str(t) for t in ftar.topo_candidates(P)]
         assert got == exp, (P, got, exp)
+
+
+def test_mpi_library_exports_ftar_mpi_h():
+    """libftar_mpi.so (built where MPICH is present) exports every include/ftar_mpi.h entry point."""
+    import ctypes
+    lib_path = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib", "libftar_mpi.so")
+    if not os.path.exists(lib_path):
+        pytest.skip("libftar_mpi.so not built (no MPI here)")
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "ftar_mpi.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"\b((?:MPI_Allreduce_FT\w*|ftar_mpi_\w+))\s*\(", src)))
+    assert "MPI_Allreduce_FT" in names and len(names) >= 5
+    import ftar  # noqa: F401  (loads libftar.so first, as the loader would)
+    lib = ctypes.CDLL(lib_path)
+    assert all(hasattr(lib, n) for n in names), names

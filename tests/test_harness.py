@@ -1,0 +1,58 @@
+"""The C++ harness (ftar_benchmark) keeps benchmark.cpp's CLI and output
+(allreduce_over_mpi/benchmark.cpp:31-244).  CPU runs: 1 rank (the reference's
+P<=1 memcpy semantics, mpi_mod.hpp:1739) and the library-MPI comparison at
+P=2; the GPU run times the device-resident entry."""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib", "ftar_benchmark")
+MPIEXEC = "/opt/conda/bin/mpiexec"
+needs = pytest.mark.skipif(not (os.path.exists(BIN) and os.path.exists(MPIEXEC)), reason="harness or MPICH missing")
+
+
+def run(n, args, tmp_path, env=None):
+    e = dict(os.environ, **(env or {}))
+    p = subprocess.run([MPIEXEC, "-n", str(n), BIN] + args, cwd=tmp_path, env=e, capture_output=True, text=True,
+                       timeout=120)
+    return p.returncode, p.stdout + p.stderr
+
+
+@needs
+def test_harness_single_rank_reference_output(tmp_path):
+    rc, out = run(1, ["--size", "1000", "--repeat", "3", "--check", "--to-file", "--tag", "t"], tmp_path,
+                  {"FT_TOPO": "1"})
+    assert rc == 0, out
+    assert "configuration:" in out
+    assert re.search(r"CHECK 0: 0\.9 1 1\.1 .*\(test passed\)", out), out
+    assert re.search(r"DONE, average time: \S+, min time: \S+", out), out
+    files = glob.glob(os.path.join(tmp_path, "t.1.1000.1-+0.ar_test.*.txt"))  # benchmark.cpp:218-238
+    assert len(files) == 1 and len(open(files[0]).read().split()) == 3
+
+
+@needs
+def test_harness_library_mpi_two_ranks(tmp_path):
+    rc, out = run(2, ["--comm-type", "mpi", "--size", "4099", "--repeat", "2", "--check", "--to-file"], tmp_path)
+    assert rc == 0, out
+    assert out.count("(test passed)") == 2, out
+    assert glob.glob(os.path.join(tmp_path, "2.4099.mpi.ar_test.*.txt"))
+
+
+@needs
+def test_harness_rejects_unknown_arguments(tmp_path):
+    rc, out = run(1, ["--bogus"], tmp_path)
+    assert rc != 0 and "unknown parameter" in out
+    rc, out = run(1, ["--comm-type", "nope"], tmp_path)
+    assert rc != 0 and "unknown comm type" in out
+
+
+@needs
+@pytest.mark.gpu
+def test_harness_device_resident_single_rank(tmp_path):
+    rc, out = run(1, ["--size", "1048576", "--repeat", "3", "--warmup", "1", "--check", "--device"], tmp_path)
+    assert rc == 0, out
+    assert "(test passed)" in out and '"resident":"device"' in out
