@@ -264,14 +264,10 @@ __global__ void __launch_bounds__(kThreads)
 // ---------------------------------------------------------------------------
 // host-side launch
 // ---------------------------------------------------------------------------
-// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32, DESIGN.md §Kernel):
+// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32, DESIGN.md §3):
 // nontemporal loads + plain stores, 2 vectors per lane, 256-thread workgroups
 // is the best of the variants at k = 2 (6.96 TB/s) and among the best at k = 8;
 // nontemporal STORES cost 6-8 % (they also evict what the next ring step sends).
-template <int K>
-constexpr int unroll_for() {
-  return K == 2 ? 4 : (K > 0 && K <= 4) ? 2 : 1;  // variant-0 baseline (kept for A/B)
-}
 constexpr int kUnroll = 2;
 constexpr bool kNtLoads = true, kNtStores = false;
 
@@ -335,34 +331,34 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// A/B variants of the fp32 kernel for tools/kbench.py (not part of ftar.h).
+// A/B variants for tools/kbench.py (not part of ftar.h): (U, NT loads, NT
+// stores, workgroup size, grid cap) for fp32 and bf16 sums, k in {2, 4, 8}.
 // ---------------------------------------------------------------------------
 namespace {
-template <int K>
-hipError_t f32_variant(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
-  constexpr int U0 = unroll_for<K>();
-  constexpr int U2 = U0 * 2;
+template <class Tr, int K>
+hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
   switch (v) {
-    case 0: return launch_cfg<F32Sum, K, U0, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 1: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 2: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 3: return launch_cfg<F32Sum, K, U0, false, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 4: return launch_cfg<F32Sum, K, U2, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 5: return launch_cfg<F32Sum, K, U2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 6: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 2048);
-    case 7: return launch_cfg<F32Sum, K, U0, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 2048);
-    case 8: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 9: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 10: return launch_cfg<F32Sum, K, U0, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 8192);
-    case 11: return launch_cfg<F32Sum, K, U0, false, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 12: return launch_cfg<F32Sum, K, U2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 13: return launch_cfg<F32Sum, K, U0, true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 14: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 15: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 8192);
-    case 16: return launch_cfg<F32Sum, K, U0, true, false, 1024>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 17: return launch_cfg<F32Sum, K, U0, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
-    case 18: return launch_cfg<F32Sum, K, (U0 > 1 ? U0 / 2 : 1), true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 19: return launch_cfg<F32Sum, K, U2 * 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 0: return launch_cfg<Tr, K, 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 1: return launch_cfg<Tr, K, 1, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 2: return launch_cfg<Tr, K, 4, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 3: return launch_cfg<Tr, K, 1, true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 4: return launch_cfg<Tr, K, 2, true, false, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 5: return launch_cfg<Tr, K, 1, true, false, 1024>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 6: return launch_cfg<Tr, K, 2, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 7: return launch_cfg<Tr, K, 2, false, false, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 8: return launch_cfg<Tr, K, 1, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 2048);
+    case 9: return launch_cfg<Tr, K, 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
+    case 10: return launch_cfg<Tr, K, 1, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 11: return launch_cfg<Tr, K, 4, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+  }
+  return hipErrorInvalidValue;
+}
+template <class Tr>
+hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
+  switch (k) {
+    case 2: return variant_k<Tr, 2>(v, srcs, k, dst, nvec, s);
+    case 4: return variant_k<Tr, 4>(v, srcs, k, dst, nvec, s);
+    case 8: return variant_k<Tr, 8>(v, srcs, k, dst, nvec, s);
   }
   return hipErrorInvalidValue;
 }
@@ -425,13 +421,14 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
 
 }  // namespace ftar
 
-extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, const void* const* srcs, int k, void* dst,
+extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, int dtype, const void* const* srcs, int k, void* dst,
                                                    size_t count, void* stream) {
-  if ((count & 3) || (reinterpret_cast<uintptr_t>(dst) & 15)) return FTAR_ERR_INVALID_ARG;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) return FTAR_ERR_INVALID_ARG;
   hipStream_t s = static_cast<hipStream_t>(stream);
   hipError_t e;
-  if (k == 2) e = ftar::f32_variant<2>(variant, srcs, k, dst, count / 4, s);
-  else if (k == 8) e = ftar::f32_variant<8>(variant, srcs, k, dst, count / 4, s);
+  if (dtype == FTAR_FLOAT32 && count % 4 == 0) e = ftar::variant_tr<ftar::F32Sum>(variant, srcs, k, dst, count / 4, s);
+  else if (dtype == FTAR_BFLOAT16 && count % 8 == 0)
+    e = ftar::variant_tr<ftar::BF16Sum>(variant, srcs, k, dst, count / 8, s);
   else return FTAR_ERR_INVALID_ARG;
   return e == hipSuccess ? FTAR_SUCCESS : FTAR_ERR_HIP;
 }
