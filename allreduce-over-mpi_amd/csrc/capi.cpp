@@ -263,13 +263,12 @@ long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t co
   return emit(s, buf, buflen);
 }
 
-long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, size_t esz, char* buf,
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, int native_allgather, char* buf,
                     size_t buflen) {
-  (void)esz;
   ftar::Topology t;
   if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -FTAR_ERR_INVALID_TOPO;
   ftar::Plan p;
-  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p);
+  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p, native_allgather != 0);
   if (st != FTAR_SUCCESS) return -(long)st;
   return emit(p.json(), buf, buflen);
 }

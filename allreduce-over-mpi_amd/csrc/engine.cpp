@@ -33,6 +33,7 @@ struct ftar_comm {
   size_t scratch_bytes = 0;
   size_t chunk_bytes = 0;
   bool auto_topo = true;
+  bool native_allgather = false;
   ftar::Topology topo;
   std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
   std::vector<hipEvent_t> events;
@@ -58,6 +59,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
+  if (const char* na = getenv("FTAR_NATIVE_ALLGATHER")) c->native_allgather = atoi(na) != 0;
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
   if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
@@ -105,11 +107,11 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
     FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
   }
-  const std::string key = t.key() + "/" + std::to_string(count);
+  const std::string key = t.key() + "/" + std::to_string(count) + (c->native_allgather ? "/ag" : "");
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     auto p = std::make_shared<Plan>();
-    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get()));
+    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), c->native_allgather));
     if (c->plans.size() > 64) c->plans.clear();
     it = c->plans.emplace(key, p).first;
   }
@@ -181,6 +183,11 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
       }
     }
     if (!st.reduces.empty()) last_red = (long)s;
+  }
+  if (plan.native_allgather) {  // the whole all-gather phase as one collective, in place
+    if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, nchunks - 1), 0));
+    FTAR_RETURN_IF(tp->allgather(bufs[BUF_DST] + (size_t)c->rank * plan.split * esz, bufs[BUF_DST], plan.split * esz,
+                                 c->rank, c->nranks, c->comm_s));
   }
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipEventRecord(ev[2], c->red_s));
@@ -269,6 +276,13 @@ ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes) {
   comm->chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : ftar::kDefaultChunkBytes;
   return FTAR_SUCCESS;
 }
+ftar_status_t ftar_comm_set_native_allgather(ftar_comm_t comm, int on) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->native_allgather = on != 0;
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes) {
   if (!comm || !bytes) return FTAR_ERR_INVALID_ARG;
   *bytes = comm->chunk_bytes;

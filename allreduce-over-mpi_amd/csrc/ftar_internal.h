@@ -71,6 +71,10 @@ struct Plan {
   int rank = 0, nranks = 1;
   size_t count = 0, split = 0;
   std::vector<Stage> stages;
+  // all-gather phase as ONE collective: every non-lonely FlexTree leaves rank r
+  // holding block r, so the reversed stages (mpi_mod.hpp:1620-1644) move the
+  // same bytes as an all-gather of `split` elements at r*split (count % P == 0).
+  bool native_allgather = false;
   size_t scratch_half = 0;  // elements per scratch half (stages alternate halves)
   int max_k = 0;
   std::string json() const;
@@ -78,7 +82,8 @@ struct Plan {
 
 // FMA-level schedule (for tests/introspection), JSON shaped like the reference dump.
 ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t count, std::string* out);
-ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out);
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out,
+                         bool native_allgather = false);
 
 // ---------------------------------------------------------------------------
 // reduce kernels (reduce_kernels.hip)
@@ -100,6 +105,16 @@ class Transport {
   virtual ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) = 0;
   virtual ftar_status_t group_end() = 0;
   virtual const char* name() const = 0;
+  // All-gather of `bytes` per rank: rank r's segment at recv + r*bytes (in place
+  // when send == recv + r*bytes).  Default: one group of p2p sends/receives.
+  virtual ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) {
+    FTAR_RETURN_IF(group_start());
+    for (int p = 0; p < nranks; ++p)
+      if (p != rank) FTAR_RETURN_IF(this->send(send, bytes, p, s));
+    for (int p = 0; p < nranks; ++p)
+      if (p != rank) FTAR_RETURN_IF(this->recv(static_cast<char*>(recv) + (size_t)p * bytes, bytes, p, s));
+    return group_end();
+  }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {

@@ -337,7 +337,7 @@ ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t coun
   return FTAR_SUCCESS;
 }
 
-ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out) {
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, bool native_allgather) {
   if (rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
   Plan p;
   p.rank = rank;
@@ -401,8 +401,9 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
                      &u, &max_k);
       p.stages.push_back(std::move(st));
     }
-    // all-gather: receive straight into dst (mpi_mod.hpp:1620-1644)
-    for (size_t i = k; i < 2 * k; ++i) {
+    // all-gather: receive straight into dst (mpi_mod.hpp:1620-1644), or one collective
+    p.native_allgather = native_allgather && t.lonely == 0 && count % P == 0;
+    for (size_t i = k; i < 2 * k && !p.native_allgather; ++i) {
       Stage st;
       for (const MemStage* ms : {at(f.send, i), at(f.send_l, i)})
         if (ms)
@@ -429,7 +430,8 @@ std::string Plan::json() const {
   std::ostringstream os;
   static const char* bn[] = {"src", "dst", "scratch"};
   os << "{\"rank\":" << rank << ",\"nranks\":" << nranks << ",\"count\":" << count << ",\"split\":" << split
-     << ",\"scratch_half\":" << scratch_half << ",\"max_k\":" << max_k << ",\"stages\":[";
+     << ",\"scratch_half\":" << scratch_half << ",\"max_k\":" << max_k
+     << ",\"native_allgather\":" << (native_allgather ? 1 : 0) << ",\"stages\":[";
   for (size_t i = 0; i < stages.size(); ++i) {
     const Stage& s = stages[i];
     os << (i ? "," : "") << "{\"sends\":[";

@@ -66,6 +66,12 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "rccl"; }
+  ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) override {
+    (void)rank;
+    (void)nranks;
+    FTAR_CHECK_NCCL(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
+    return FTAR_SUCCESS;
+  }
   ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                  hipStream_t s) override {
     ncclDataType_t t;

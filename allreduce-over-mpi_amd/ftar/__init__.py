@@ -103,7 +103,8 @@ _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), 
                                       ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
 _lib.ftar_schedule_json.restype = ctypes.c_long
-_lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _sz, ctypes.c_char_p, _sz]
+_lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _int, ctypes.c_char_p, _sz]
+_lib.ftar_comm_set_native_allgather.argtypes = [_vp, _int]
 _lib.ftar_plan_json.restype = ctypes.c_long
 
 
@@ -236,13 +237,13 @@ def schedule_json(t, nranks, rank, count):
     return json.loads(buf.value.decode())
 
 
-def plan_json(t, nranks, rank, count, esz=4):
+def plan_json(t, nranks, rank, count, native_allgather=False):
     t = topo(t)
-    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, esz, None, 0)
+    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, int(native_allgather), None, 0)
     if n < 0:
         raise FtarError(-n, "ftar_plan_json")
     buf = ctypes.create_string_buffer(n + 1)
-    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, esz, buf, n + 1)
+    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, int(native_allgather), buf, n + 1)
     return json.loads(buf.value.decode())
 
 
@@ -294,6 +295,15 @@ class Comm:
                                  _stream(stream))
         _check(st, "ftar_allreduce")
 
+    @property
+    def native_allgather(self):
+        return getattr(self, "_native_ag", False)
+
+    @native_allgather.setter
+    def native_allgather(self, on):
+        _check(_lib.ftar_comm_set_native_allgather(self.handle, int(bool(on))), "native_allgather")
+        self._native_ag = bool(on)
+
     def rccl_allreduce(self, sendbuf, recvbuf, count, dtype="f32", op="sum", stream=None):
         """RCCL's own ncclAllReduce on this communicator (comparison yardstick)."""
         st = _lib.ftar_rccl_allreduce(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), self.handle,
@@ -321,6 +331,10 @@ class LocalGroup:
     def set_chunk_bytes(self, b):
         for c in self.comms:
             c.chunk_bytes = b
+
+    def set_native_allgather(self, on):
+        for c in self.comms:
+            c.native_allgather = on
 
     def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None):
         P = len(self.comms)

@@ -229,8 +229,9 @@ def bench_distributed(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / max(1, steps) * 1e3
 
-    def run_with(topo, chunk):
+    def run_with(topo, chunk, native_ag=False):
         comm.chunk_bytes = chunk
+        comm.native_allgather = native_ag
         return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
 
     # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
@@ -250,17 +251,21 @@ def bench_distributed(a):
         if key in seen:
             continue
         seen.add(key)
-        for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
-            ms_ = timed(run_with(t, chunk), steps=min(5, a.steps), warmup=1)
-            sweep.append({"topology": key, "chunk_bytes": chunk, "ms": round(ms_, 4),
-                          "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
+        # all-gather phase: p2p stages, or one collective (non-lonely trees, P | n)
+        ags = [False] + ([True] if (not t.ring and n % world == 0 and world > 1) else [])
+        for ag in ags:
+            for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
+                ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
+                sweep.append({"topology": key, "chunk_bytes": chunk, "native_allgather": ag, "ms": round(ms_, 4),
+                              "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
     best = min(sweep, key=lambda r: r["ms"])
     best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
 
-    # headline: the swept-best (topology, chunk), K timed steps after W warmup
-    ms = timed(run_with(best_topo, best["chunk_bytes"]), a.steps, a.warmup)
+    # headline: the swept-best configuration, K timed steps after W warmup
+    ms = timed(run_with(best_topo, best["chunk_bytes"], best["native_allgather"]), a.steps, a.warmup)
     ms_default = timed(run_with(default_topo, default_chunk), min(a.steps, 10), 1)
     comm.chunk_bytes = best["chunk_bytes"]
+    comm.native_allgather = best["native_allgather"]
     comm.allreduce(x, y, n, a.dtype, "sum", topo_=best_topo, stream=stream)
     torch.cuda.synchronize()
 
@@ -302,7 +307,8 @@ def bench_distributed(a):
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
             "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
-                       "chunk_bytes": best["chunk_bytes"], "selection": "best of sweep (FT_TOPO x chunk)",
+                       "chunk_bytes": best["chunk_bytes"], "native_allgather": best["native_allgather"],
+                       "selection": "best of sweep (FT_TOPO x chunk x all-gather form)",
                        "parallelism": f"dp{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",

@@ -135,6 +135,11 @@ ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device);
 /* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = default. */
 ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes);
 ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
+/* Run a non-lonely tree's all-gather phase (mpi_mod.hpp:1620-1644) as ONE
+ * all-gather collective (ncclAllGather on RCCL) instead of k stages of p2p
+ * groups.  Same bytes moved, identical results; needs count % P == 0 (else the
+ * stages are kept).  Default off, or FTAR_NATIVE_ALLGATHER=1 at init. */
+ftar_status_t ftar_comm_set_native_allgather(ftar_comm_t comm, int on);
 
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
@@ -159,8 +164,9 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
  * FMA-level schedule of `rank` (same JSON shape as the reference dump in
  * tests/golden/schedules.jsonl). Returns needed length, or <0 on error. */
 long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, char* buf, size_t buflen);
-/* Executable plan summary: stages, transfers, reduces, scratch bytes (JSON). */
-long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, size_t esz, char* buf,
+/* Executable plan of `rank` (JSON): stages of transfers/reduces, scratch size,
+ * and whether the all-gather phase is one collective. */
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, int native_allgather, char* buf,
                     size_t buflen);
 
 #ifdef __cplusplus

@@ -32,9 +32,10 @@ def group(P):
     return _groups[P]
 
 
-def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1):
+def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1, native_ag=False):
     g = group(len(ins))
     g.set_chunk_bytes(chunk_bytes)
+    g.set_native_allgather(native_ag)
     n = ins[0].size
     send = [to_dev(x) for x in ins]
     if outofplace:
@@ -115,3 +116,15 @@ def test_rccl_single_rank_comm():
         np.testing.assert_array_equal(from_dev(d, np.float32, 1000), x)
     finally:
         comm.destroy()
+
+
+@pytest.mark.parametrize("P,topo", [(2, "2"), (4, "2,2"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3")])
+@pytest.mark.parametrize("outofplace", [False, True])
+def test_allreduce_native_allgather(P, topo, outofplace):
+    """All-gather phase as one collective (p2p-group fallback on the local transport): bit-exact."""
+    n = P * 12_345
+    ins = [fi.fill("f32", 12, r, n) for r in range(P)]
+    outs = run_group(ins, topo, outofplace=outofplace, chunk_bytes=1 << 16, native_ag=True)
+    ref = oracle_lib.allreduce(ins, topo, outofplace=outofplace)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))

@@ -59,6 +59,12 @@ def simulate(plans, inputs, dtype, op, outofplace):
                 srcs = [bufs[r][it["own"]][off:off + ln]] + [bufs[r]["scratch"][so:so + ln] for so in it["scratch"]]
                 out = oracle_lib.reduce(dtype, op, [np.ascontiguousarray(x) for x in srcs])
                 bufs[r]["dst"][off:off + ln] = out
+    if plans[0]["native_allgather"]:  # one all-gather: rank p contributes dst[p*split : (p+1)*split]
+        split = plans[0]["split"]
+        segs = [dst[p][p * split:(p + 1) * split].copy() for p in range(P)]
+        for r in range(P):
+            for p in range(P):
+                dst[r][p * split:(p + 1) * split] = segs[p]
     return dst
 
 
@@ -89,3 +95,23 @@ def test_scratch_is_compact():
     tree = ftar.plan_json("8", 8, 3, n)
     assert tree["scratch_half"] == 7 * (n // 8)
     assert tree["max_k"] == 8
+
+
+@pytest.mark.parametrize("P,topo", [(2, "2"), (4, "4"), (4, "2,2"), (6, "2,3"), (8, "8"), (8, "2,4"), (8, "4,2"),
+                                    (8, "2,2,2"), (9, "3,3")])
+def test_native_allgather_plans_match_oracle(P, topo):
+    """Every non-lonely FlexTree leaves rank r holding block r, so the all-gather phase may be one
+    collective (ftar_comm_set_native_allgather): same result, bit for bit."""
+    import ftar
+    n = P * 1001
+    ins = [fi.fill("f32", 404, r, n) for r in range(P)]
+    plans = [ftar.plan_json(topo, P, r, n, native_allgather=True) for r in range(P)]
+    assert all(p["native_allgather"] for p in plans)
+    assert len(plans[0]["stages"]) == len(topo.split(","))      # reduce-scatter stages only
+    outs = simulate(plans, ins, 6, 0, False)
+    ref = oracle_lib.allreduce(ins, topo)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+    # not applicable: ragged counts, lonely ranks and the ring keep their stages
+    assert not ftar.plan_json(topo, P, 0, n + 1, native_allgather=True)["native_allgather"]
+    assert not ftar.plan_json("1", P, 0, n, native_allgather=True)["native_allgather"]
