@@ -255,10 +255,16 @@ def bench_distributed(a):
         ags = [False] + ([True] if (not t.ring and n % world == 0 and world > 1) else [])
         for ag in ags:
             for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
-                ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
+                try:
+                    ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
+                except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
+                    sweep.append({"topology": key, "chunk_bytes": chunk, "native_allgather": ag, "error": str(e)[:200]})
+                    continue
                 sweep.append({"topology": key, "chunk_bytes": chunk, "native_allgather": ag, "ms": round(ms_, 4),
                               "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
-    best = min(sweep, key=lambda r: r["ms"])
+    ok_runs = [r for r in sweep if "ms" in r]
+    best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else {
+        "topology": str(default_topo), "chunk_bytes": default_chunk, "native_allgather": False}
     best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
 
     # headline: the swept-best configuration, K timed steps after W warmup

@@ -118,3 +118,21 @@ def test_reduce_bf16_matches_fp32_reference_within_one_rounding():
         f32 = (f32 + fi.bf16_bits_to_f32(x)).astype(np.float32)
     ulp = np.abs(f32) * 2.0 ** -8 + 1e-30
     assert np.all(np.abs(got - f32) <= ulp)
+
+
+def test_reduce_beyond_int32_index():
+    """2^31 + 77 elements (the reference kernel indexes with `int`, vector_add/reduce_sum_gpu.h:8):
+    u8 sums wrap, checked on a head, a window across the 2^31 boundary and the tail."""
+    import ftar
+    import torch
+    n = (1 << 31) + 77
+    a = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    b = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    out = torch.empty_like(a)
+    ftar.reduce([a.data_ptr(), b.data_ptr()], out.data_ptr(), n, "u8", "sum")
+    torch.cuda.synchronize()
+    for lo, hi in ((0, 1 << 16), ((1 << 31) - (1 << 15), (1 << 31) + (1 << 15)), (n - (1 << 16), n)):
+        exp = oracle_lib.reduce(0, 0, [a[lo:hi].cpu().numpy(), b[lo:hi].cpu().numpy()])
+        np.testing.assert_array_equal(out[lo:hi].cpu().numpy(), exp)
+    # full-size property: sum of all bytes is preserved mod 2^8 per element -> compare checksums
+    assert int(((a.to(torch.int64) + b.to(torch.int64)) % 256).sum()) == int(out.to(torch.int64).sum())
