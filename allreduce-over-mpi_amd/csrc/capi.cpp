@@ -41,7 +41,7 @@ namespace {
 // override them.
 // ---------------------------------------------------------------------------
 struct CostConsts {
-  double alpha = 20e-6, link = 48e9, hbm = 5.0e12;
+  double alpha = 20e-6, link = 48e9, hbm = 6.3e12;  // hbm: measured k=2..8 reduce (profiles/r01/kbench3)
   CostConsts() {
     if (const char* e = getenv("FTAR_COST_ALPHA_US")) alpha = atof(e) * 1e-6;
     if (const char* e = getenv("FTAR_COST_LINK_GBPS")) link = atof(e) * 1e9;

@@ -17,7 +17,6 @@ raises at import time.
 import ctypes
 import json
 import os
-import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FTAR_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libftar.so"))
