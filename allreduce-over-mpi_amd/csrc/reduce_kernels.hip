@@ -248,6 +248,58 @@ __global__ void __launch_bounds__(BS)
   }
 }
 
+// LDS-staged variant (A/B only, tools/kbench.py variants 20-22): each wave
+// streams its sources into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB
+// per wave instruction, no VGPR destination), waits on its own vmcnt, then
+// every lane reads back its own 16 B with ds_read_b128 and folds.  On an
+// element-wise reduce nothing is shared between lanes, so LDS only replaces
+// VGPRs as the landing zone of the loads; measured against the register path
+// in DESIGN.md §3.
+template <class Tr, int K, int U, int AUX>
+__global__ void __launch_bounds__(256) reduce_lds_kernel(Srcs<K> src, void* __restrict__ dst, size_t nvec) {
+  __shared__ u32x4 lds[4][K][U][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t base = ((size_t)blockIdx.x * 4 + wave) * (U * 64);
+  u32x4* d = static_cast<u32x4*>(dst);
+  if (base + U * 64 <= nvec) {
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const u32x4* g = static_cast<const u32x4*>(src.p[j]) + base + u * 64 + lane;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                         (__attribute__((address_space(3))) void*)&lds[wave][j][u][0], 16, 0, AUX);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      typename Tr::VA a = Tr::v_init(lds[wave][0][u][lane]);
+#pragma unroll
+      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, lds[wave][j][u][lane]);
+      d[base + u * 64 + lane] = Tr::v_fin(a);
+    }
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const size_t v = base + u * 64 + lane;
+      if (v >= nvec) break;
+      typename Tr::VA a = Tr::v_init(static_cast<const u32x4*>(src.p[0])[v]);
+      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, static_cast<const u32x4*>(src.p[j])[v]);
+      d[v] = Tr::v_fin(a);
+    }
+  }
+}
+
+template <class Tr, int K, int U, int AUX>
+hipError_t launch_lds(const void* const* srcs, void* dst, size_t nvec, hipStream_t s) {
+  Srcs<K> a{};
+  for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
+  const size_t per_block = (size_t)4 * U * 64;
+  const size_t blocks = (nvec + per_block - 1) / per_block;
+  hipLaunchKernelGGL((reduce_lds_kernel<Tr, K, U, AUX>), dim3((unsigned)(blocks ? blocks : 1)), dim3(256), 0, s, a,
+                     dst, nvec);
+  return hipGetLastError();
+}
+
 // element-wise fallback for sources not co-aligned with dst
 template <class Tr>
 __global__ void __launch_bounds__(kThreads)
@@ -350,6 +402,9 @@ hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nv
     case 9: return launch_cfg<Tr, K, 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
     case 10: return launch_cfg<Tr, K, 1, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 11: return launch_cfg<Tr, K, 4, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 20: return launch_lds<Tr, K, 2, 2>(srcs, dst, nvec, s);  // LDS-DMA, nt
+    case 21: return launch_lds<Tr, K, 4, 2>(srcs, dst, nvec, s);
+    case 22: return launch_lds<Tr, K, 2, 0>(srcs, dst, nvec, s);  // LDS-DMA, default policy
   }
   return hipErrorInvalidValue;
 }
