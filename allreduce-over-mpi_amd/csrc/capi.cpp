@@ -152,6 +152,8 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   ftar::Topology chk;
   ftar_status_t st = ftar::to_topology(&t, nranks, &chk);
   if (st != FTAR_SUCCESS) return st;
+  if (chk.lonely && ftar::check_world(chk, nranks, (size_t)nranks * 64, false) != FTAR_SUCCESS)
+    return FTAR_ERR_INVALID_TOPO;  // a lonely layout the reference cannot run (its asserts / a blocked Waitall)
   *out = t;
   return FTAR_SUCCESS;
 }

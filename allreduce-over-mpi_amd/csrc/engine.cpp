@@ -111,6 +111,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     auto p = std::make_shared<Plan>();
+    FTAR_RETURN_IF(check_world(t, c->nranks, count, c->native_allgather));  // once per (topology, count)
     FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), c->native_allgather));
     if (c->plans.size() > 64) c->plans.clear();
     it = c->plans.emplace(key, p).first;

@@ -84,6 +84,8 @@ struct Plan {
 ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t count, std::string* out);
 ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out,
                          bool native_allgather = false);
+// All ranks' plans pair up stage by stage (else FTAR_ERR_INVALID_TOPO).
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, bool native_allgather);
 
 // ---------------------------------------------------------------------------
 // reduce kernels (reduce_kernels.hip)

@@ -95,14 +95,17 @@ class Tree {
   bool lonely_rank() const { return me_ >= S_; }
 
   // Send_Operations::generate / Recv_Operations::generate, per stage.
-  void build(std::vector<PeerList>* send, std::vector<PeerList>* send_l, std::vector<PeerList>* recv,
+  // false where the reference would assert (followers > 1, mpi_mod.hpp:281, :366, :444)
+  bool build(std::vector<PeerList>* send, std::vector<PeerList>* send_l, std::vector<PeerList>* recv,
              std::vector<PeerList>* recv_l) const {
+    bool ok = true;
     if (!lonely_rank()) {
       for (size_t i = 0, g = 1; i < stages(); g *= w_[i], ++i) {
         const size_t G = g * w_[i];
         const size_t first = me_ / G * G + me_ % g;  // smallest rank of my stage-i group
         const std::vector<size_t> mine = residues(me_, G);
         const auto my_followers = followers(i + 1, me_);
+        if (my_followers.size() > 1) ok = false;
         PeerList s, sl, r, rl;
         for (size_t j = 0; j < w_[i]; ++j) {
           const size_t p = first + j * g;
@@ -110,6 +113,7 @@ class Tree {
           r.push_back({p, mine});
           if (owns_lonely(i, me_)) {
             auto f = followers(i + 1, p);
+            if (f.size() > 1) ok = false;
             if (f.size() == 1) sl.push_back(i + 1 < stages() ? Peer{p, {f[0]}} : Peer{f[0], {f[0]}});
           }
           if (!my_followers.empty() && owns_lonely(i, p) && i + 1 < stages()) rl.push_back({p, {my_followers[0]}});
@@ -146,9 +150,13 @@ class Tree {
       }
       PeerList& last = recv_l->back();
       const long step = (long)(S_ / w_.back());
-      for (long i = (long)me_ - (long)w_[0]; i >= 0; i -= step)
-        if (followers(stages() - 1, (size_t)i).size() == 1) last.push_back({(size_t)i, {me_}});
+      for (long i = (long)me_ - (long)w_[0]; i >= 0; i -= step) {
+        auto f = followers(stages() - 1, (size_t)i);
+        if (f.size() == 1 && f[0] != me_) ok = false;
+        if (f.size() == 1) last.push_back({(size_t)i, {me_}});
+      }
     }
+    return ok;
   }
 
  private:
@@ -209,9 +217,10 @@ Range block_range(size_t b, size_t P, size_t count) {
 }
 
 // FMA lowering (mpi_mod.hpp:635-689, :699-765)
-Fma lower(const Topology& t, size_t P, size_t me, size_t count) {
+Fma lower(const Topology& t, size_t P, size_t me, size_t count, bool* ok = nullptr) {
   std::vector<PeerList> S, SL, R, RL;
-  Tree(t, P, me).build(&S, &SL, &R, &RL);
+  const bool good = Tree(t, P, me).build(&S, &SL, &R, &RL);
+  if (ok) *ok = good;
   const size_t k = t.widths.size();
   const size_t split = (count + P - 1) / P;
   auto as_sends = [&](const PeerList& pl, bool from_src) {
@@ -381,7 +390,9 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
     half = p.split;
     p.max_k = 2;
   } else {
-    Fma f = lower(t, P, me, count);
+    bool good = true;
+    Fma f = lower(t, P, me, count, &good);
+    if (!good) return FTAR_ERR_INVALID_TOPO;
     const size_t k = t.widths.size();
     auto at = [](const std::vector<MemStage>& v, size_t i) -> const MemStage* { return i < v.size() ? &v[i] : nullptr; };
     // pass 1: scratch needed per reduce-scatter stage
@@ -423,6 +434,31 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
   }
   p.scratch_half = half;
   *out = std::move(p);
+  return FTAR_SUCCESS;
+}
+
+// Every rank's plan, built here, must pair up: per stage and per (sender,
+// receiver), the sender's transfers to the receiver and the receiver's
+// transfers from the sender have the same lengths in the same order (RCCL and
+// MPI match p2p messages per peer pair in posting order).  Topologies the
+// reference cannot run (its asserts, or schedules that would block in
+// MPI_Waitall) fail here instead of hanging a collective.
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, bool native_allgather) {
+  std::vector<Plan> plans(nranks);
+  for (int r = 0; r < nranks; ++r) FTAR_RETURN_IF(build_plan(t, nranks, r, count, &plans[r], native_allgather));
+  for (int r = 1; r < nranks; ++r)
+    if (plans[r].stages.size() != plans[0].stages.size()) return FTAR_ERR_INVALID_TOPO;
+  for (size_t s = 0; s < plans[0].stages.size(); ++s)
+    for (int a = 0; a < nranks; ++a)
+      for (int b = 0; b < nranks; ++b) {
+        if (a == b) continue;
+        std::vector<size_t> sent, got;
+        for (const Transfer& x : plans[a].stages[s].sends)
+          if (x.peer == b) sent.push_back(x.len);
+        for (const Transfer& x : plans[b].stages[s].recvs)
+          if (x.peer == a) got.push_back(x.len);
+        if (sent != got) return FTAR_ERR_INVALID_TOPO;
+      }
   return FTAR_SUCCESS;
 }
 

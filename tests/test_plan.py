@@ -115,3 +115,44 @@ def test_native_allgather_plans_match_oracle(P, topo):
     # not applicable: ragged counts, lonely ranks and the ring keep their stages
     assert not ftar.plan_json(topo, P, 0, n + 1, native_allgather=True)["native_allgather"]
     assert not ftar.plan_json("1", P, 0, n, native_allgather=True)["native_allgather"]
+
+
+def test_random_plans_match_oracle():
+    """200 seeded random cases: topologies incl. lonely, ragged sizes, every dtype, SUM/BAND, in/out of place."""
+    import ftar
+    import random_cases
+    for c in random_cases.cases(seed=2024, count=200):
+        P = c["P"]
+        t = ftar.topo(c["topo"], c["lonely"])
+        plans = [ftar.plan_json(t, P, r, c["n"]) for r in range(P)]
+        outs = simulate(plans, c["ins"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1, c["oop"])
+        for r in range(P):
+            assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"], r)
+
+
+def test_product_rejects_exactly_the_topologies_the_reference_cannot_run():
+    """Lonely layouts where the reference asserts (followers > 1) or would block: the product refuses them
+    (FTAR_ERR_INVALID_TOPO) instead of posting a schedule that hangs; every other layout builds."""
+    import random
+    import ftar
+    import random_cases
+    rng = random.Random(5)
+    seen = set()
+    for _ in range(400):
+        P = rng.randint(2, 13)
+        topo, lonely = random_cases.random_topology(rng, P)
+        if (P, topo, lonely) in seen:
+            continue
+        seen.add((P, topo, lonely))
+        ins = [fi.fill("f32", 1, r, 97) for r in range(P)]
+        try:
+            oracle_lib.allreduce(ins, topo, lonely)
+            ref_ok = True
+        except RuntimeError:
+            ref_ok = False
+        try:
+            ftar.topo_parse(topo, str(lonely), P)
+            prod_ok = True
+        except ftar.FtarError:
+            prod_ok = False
+        assert ref_ok == prod_ok, (P, topo, lonely, ref_ok, prod_ok)
