@@ -225,6 +225,18 @@ ftar_status_t ftar_comm_init_rank(ftar_comm_t* comm, int nranks, ftar_unique_id_
 
 ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* devices) {
   if (!comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  // ranks on different GPUs of this process copy straight over xGMI
+  for (int a = 0; devices && a < nranks; ++a)
+    for (int b = 0; b < nranks; ++b) {
+      if (devices[a] == devices[b]) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can) {
+        FTAR_CHECK_HIP(hipSetDevice(devices[a]));
+        hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) FTAR_CHECK_HIP(e);
+        (void)hipGetLastError();
+      }
+    }
   auto hub = ftar::make_local_hub(nranks);
   std::vector<ftar_comm*> made;
   for (int r = 0; r < nranks; ++r) {
