@@ -142,8 +142,8 @@ def bench_single(a):
             for h in host[1:]:
                 exp = (exp + h[lo:lo + m]).astype(np.float32)
             ok &= bool(np.array_equal(got[lo:lo + m].view(np.uint32), exp.view(np.uint32)))
-    del host
         check = "bit-exact" if ok else "MISMATCH"
+    del host
 
     workload = f"reduce_k{k}_{a.dtype}_n{n}"
     res = {
