@@ -150,10 +150,19 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev[0], 0));
 
   long last_red = -1;
+  long half_owner[2] = {-1, -1};  // last reducing stage that read each scratch half
   std::vector<const void*> srcs;
   for (size_t s = 0; s < nst; ++s) {
     const Stage& st = plan.stages[s];
     const bool moves = !st.sends.empty() || !st.recvs.empty();
+    bool to_scratch = false;
+    for (const Transfer& x : st.recvs) to_scratch |= x.buf == BUF_SCRATCH;
+    // WAR on the scratch half this stage receives into: every reduce that read it
+    // (stage s-2, or earlier when stages in between were empty) must be done.
+    // When stage s-1 reduced, its piece-0 event already implies this (the reduce
+    // stream runs in order), so the wait is free; it matters when s-1 was empty.
+    if (to_scratch && half_owner[s % 2] >= 0)
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)half_owner[s % 2], nchunks - 1), 0));
     for (size_t k = 0; k < nchunks; ++k) {
       const size_t lo = k * chunk;
       if (moves) {
@@ -183,7 +192,10 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
         FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
       }
     }
-    if (!st.reduces.empty()) last_red = (long)s;
+    if (!st.reduces.empty()) {
+      last_red = (long)s;
+      if (to_scratch) half_owner[s % 2] = (long)s;
+    }
   }
   if (plan.native_allgather) {  // the whole all-gather phase as one collective, in place
     if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, nchunks - 1), 0));
