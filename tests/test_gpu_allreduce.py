@@ -138,3 +138,15 @@ def test_random_cases_through_engine():
                          c["oop"], chunk_bytes=c["chunk"])
         for r in range(c["P"]):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"], r)
+
+
+@pytest.mark.parametrize("P,topo,lonely", [(13, "2,2,3", 1), (17, "2,2,2,2", 1), (18, "2,2,2,2", 2), (25, "2,2,2,3", 1)])
+def test_allreduce_deep_lonely_trees(P, topo, lonely):
+    """Lonely ranks with empty intermediate stages (scratch halves reused across an empty stage), many ranks,
+    tiny pipeline pieces: bit-exact vs the oracle."""
+    n = 100_003
+    ins = [fi.fill("f32", 91, r, n) for r in range(P)]
+    outs = run_group(ins, topo, lonely, chunk_bytes=256)
+    ref = oracle_lib.allreduce(ins, topo, lonely)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))

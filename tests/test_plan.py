@@ -156,3 +156,15 @@ def test_product_rejects_exactly_the_topologies_the_reference_cannot_run():
         except ftar.FtarError:
             prod_ok = False
         assert ref_ok == prod_ok, (P, topo, lonely, ref_ok, prod_ok)
+
+
+@pytest.mark.parametrize("P,topo,lonely", [(13, "2,2,3", 1), (17, "2,2,2,2", 1), (18, "2,2,2,2", 2), (33, "2,2,2,2,2", 1)])
+def test_deep_lonely_plans_match_oracle(P, topo, lonely):
+    import ftar
+    n = 4099
+    ins = [fi.fill("f32", 93, r, n) for r in range(P)]
+    plans = [ftar.plan_json(ftar.topo(topo, lonely), P, r, n) for r in range(P)]
+    outs = simulate(plans, ins, 6, 0, False)
+    ref = oracle_lib.allreduce(ins, topo, lonely)
+    for r in range(P):
+        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
