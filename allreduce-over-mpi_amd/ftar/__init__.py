@@ -303,6 +303,20 @@ class Comm:
         _check(_lib.ftar_comm_set_native_allgather(self.handle, int(bool(on))), "native_allgather")
         self._native_ag = bool(on)
 
+    def allreduce_tensor(self, tensor, out=None, op="sum", topo_=None, lonely=0, stream=None):
+        """In-place (out=None) or out-of-place AllReduce of a contiguous device tensor,
+        e.g. a data-parallel gradient bucket; dtype and count come from the tensor."""
+        if not tensor.is_contiguous() or (out is not None and not out.is_contiguous()):
+            raise ValueError("ftar needs contiguous tensors")
+        if out is not None and (out.numel() != tensor.numel() or out.dtype != tensor.dtype):
+            raise ValueError("out must match tensor in size and dtype")
+        dt = _dt(str(tensor.dtype))
+        if out is None:
+            self.allreduce(None, tensor, tensor.numel(), dt, op, topo_, lonely, stream)
+            return tensor
+        self.allreduce(tensor, out, tensor.numel(), dt, op, topo_, lonely, stream)
+        return out
+
     def rccl_allreduce(self, sendbuf, recvbuf, count, dtype="f32", op="sum", stream=None):
         """RCCL's own ncclAllReduce on this communicator (comparison yardstick)."""
         st = _lib.ftar_rccl_allreduce(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), self.handle,
@@ -344,6 +358,14 @@ class LocalGroup:
         ss = None if streams is None else (_vp * P)(*[_stream(s) for s in streams])
         st = _lib.ftar_allreduce_group(sb, rb, count, _dt(dtype), _op(op), t, hs, P, ss)
         _check(st, "ftar_allreduce_group")
+
+    def allreduce_tensors(self, tensors, op="sum", topo_=None, lonely=0):
+        """In-place AllReduce of one contiguous device tensor per rank (same shape and dtype)."""
+        t0 = tensors[0]
+        if any(not t.is_contiguous() or t.numel() != t0.numel() or t.dtype != t0.dtype for t in tensors):
+            raise ValueError("tensors must be contiguous and alike")
+        self.allreduce(None, tensors, t0.numel(), _dt(str(t0.dtype)), op, topo_, lonely)
+        return tensors
 
     def destroy(self):
         for c in self.comms:

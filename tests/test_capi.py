@@ -137,3 +137,17 @@ def test_mpi_library_exports_ftar_mpi_h():
     import ftar  # noqa: F401  (loads libftar.so first, as the loader would)
     lib = ctypes.CDLL(lib_path)
     assert all(hasattr(lib, n) for n in names), names
+
+
+def test_header_is_plain_c99(tmp_path):
+    """include/ftar.h compiles as C99 and links against libftar.so (the FFI boundary needs no C++)."""
+    import subprocess
+    import ftar  # noqa: F401  (library is built)
+    lib_dir = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib")
+    exe = str(tmp_path / "abi_c99")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "c", "abi_c99.c"), "-o", exe, "-L", lib_dir, "-lftar",
+                    f"-Wl,-rpath,{lib_dir}"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, (out.returncode, out.stdout, out.stderr)
+    assert "c99 ok" in out.stdout

@@ -150,3 +150,22 @@ def test_allreduce_deep_lonely_trees(P, topo, lonely):
     ref = oracle_lib.allreduce(ins, topo, lonely)
     for r in range(P):
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+
+
+def test_tensor_api_bf16_and_f32():
+    """LocalGroup.allreduce_tensors / Comm.allreduce_tensor on torch tensors (dtype and count from the tensor)."""
+    import torch
+    g = group(4)
+    g.set_chunk_bytes(0)
+    g.set_native_allgather(False)
+    for dt, name in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        xs = [fi.fill(name, 3, r, 5000) for r in range(4)]
+        ts = [torch.from_numpy(x.view(np.int16) if name == "bf16" else x).cuda().view(dt) for x in xs]
+        g.allreduce_tensors(ts, topo_="2,2")
+        torch.cuda.synchronize()
+        ref = oracle_lib.allreduce(xs, "2,2", dtype=fi.BY_NAME[name])
+        for r in range(4):
+            got = ts[r].view(torch.int16 if name == "bf16" else torch.int32).cpu().numpy()
+            assert got.tobytes() == ref[r].tobytes()
+    with pytest.raises(ValueError):
+        g.allreduce_tensors([torch.zeros(4, device="cuda"), torch.zeros(5, device="cuda")] * 2)
