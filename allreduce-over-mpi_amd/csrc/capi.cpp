@@ -152,7 +152,7 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   ftar::Topology chk;
   ftar_status_t st = ftar::to_topology(&t, nranks, &chk);
   if (st != FTAR_SUCCESS) return st;
-  if (chk.lonely && ftar::check_world(chk, nranks, (size_t)nranks * 64, false) != FTAR_SUCCESS)
+  if (chk.lonely && ftar::check_world(chk, nranks, (size_t)nranks * 64, FTAR_AG_STAGES) != FTAR_SUCCESS)
     return FTAR_ERR_INVALID_TOPO;  // a lonely layout the reference cannot run (its asserts / a blocked Waitall)
   *out = t;
   return FTAR_SUCCESS;
@@ -265,12 +265,12 @@ long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t co
   return emit(s, buf, buflen);
 }
 
-long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, int native_allgather, char* buf,
-                    size_t buflen) {
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, ftar_allgather_t allgather,
+                    char* buf, size_t buflen) {
   ftar::Topology t;
   if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -FTAR_ERR_INVALID_TOPO;
   ftar::Plan p;
-  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p, native_allgather != 0);
+  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p, allgather);
   if (st != FTAR_SUCCESS) return -(long)st;
   return emit(p.json(), buf, buflen);
 }

@@ -33,7 +33,7 @@ struct ftar_comm {
   size_t scratch_bytes = 0;
   size_t chunk_bytes = 0;
   bool auto_topo = true;
-  bool native_allgather = false;
+  int allgather = FTAR_AG_DIRECT;
   ftar::Topology topo;
   std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
   std::vector<hipEvent_t> events;
@@ -59,7 +59,10 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
-  if (const char* na = getenv("FTAR_NATIVE_ALLGATHER")) c->native_allgather = atoi(na) != 0;
+  if (const char* ag = getenv("FTAR_ALLGATHER")) {
+    const std::string m(ag);
+    c->allgather = m == "stages" ? FTAR_AG_STAGES : m == "collective" ? FTAR_AG_COLLECTIVE : FTAR_AG_DIRECT;
+  }
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
   if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
@@ -107,12 +110,12 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
     FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
   }
-  const std::string key = t.key() + "/" + std::to_string(count) + (c->native_allgather ? "/ag" : "");
+  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(c->allgather);
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     auto p = std::make_shared<Plan>();
-    FTAR_RETURN_IF(check_world(t, c->nranks, count, c->native_allgather));  // once per (topology, count)
-    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), c->native_allgather));
+    FTAR_RETURN_IF(check_world(t, c->nranks, count, c->allgather));  // once per (topology, count, form)
+    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), c->allgather));
     if (c->plans.size() > 64) c->plans.clear();
     it = c->plans.emplace(key, p).first;
   }
@@ -197,7 +200,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
       if (to_scratch) half_owner[s % 2] = (long)s;
     }
   }
-  if (plan.native_allgather) {  // the whole all-gather phase as one collective, in place
+  if (plan.allgather == FTAR_AG_COLLECTIVE) {  // the whole all-gather phase as one collective, in place
     if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, nchunks - 1), 0));
     FTAR_RETURN_IF(tp->allgather(bufs[BUF_DST] + (size_t)c->rank * plan.split * esz, bufs[BUF_DST], plan.split * esz,
                                  c->rank, c->nranks, c->comm_s));
@@ -301,10 +304,17 @@ ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes) {
   comm->chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : ftar::kDefaultChunkBytes;
   return FTAR_SUCCESS;
 }
-ftar_status_t ftar_comm_set_native_allgather(ftar_comm_t comm, int on) {
-  if (!comm) return FTAR_ERR_INVALID_ARG;
+ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode) {
+  if (!comm || (mode != FTAR_AG_STAGES && mode != FTAR_AG_COLLECTIVE && mode != FTAR_AG_DIRECT))
+    return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
-  comm->native_allgather = on != 0;
+  comm->allgather = mode;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_get_allgather(ftar_comm_t comm, ftar_allgather_t* mode) {
+  if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  *mode = static_cast<ftar_allgather_t>(comm->allgather);
   return FTAR_SUCCESS;
 }
 

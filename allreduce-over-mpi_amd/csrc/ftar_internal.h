@@ -71,10 +71,9 @@ struct Plan {
   int rank = 0, nranks = 1;
   size_t count = 0, split = 0;
   std::vector<Stage> stages;
-  // all-gather phase as ONE collective: every non-lonely FlexTree leaves rank r
-  // holding block r, so the reversed stages (mpi_mod.hpp:1620-1644) move the
-  // same bytes as an all-gather of `split` elements at r*split (count % P == 0).
-  bool native_allgather = false;
+  // all-gather form actually used (ftar_allgather_t); COLLECTIVE = one
+  // all-gather of `split` elements at r*split after the reduce-scatter stages
+  int allgather = FTAR_AG_STAGES;
   size_t scratch_half = 0;  // elements per scratch half (stages alternate halves)
   int max_k = 0;
   std::string json() const;
@@ -83,9 +82,9 @@ struct Plan {
 // FMA-level schedule (for tests/introspection), JSON shaped like the reference dump.
 ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t count, std::string* out);
 ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out,
-                         bool native_allgather = false);
+                         int allgather = FTAR_AG_STAGES);
 // All ranks' plans pair up stage by stage (else FTAR_ERR_INVALID_TOPO).
-ftar_status_t check_world(const Topology& t, int nranks, size_t count, bool native_allgather);
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, int allgather);
 
 // ---------------------------------------------------------------------------
 // reduce kernels (reduce_kernels.hip)

@@ -346,7 +346,25 @@ ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t coun
   return FTAR_SUCCESS;
 }
 
-ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, bool native_allgather) {
+namespace {
+// One-round all-gather: after the reduce-scatter stages rank q holds the final
+// value of exactly one block, owner_block(q); send mine to every peer, receive
+// each peer's (ascending peer order on both sides, so per-pair FIFO matches).
+Stage direct_allgather_stage(size_t P, size_t me, size_t count, bool ring) {
+  auto owner_block = [&](size_t q) { return ring ? (q + 1) % P : q; };
+  Stage st;
+  const Range mine = block_range(owner_block(me), P, count);
+  for (size_t p = 0; p < P; ++p) {
+    if (p == me) continue;
+    if (mine.len) st.sends.push_back({(int)p, BUF_DST, mine.actual, mine.len});
+    const Range theirs = block_range(owner_block(p), P, count);
+    if (theirs.len) st.recvs.push_back({(int)p, BUF_DST, theirs.actual, theirs.len});
+  }
+  return st;
+}
+}  // namespace
+
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, int allgather) {
   if (rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
   Plan p;
   p.rank = rank;
@@ -378,14 +396,20 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
       bs = (bs + P - 1) % P;
       br = (br + P - 1) % P;
     }
-    for (size_t i = 0; i + 1 < P; ++i) {
-      Stage st;
-      Range s = block_range(bs, P, count), r = block_range(br, P, count);
-      if (s.len) st.sends.push_back({right, BUF_DST, s.actual, s.len});
-      if (r.len) st.recvs.push_back({left, BUF_DST, r.actual, r.len});
-      p.stages.push_back(std::move(st));
-      bs = (bs + P - 1) % P;
-      br = (br + P - 1) % P;
+    if (allgather == FTAR_AG_STAGES) {
+      for (size_t i = 0; i + 1 < P; ++i) {  // mpi_mod.hpp:1705-1715
+        Stage st;
+        Range s = block_range(bs, P, count), r = block_range(br, P, count);
+        if (s.len) st.sends.push_back({right, BUF_DST, s.actual, s.len});
+        if (r.len) st.recvs.push_back({left, BUF_DST, r.actual, r.len});
+        p.stages.push_back(std::move(st));
+        bs = (bs + P - 1) % P;
+        br = (br + P - 1) % P;
+      }
+      p.allgather = FTAR_AG_STAGES;
+    } else {  // the ring's final blocks sit one rank off: no collective layout, go direct
+      p.stages.push_back(direct_allgather_stage(P, me, count, true));
+      p.allgather = FTAR_AG_DIRECT;
     }
     half = p.split;
     p.max_k = 2;
@@ -412,9 +436,15 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
                      &u, &max_k);
       p.stages.push_back(std::move(st));
     }
-    // all-gather: receive straight into dst (mpi_mod.hpp:1620-1644), or one collective
-    p.native_allgather = native_allgather && t.lonely == 0 && count % P == 0;
-    for (size_t i = k; i < 2 * k && !p.native_allgather; ++i) {
+    // all-gather: the reference's reversed stages straight into dst (mpi_mod.hpp:1620-1644),
+    // one direct round, or one collective
+    if (allgather == FTAR_AG_COLLECTIVE && t.lonely == 0 && count % P == 0) p.allgather = FTAR_AG_COLLECTIVE;
+    else if (allgather == FTAR_AG_STAGES) p.allgather = FTAR_AG_STAGES;
+    else {
+      p.allgather = FTAR_AG_DIRECT;
+      p.stages.push_back(direct_allgather_stage(P, me, count, false));
+    }
+    for (size_t i = k; i < 2 * k && p.allgather == FTAR_AG_STAGES; ++i) {
       Stage st;
       for (const MemStage* ms : {at(f.send, i), at(f.send_l, i)})
         if (ms)
@@ -443,9 +473,9 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
 // MPI match p2p messages per peer pair in posting order).  Topologies the
 // reference cannot run (its asserts, or schedules that would block in
 // MPI_Waitall) fail here instead of hanging a collective.
-ftar_status_t check_world(const Topology& t, int nranks, size_t count, bool native_allgather) {
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, int allgather) {
   std::vector<Plan> plans(nranks);
-  for (int r = 0; r < nranks; ++r) FTAR_RETURN_IF(build_plan(t, nranks, r, count, &plans[r], native_allgather));
+  for (int r = 0; r < nranks; ++r) FTAR_RETURN_IF(build_plan(t, nranks, r, count, &plans[r], allgather));
   for (int r = 1; r < nranks; ++r)
     if (plans[r].stages.size() != plans[0].stages.size()) return FTAR_ERR_INVALID_TOPO;
   for (size_t s = 0; s < plans[0].stages.size(); ++s)
@@ -467,7 +497,8 @@ std::string Plan::json() const {
   static const char* bn[] = {"src", "dst", "scratch"};
   os << "{\"rank\":" << rank << ",\"nranks\":" << nranks << ",\"count\":" << count << ",\"split\":" << split
      << ",\"scratch_half\":" << scratch_half << ",\"max_k\":" << max_k
-     << ",\"native_allgather\":" << (native_allgather ? 1 : 0) << ",\"stages\":[";
+     << ",\"allgather\":\"" << (allgather == FTAR_AG_COLLECTIVE ? "collective" : allgather == FTAR_AG_DIRECT ? "direct" : "stages")
+     << "\",\"stages\":[";
   for (size_t i = 0; i < stages.size(); ++i) {
     const Stage& s = stages[i];
     os << (i ? "," : "") << "{\"sends\":[";

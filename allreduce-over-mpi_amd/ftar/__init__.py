@@ -43,6 +43,8 @@ MPI_DTYPE = {"MPI_UINT8_T": 0, "MPI_INT8_T": 1, "MPI_UINT16_T": 2, "MPI_INT16_T"
              "MPI_INT64_T": 5, "MPI_LONG_LONG": 5, "MPI_LONG_LONG_INT": 5, "MPI_FLOAT": 6, "MPI_DOUBLE": 7,
              "MPI_C_BOOL": 8}
 OP = {"sum": 0, "band": 1, "MPI_SUM": 0, "MPI_BAND": 1}
+ALLGATHER = {"stages": 0, "collective": 1, "direct": 2}   # ftar_allgather_t
+_AG_NAME = {v: k for k, v in ALLGATHER.items()}
 STATUS = {0: "success", 1: "invalid argument", 2: "unsupported dtype/op", 3: "invalid FT_TOPO/FT_LONELY",
           4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout"}
 MAX_STAGES = 16
@@ -103,7 +105,8 @@ _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), 
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
 _lib.ftar_schedule_json.restype = ctypes.c_long
 _lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _int, ctypes.c_char_p, _sz]
-_lib.ftar_comm_set_native_allgather.argtypes = [_vp, _int]
+_lib.ftar_comm_set_allgather.argtypes = [_vp, _int]
+_lib.ftar_comm_get_allgather.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_plan_json.restype = ctypes.c_long
 
 
@@ -236,13 +239,14 @@ def schedule_json(t, nranks, rank, count):
     return json.loads(buf.value.decode())
 
 
-def plan_json(t, nranks, rank, count, native_allgather=False):
+def plan_json(t, nranks, rank, count, allgather="direct"):
     t = topo(t)
-    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, int(native_allgather), None, 0)
+    ag = ALLGATHER[allgather] if isinstance(allgather, str) else int(allgather)
+    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, None, 0)
     if n < 0:
         raise FtarError(-n, "ftar_plan_json")
     buf = ctypes.create_string_buffer(n + 1)
-    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, int(native_allgather), buf, n + 1)
+    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, buf, n + 1)
     return json.loads(buf.value.decode())
 
 
@@ -295,13 +299,16 @@ class Comm:
         _check(st, "ftar_allreduce")
 
     @property
-    def native_allgather(self):
-        return getattr(self, "_native_ag", False)
+    def allgather(self):
+        """All-gather form: "direct" (default), "stages" (the reference's rounds) or "collective"."""
+        v = _int()
+        _check(_lib.ftar_comm_get_allgather(self.handle, ctypes.byref(v)), "allgather")
+        return _AG_NAME[v.value]
 
-    @native_allgather.setter
-    def native_allgather(self, on):
-        _check(_lib.ftar_comm_set_native_allgather(self.handle, int(bool(on))), "native_allgather")
-        self._native_ag = bool(on)
+    @allgather.setter
+    def allgather(self, mode):
+        _check(_lib.ftar_comm_set_allgather(self.handle, ALLGATHER[mode] if isinstance(mode, str) else int(mode)),
+               "allgather")
 
     def allreduce_tensor(self, tensor, out=None, op="sum", topo_=None, lonely=0, stream=None):
         """In-place (out=None) or out-of-place AllReduce of a contiguous device tensor,
@@ -345,9 +352,9 @@ class LocalGroup:
         for c in self.comms:
             c.chunk_bytes = b
 
-    def set_native_allgather(self, on):
+    def set_allgather(self, mode):
         for c in self.comms:
-            c.native_allgather = on
+            c.allgather = mode
 
     def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None):
         P = len(self.comms)

@@ -232,9 +232,9 @@ def bench_distributed(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / max(1, steps) * 1e3
 
-    def run_with(topo, chunk, native_ag=False):
+    def run_with(topo, chunk, ag="direct"):
         comm.chunk_bytes = chunk
-        comm.native_allgather = native_ag
+        comm.allgather = ag
         return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
 
     # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
@@ -254,27 +254,29 @@ def bench_distributed(a):
         if key in seen:
             continue
         seen.add(key)
-        # all-gather phase: p2p stages, or one collective (non-lonely trees, P | n)
-        ags = [False] + ([True] if (not t.ring and n % world == 0 and world > 1) else [])
+        # all-gather form: one direct round (default), the reference's rounds, or one collective
+        ags = ["direct", "stages"] + (["collective"] if (not t.ring and n % world == 0 and world > 1) else [])
         for ag in ags:
             for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
+                if world > 1 and ag == "stages" and t.ring and chunk != default_chunk:
+                    continue  # the reference's ring rounds: one point is enough
                 try:
                     ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
                 except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
-                    sweep.append({"topology": key, "chunk_bytes": chunk, "native_allgather": ag, "error": str(e)[:200]})
+                    sweep.append({"topology": key, "chunk_bytes": chunk, "allgather": ag, "error": str(e)[:200]})
                     continue
-                sweep.append({"topology": key, "chunk_bytes": chunk, "native_allgather": ag, "ms": round(ms_, 4),
+                sweep.append({"topology": key, "chunk_bytes": chunk, "allgather": ag, "ms": round(ms_, 4),
                               "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
     ok_runs = [r for r in sweep if "ms" in r]
     best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else {
-        "topology": str(default_topo), "chunk_bytes": default_chunk, "native_allgather": False}
+        "topology": str(default_topo), "chunk_bytes": default_chunk, "allgather": "direct"}
     best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
 
     # headline: the swept-best configuration, K timed steps after W warmup
-    ms = timed(run_with(best_topo, best["chunk_bytes"], best["native_allgather"]), a.steps, a.warmup)
+    ms = timed(run_with(best_topo, best["chunk_bytes"], best["allgather"]), a.steps, a.warmup)
     ms_default = timed(run_with(default_topo, default_chunk), min(a.steps, 10), 1)
     comm.chunk_bytes = best["chunk_bytes"]
-    comm.native_allgather = best["native_allgather"]
+    comm.allgather = best["allgather"]
     comm.allreduce(x, y, n, a.dtype, "sum", topo_=best_topo, stream=stream)
     torch.cuda.synchronize()
 
@@ -316,7 +318,7 @@ def bench_distributed(a):
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
             "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
-                       "chunk_bytes": best["chunk_bytes"], "native_allgather": best["native_allgather"],
+                       "chunk_bytes": best["chunk_bytes"], "allgather": best["allgather"],
                        "selection": "best of sweep (FT_TOPO x chunk x all-gather form)",
                        "parallelism": f"dp{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),

@@ -135,11 +135,20 @@ ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device);
 /* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = default. */
 ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes);
 ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
-/* Run a non-lonely tree's all-gather phase (mpi_mod.hpp:1620-1644) as ONE
- * all-gather collective (ncclAllGather on RCCL) instead of k stages of p2p
- * groups.  Same bytes moved, identical results; needs count % P == 0 (else the
- * stages are kept).  Default off, or FTAR_NATIVE_ALLGATHER=1 at init. */
-ftar_status_t ftar_comm_set_native_allgather(ftar_comm_t comm, int on);
+/* How the all-gather phase is moved.  After the reduce-scatter stages every
+ * rank holds exactly one fully reduced block (block r on trees, lonely ranks
+ * included; block (r+1) mod P on the ring), so the phase only delivers final
+ * values and every form gives bit-identical results:
+ *   FTAR_AG_STAGES      the reference's rounds (ring: P-1 neighbour steps,
+ *                       tree: the k stages reversed, mpi_mod.hpp:1620-1644, :1705-1715)
+ *   FTAR_AG_DIRECT      one p2p group: each rank sends its block to all P-1
+ *                       peers at once (every xGMI link busy; default)
+ *   FTAR_AG_COLLECTIVE  one ncclAllGather (non-lonely trees with P | count;
+ *                       otherwise DIRECT)
+ * Default: FTAR_ALLGATHER=stages|direct|collective at init, else DIRECT. */
+typedef enum { FTAR_AG_STAGES = 0, FTAR_AG_COLLECTIVE = 1, FTAR_AG_DIRECT = 2 } ftar_allgather_t;
+ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode);
+ftar_status_t ftar_comm_get_allgather(ftar_comm_t comm, ftar_allgather_t* mode);
 
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
@@ -165,9 +174,9 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
  * tests/golden/schedules.jsonl). Returns needed length, or <0 on error. */
 long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, char* buf, size_t buflen);
 /* Executable plan of `rank` (JSON): stages of transfers/reduces, scratch size,
- * and whether the all-gather phase is one collective. */
-long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, int native_allgather, char* buf,
-                    size_t buflen);
+ * and the all-gather form actually used. */
+long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, ftar_allgather_t allgather,
+                    char* buf, size_t buflen);
 
 #ifdef __cplusplus
 }

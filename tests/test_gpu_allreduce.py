@@ -32,10 +32,10 @@ def group(P):
     return _groups[P]
 
 
-def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1, native_ag=False):
+def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1, ag="direct"):
     g = group(len(ins))
     g.set_chunk_bytes(chunk_bytes)
-    g.set_native_allgather(native_ag)
+    g.set_allgather(ag)
     n = ins[0].size
     send = [to_dev(x) for x in ins]
     if outofplace:
@@ -50,11 +50,12 @@ def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=
     return [from_dev(t, ins[0].dtype, n) for t, _ in recv]
 
 
+@pytest.mark.parametrize("ag", ["direct", "stages"])
 @pytest.mark.parametrize("case", gc.allreduce_cases(max_n=70000), ids=lambda c: c["id"])
-def test_allreduce_matches_reference_golden(case):
+def test_allreduce_matches_reference_golden(case, ag):
     ins = gc.case_inputs(case)
     outs = run_group(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
-                     repeat=case["repeat"])
+                     repeat=case["repeat"], ag=ag)
     for r in range(case["P"]):
         gc.check_output(case, r, outs[r])
 
@@ -66,7 +67,7 @@ def test_allreduce_pipelined_pieces(P, topo, lonely, chunk_bytes):
     """Many pieces per block: exercises the per-piece comm->reduce->comm event chain and the scratch halves."""
     n = 100_003
     ins = [fi.fill("f32", 31, r, n) for r in range(P)]
-    outs = run_group(ins, topo, lonely, chunk_bytes=chunk_bytes)
+    outs = run_group(ins, topo, lonely, chunk_bytes=chunk_bytes, ag=("stages", "direct")[chunk_bytes > 256])
     ref = oracle_lib.allreduce(ins, topo, lonely)
     for r in range(P):
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
@@ -120,11 +121,11 @@ def test_rccl_single_rank_comm():
 
 @pytest.mark.parametrize("P,topo", [(2, "2"), (4, "2,2"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3")])
 @pytest.mark.parametrize("outofplace", [False, True])
-def test_allreduce_native_allgather(P, topo, outofplace):
+def test_allreduce_collective_allgather(P, topo, outofplace):
     """All-gather phase as one collective (p2p-group fallback on the local transport): bit-exact."""
     n = P * 12_345
     ins = [fi.fill("f32", 12, r, n) for r in range(P)]
-    outs = run_group(ins, topo, outofplace=outofplace, chunk_bytes=1 << 16, native_ag=True)
+    outs = run_group(ins, topo, outofplace=outofplace, chunk_bytes=1 << 16, ag="collective")
     ref = oracle_lib.allreduce(ins, topo, outofplace=outofplace)
     for r in range(P):
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
@@ -135,7 +136,7 @@ def test_random_cases_through_engine():
     import random_cases
     for c in random_cases.cases(seed=77, count=80, max_p=9):
         outs = run_group(c["ins"], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1,
-                         c["oop"], chunk_bytes=c["chunk"])
+                         c["oop"], chunk_bytes=c["chunk"], ag=("stages", "direct", "collective")[c["n"] % 3])
         for r in range(c["P"]):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"], r)
 
@@ -157,7 +158,7 @@ def test_tensor_api_bf16_and_f32():
     import torch
     g = group(4)
     g.set_chunk_bytes(0)
-    g.set_native_allgather(False)
+    g.set_allgather("direct")
     for dt, name in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
         xs = [fi.fill(name, 3, r, 5000) for r in range(4)]
         ts = [torch.from_numpy(x.view(np.int16) if name == "bf16" else x).cuda().view(dt) for x in xs]

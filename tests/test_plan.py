@@ -59,7 +59,7 @@ def simulate(plans, inputs, dtype, op, outofplace):
                 srcs = [bufs[r][it["own"]][off:off + ln]] + [bufs[r]["scratch"][so:so + ln] for so in it["scratch"]]
                 out = oracle_lib.reduce(dtype, op, [np.ascontiguousarray(x) for x in srcs])
                 bufs[r]["dst"][off:off + ln] = out
-    if plans[0]["native_allgather"]:  # one all-gather: rank p contributes dst[p*split : (p+1)*split]
+    if plans[0]["allgather"] == "collective":  # one all-gather: rank p contributes dst[p*split : (p+1)*split]
         split = plans[0]["split"]
         segs = [dst[p][p * split:(p + 1) * split].copy() for p in range(P)]
         for r in range(P):
@@ -71,12 +71,13 @@ def simulate(plans, inputs, dtype, op, outofplace):
 CASES = gc.allreduce_cases(max_n=70000)
 
 
+@pytest.mark.parametrize("ag", ["stages", "direct"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c["id"])
-def test_product_plans_reproduce_reference(case):
+def test_product_plans_reproduce_reference(case, ag):
     import ftar
     P = case["P"]
     t = ftar.topo(case["topo"], case["lonely"])
-    plans = [ftar.plan_json(t, P, r, case["n"]) for r in range(P)]
+    plans = [ftar.plan_json(t, P, r, case["n"], allgather=ag) for r in range(P)]
     ins = gc.case_inputs(case)
     outs = None
     for _ in range(case["repeat"]):
@@ -99,22 +100,23 @@ def test_scratch_is_compact():
 
 @pytest.mark.parametrize("P,topo", [(2, "2"), (4, "4"), (4, "2,2"), (6, "2,3"), (8, "8"), (8, "2,4"), (8, "4,2"),
                                     (8, "2,2,2"), (9, "3,3")])
-def test_native_allgather_plans_match_oracle(P, topo):
+def test_collective_allgather_plans_match_oracle(P, topo):
     """Every non-lonely FlexTree leaves rank r holding block r, so the all-gather phase may be one
-    collective (ftar_comm_set_native_allgather): same result, bit for bit."""
+    collective (ftar_comm_set_allgather(FTAR_AG_COLLECTIVE)): same result, bit for bit."""
     import ftar
     n = P * 1001
     ins = [fi.fill("f32", 404, r, n) for r in range(P)]
-    plans = [ftar.plan_json(topo, P, r, n, native_allgather=True) for r in range(P)]
-    assert all(p["native_allgather"] for p in plans)
+    plans = [ftar.plan_json(topo, P, r, n, allgather="collective") for r in range(P)]
+    assert all(p["allgather"] == "collective" for p in plans)
     assert len(plans[0]["stages"]) == len(topo.split(","))      # reduce-scatter stages only
     outs = simulate(plans, ins, 6, 0, False)
     ref = oracle_lib.allreduce(ins, topo)
     for r in range(P):
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
     # not applicable: ragged counts, lonely ranks and the ring keep their stages
-    assert not ftar.plan_json(topo, P, 0, n + 1, native_allgather=True)["native_allgather"]
-    assert not ftar.plan_json("1", P, 0, n, native_allgather=True)["native_allgather"]
+    # not applicable: ragged counts and the ring (its final blocks sit one rank off) fall back to direct
+    assert ftar.plan_json(topo, P, 0, n + 1, allgather="collective")["allgather"] == "direct"
+    assert ftar.plan_json("1", P, 0, n, allgather="collective")["allgather"] == "direct"
 
 
 def test_random_plans_match_oracle():
@@ -124,7 +126,7 @@ def test_random_plans_match_oracle():
     for c in random_cases.cases(seed=2024, count=200):
         P = c["P"]
         t = ftar.topo(c["topo"], c["lonely"])
-        plans = [ftar.plan_json(t, P, r, c["n"]) for r in range(P)]
+        plans = [ftar.plan_json(t, P, r, c["n"], allgather=("stages", "direct")[c["n"] % 2]) for r in range(P)]
         outs = simulate(plans, c["ins"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1, c["oop"])
         for r in range(P):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"], r)
@@ -168,3 +170,14 @@ def test_deep_lonely_plans_match_oracle(P, topo, lonely):
     ref = oracle_lib.allreduce(ins, topo, lonely)
     for r in range(P):
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+
+
+def test_direct_allgather_is_one_round():
+    """Ring and trees: one all-gather stage with P-1 sends and P-1 receives per rank."""
+    import ftar
+    for P, topo, L in ((8, "1", 0), (8, "2,2,2", 0), (5, "2,2", 1)):
+        for r in range(P):
+            p = ftar.plan_json(ftar.topo(topo, L), P, r, 8000, allgather="direct")
+            ag = p["stages"][-1]
+            assert p["allgather"] == "direct" and not ag["reduces"]
+            assert len(ag["sends"]) == P - 1 and len(ag["recvs"]) == P - 1
