@@ -34,7 +34,9 @@ namespace {
 // here a stage of width w on data D moves D/w to each of w-1 peers in
 // parallel, then reduces w+1 streams through HBM:
 //   stage(w, D) = 2*alpha + 2*(D/w)/link + (w+1)*(D/w)/hbm,   D /= w per stage
-//   ring        = 2(P-1)*alpha + 2(P-1)*(S/P)/link + 3(P-1)*(S/P)/hbm
+//   ring        = stage(P, S): with the direct forms (default) the ring is one
+//                 gather-and-fold round plus one all-gather round, like tree(P);
+//                 its reference form would be 2(P-1)*alpha + 2(P-1)*(S/P)/link
 // alpha = one p2p group (launch + handshake), link = one peer's unidirectional
 // xGMI bandwidth, hbm = achieved reduce bandwidth.  Defaults are MI355X
 // figures (DESIGN.md §Cost model); FTAR_COST_{ALPHA_US,LINK_GBPS,HBM_GBPS}
@@ -53,9 +55,10 @@ double model_cost(const Topology& t, int P, size_t bytes) {
   CostConsts k;
   const double S = (double)bytes;
   if (P <= 1) return 0.0;
-  if (t.ring) {
-    const double blk = S / P;
-    return 2.0 * (P - 1) * k.alpha + 2.0 * (P - 1) * blk / k.link + 3.0 * (P - 1) * blk / k.hbm;
+  if (t.ring) {  // direct forms (the default): one gather-and-fold round + one all-gather round, = tree(P)
+    Topology one;
+    one.widths = {(size_t)P};
+    return model_cost(one, P, bytes);
   }
   double D = S, cost = 0.0;
   for (size_t w : t.widths) {
@@ -152,7 +155,7 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   ftar::Topology chk;
   ftar_status_t st = ftar::to_topology(&t, nranks, &chk);
   if (st != FTAR_SUCCESS) return st;
-  if (chk.lonely && ftar::check_world(chk, nranks, (size_t)nranks * 64, FTAR_AG_STAGES) != FTAR_SUCCESS)
+  if (chk.lonely && ftar::check_world(chk, nranks, (size_t)nranks * 64, ftar::Form()) != FTAR_SUCCESS)
     return FTAR_ERR_INVALID_TOPO;  // a lonely layout the reference cannot run (its asserts / a blocked Waitall)
   *out = t;
   return FTAR_SUCCESS;
@@ -160,11 +163,14 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
 
 ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
   if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
-  ftar::Topology best;
-  best.ring = true;
-  best.widths = {1};
+  ftar::Topology ring;
+  ring.ring = true;
+  ring.widths = {1};
+  ftar::Topology best = ring;
   if (nranks > 1) {
-    double best_cost = ftar::model_cost(best, nranks, bytes);
+    // trees first, the ring last: on a tie (the direct ring costs what tree(P) costs)
+    // keep the tree, whose bf16 fold rounds once instead of once per hop
+    double best_cost = 1e300;
     std::vector<size_t> cur;
     std::vector<std::vector<size_t>> cands;
     ftar::factorizations((size_t)nranks, cur, cands);
@@ -178,6 +184,7 @@ ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
         best = t;
       }
     }
+    if (ftar::model_cost(ring, nranks, bytes) < best_cost) best = ring;
   }
   ftar::from_topology(best, out);
   return FTAR_SUCCESS;
@@ -266,11 +273,14 @@ long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t co
 }
 
 long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, ftar_allgather_t allgather,
-                    char* buf, size_t buflen) {
+                    ftar_reduce_scatter_t reduce_scatter, char* buf, size_t buflen) {
   ftar::Topology t;
   if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -FTAR_ERR_INVALID_TOPO;
   ftar::Plan p;
-  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p, allgather);
+  ftar::Form form;
+  form.allgather = allgather;
+  form.reduce_scatter = reduce_scatter;
+  ftar_status_t st = ftar::build_plan(t, nranks, rank, count, &p, form);
   if (st != FTAR_SUCCESS) return -(long)st;
   return emit(p.json(), buf, buflen);
 }

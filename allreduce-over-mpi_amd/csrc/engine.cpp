@@ -34,6 +34,7 @@ struct ftar_comm {
   size_t chunk_bytes = 0;
   bool auto_topo = true;
   int allgather = FTAR_AG_DIRECT;
+  int reduce_scatter = FTAR_RS_DIRECT;
   ftar::Topology topo;
   std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
   std::vector<hipEvent_t> events;
@@ -59,6 +60,8 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
+  if (const char* rs = getenv("FTAR_REDUCE_SCATTER"))
+    c->reduce_scatter = std::string(rs) == "stages" ? FTAR_RS_STAGES : FTAR_RS_DIRECT;
   if (const char* ag = getenv("FTAR_ALLGATHER")) {
     const std::string m(ag);
     c->allgather = m == "stages" ? FTAR_AG_STAGES : m == "collective" ? FTAR_AG_COLLECTIVE : FTAR_AG_DIRECT;
@@ -110,12 +113,16 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
     FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
   }
-  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(c->allgather);
+  Form form;
+  form.allgather = c->allgather;
+  form.reduce_scatter = c->reduce_scatter;
+  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(c->allgather) + "/rs" +
+                          std::to_string(c->reduce_scatter);
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     auto p = std::make_shared<Plan>();
-    FTAR_RETURN_IF(check_world(t, c->nranks, count, c->allgather));  // once per (topology, count, form)
-    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), c->allgather));
+    FTAR_RETURN_IF(check_world(t, c->nranks, count, form));  // once per (topology, count, form)
+    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), form));
     if (c->plans.size() > 64) c->plans.clear();
     it = c->plans.emplace(key, p).first;
   }
@@ -187,10 +194,9 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
         for (const ReduceItem& r : st.reduces) {
           if (r.len <= lo) continue;
           srcs.clear();
-          srcs.push_back(bufs[r.own_buf] + (r.off + lo) * esz);
-          for (size_t so : r.scratch_offs) srcs.push_back(bufs[BUF_SCRATCH] + (so + lo) * esz);
+          for (const Operand& o : r.srcs) srcs.push_back(bufs[o.buf] + (o.off + lo) * esz);
           FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), bufs[BUF_DST] + (r.off + lo) * esz,
-                                       std::min(chunk, r.len - lo), dt, op, c->red_s));
+                                       std::min(chunk, r.len - lo), dt, op, c->red_s, r.round_each));
         }
         FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
       }
@@ -309,6 +315,19 @@ ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode) {
     return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   comm->allgather = mode;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t mode) {
+  if (!comm || (mode != FTAR_RS_STAGES && mode != FTAR_RS_DIRECT)) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->reduce_scatter = mode;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode) {
+  if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  *mode = static_cast<ftar_reduce_scatter_t>(comm->reduce_scatter);
   return FTAR_SUCCESS;
 }
 

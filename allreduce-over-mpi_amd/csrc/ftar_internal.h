@@ -55,11 +55,16 @@ struct Transfer {
   size_t len;  // elements (> 0)
 };
 
+struct Operand {
+  int buf;     // BufId
+  size_t off;  // element offset of this operand's copy of the block
+};
+
 struct ReduceItem {
-  size_t off;                        // element offset of the block in dst (and own)
-  size_t len;                        // elements (> 0)
-  int own_buf;                       // BUF_SRC or BUF_DST
-  std::vector<size_t> scratch_offs;  // peers' partials, in reduction order
+  size_t off;                   // element offset of the block in dst
+  size_t len;                   // elements (> 0)
+  std::vector<Operand> srcs;    // fold order: dst = ((srcs[0] OP srcs[1]) OP srcs[2]) ...
+  bool round_each = false;      // bf16: round after every add (one hop per add)
 };
 
 struct Stage {
@@ -71,9 +76,10 @@ struct Plan {
   int rank = 0, nranks = 1;
   size_t count = 0, split = 0;
   std::vector<Stage> stages;
-  // all-gather form actually used (ftar_allgather_t); COLLECTIVE = one
-  // all-gather of `split` elements at r*split after the reduce-scatter stages
+  // forms actually used; COLLECTIVE = one all-gather of `split` elements at
+  // r*split after the reduce-scatter stages
   int allgather = FTAR_AG_STAGES;
+  int reduce_scatter = FTAR_RS_STAGES;
   size_t scratch_half = 0;  // elements per scratch half (stages alternate halves)
   int max_k = 0;
   std::string json() const;
@@ -81,17 +87,21 @@ struct Plan {
 
 // FMA-level schedule (for tests/introspection), JSON shaped like the reference dump.
 ftar_status_t schedule_json(const Topology& t, int nranks, int rank, size_t count, std::string* out);
-ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out,
-                         int allgather = FTAR_AG_STAGES);
+struct Form {
+  int allgather = FTAR_AG_STAGES;
+  int reduce_scatter = FTAR_RS_STAGES;
+};
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, Form form = Form());
 // All ranks' plans pair up stage by stage (else FTAR_ERR_INVALID_TOPO).
-ftar_status_t check_world(const Topology& t, int nranks, size_t count, int allgather);
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, Form form);
 
 // ---------------------------------------------------------------------------
 // reduce kernels (reduce_kernels.hip)
 // ---------------------------------------------------------------------------
 // srcs: host array of k device pointers. k == 1 copies.
+// round_each: bf16 sums round to bf16 after every add (no effect on other dtypes).
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                            hipStream_t stream);
+                            hipStream_t stream, bool round_each = false);
 bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op);
 size_t dtype_size(ftar_dtype_t dt);
 

@@ -108,6 +108,17 @@ struct BF16Sum {
     return u32x4{pack(a.lo.x, a.lo.y), pack(a.lo.z, a.lo.w), pack(a.hi.x, a.hi.y), pack(a.hi.z, a.hi.w)};
   }
 };
+// bf16 folded hop by hop: every add rounds to bf16 (the one-round ring fold has
+// to reproduce the staged ring, which rounds once per hop)
+struct BF16SumHop : BF16Sum {
+  __device__ static float rnd(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+  __device__ static SA s_comb(SA a, S x) { return rnd(a + bf16_to_f32(x)); }
+  __device__ static VA v_comb(VA a, u32x4 x) {
+    VA b = v_init(x);
+    const f32x4 lo = a.lo + b.lo, hi = a.hi + b.hi;
+    return {f32x4{rnd(lo.x), rnd(lo.y), rnd(lo.z), rnd(lo.w)}, f32x4{rnd(hi.x), rnd(hi.y), rnd(hi.z), rnd(hi.w)}};
+  }
+};
 // modular integer sums on packed lanes (SWAR for 8/16-bit lanes)
 template <class S_, unsigned HI>
 struct SwarSum {
@@ -439,7 +450,7 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
 }
 
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                            hipStream_t s) {
+                            hipStream_t s, bool round_each) {
   if (k < 1 || k > FTAR_MAX_K || !srcs || !dst) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
   if (count == 0) return FTAR_SUCCESS;
@@ -453,7 +464,10 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   if (op == FTAR_SUM) {
     switch (dt) {
       case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, true); break;
-      case FTAR_BFLOAT16: e = launch_tr<BF16Sum>(srcs, k, dst, count, s, true); break;
+      case FTAR_BFLOAT16:
+        e = round_each && k > 2 ? launch_tr<BF16SumHop>(srcs, k, dst, count, s, true)
+                                : launch_tr<BF16Sum>(srcs, k, dst, count, s, true);
+        break;
       case FTAR_FLOAT64: e = launch_tr<F64Sum>(srcs, k, dst, count, s, false); break;
       case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum>(srcs, k, dst, count, s, false); break;
       case FTAR_UINT16: case FTAR_INT16: e = launch_tr<U16Sum>(srcs, k, dst, count, s, false); break;

@@ -315,11 +315,11 @@ void add_tree_stage(Stage& st, size_t me, const MemStage* send, const MemStage* 
     const MemOp& lead = (*ms)[0];
     for (size_t q = 0; q < lead.r.size(); ++q) {
       if (!lead.r[q].len) continue;
-      ReduceItem it{lead.r[q].actual, lead.r[q].len, first ? BUF_SRC : BUF_DST, {}};
+      ReduceItem it{lead.r[q].actual, lead.r[q].len, {{first ? BUF_SRC : BUF_DST, lead.r[q].actual}}};
       for (size_t j = 0; j < ms->size(); ++j)
-        if ((*ms)[j].peer != me) it.scratch_offs.push_back(slot[j][q]);
-      if (it.scratch_offs.empty()) continue;
-      *max_k = std::max(*max_k, (int)it.scratch_offs.size() + 1);
+        if ((*ms)[j].peer != me) it.srcs.push_back({BUF_SCRATCH, slot[j][q]});
+      if (it.srcs.size() < 2) continue;
+      *max_k = std::max(*max_k, (int)it.srcs.size());
       st.reduces.push_back(std::move(it));
     }
   };
@@ -364,7 +364,8 @@ Stage direct_allgather_stage(size_t P, size_t me, size_t count, bool ring) {
 }
 }  // namespace
 
-ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, int allgather) {
+ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, Form form) {
+  const int allgather = form.allgather;
   if (rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
   Plan p;
   p.rank = rank;
@@ -383,18 +384,54 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
     // dst = own(sendbuf) + recv, own always from the caller's send buffer.
     const int right = (int)((me + 1) % P), left = (int)((me + P - 1) % P);
     size_t bs = me, br = (me + P - 1) % P;
-    for (size_t i = 0; i + 1 < P; ++i) {
+    if (form.reduce_scatter == FTAR_RS_DIRECT) {
+      // one round: block b = (me+1) mod P is folded here from every rank's copy,
+      // in the ring's order b, b+1, ..., b+P-1 (= me, the caller's own copy last)
       Stage st;
-      Range s = block_range(bs, P, count), r = block_range(br, P, count);
-      if (s.len) st.sends.push_back({right, i == 0 ? BUF_SRC : BUF_DST, s.actual, s.len});
-      const size_t base = (i % 2) * p.split;
-      if (r.len) {
-        st.recvs.push_back({left, BUF_SCRATCH, base, r.len});
-        st.reduces.push_back({r.actual, r.len, BUF_SRC, {base}});
+      const size_t ob = (me + 1) % P;
+      for (size_t q = 0; q < P; ++q) {  // my copy of the block rank q owns
+        if (q == me) continue;
+        const Range c = block_range((q + 1) % P, P, count);
+        if (c.len) st.sends.push_back({(int)q, BUF_SRC, c.actual, c.len});
+      }
+      const Range mine = block_range(ob, P, count);
+      if (mine.len) {
+        ReduceItem it{mine.actual, mine.len, {}, true};
+        size_t slot = 0;
+        for (size_t j = 0; j < P; ++j) {
+          const size_t q = (ob + j) % P;
+          if (q == me) {
+            it.srcs.push_back({BUF_SRC, mine.actual});
+            continue;
+          }
+          st.recvs.push_back({(int)q, BUF_SCRATCH, slot, mine.len});
+          it.srcs.push_back({BUF_SCRATCH, slot});
+          slot += mine.len;
+        }
+        st.reduces.push_back(std::move(it));
       }
       p.stages.push_back(std::move(st));
-      bs = (bs + P - 1) % P;
-      br = (br + P - 1) % P;
+      p.reduce_scatter = FTAR_RS_DIRECT;
+      half = (P - 1) * p.split;
+      p.max_k = (int)P;
+      bs = (me + 1) % P;  // where the staged loop would leave them
+      br = me;
+    } else {
+      for (size_t i = 0; i + 1 < P; ++i) {
+        Stage st;
+        Range s = block_range(bs, P, count), r = block_range(br, P, count);
+        if (s.len) st.sends.push_back({right, i == 0 ? BUF_SRC : BUF_DST, s.actual, s.len});
+        const size_t base = (i % 2) * p.split;
+        if (r.len) {
+          st.recvs.push_back({left, BUF_SCRATCH, base, r.len});
+          st.reduces.push_back({r.actual, r.len, {{BUF_SRC, r.actual}, {BUF_SCRATCH, base}}, true});
+        }
+        p.stages.push_back(std::move(st));
+        bs = (bs + P - 1) % P;
+        br = (br + P - 1) % P;
+      }
+      half = p.split;
+      p.max_k = 2;
     }
     if (allgather == FTAR_AG_STAGES) {
       for (size_t i = 0; i + 1 < P; ++i) {  // mpi_mod.hpp:1705-1715
@@ -411,8 +448,6 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
       p.stages.push_back(direct_allgather_stage(P, me, count, true));
       p.allgather = FTAR_AG_DIRECT;
     }
-    half = p.split;
-    p.max_k = 2;
   } else {
     bool good = true;
     Fma f = lower(t, P, me, count, &good);
@@ -473,9 +508,9 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
 // MPI match p2p messages per peer pair in posting order).  Topologies the
 // reference cannot run (its asserts, or schedules that would block in
 // MPI_Waitall) fail here instead of hanging a collective.
-ftar_status_t check_world(const Topology& t, int nranks, size_t count, int allgather) {
+ftar_status_t check_world(const Topology& t, int nranks, size_t count, Form form) {
   std::vector<Plan> plans(nranks);
-  for (int r = 0; r < nranks; ++r) FTAR_RETURN_IF(build_plan(t, nranks, r, count, &plans[r], allgather));
+  for (int r = 0; r < nranks; ++r) FTAR_RETURN_IF(build_plan(t, nranks, r, count, &plans[r], form));
   for (int r = 1; r < nranks; ++r)
     if (plans[r].stages.size() != plans[0].stages.size()) return FTAR_ERR_INVALID_TOPO;
   for (size_t s = 0; s < plans[0].stages.size(); ++s)
@@ -498,7 +533,7 @@ std::string Plan::json() const {
   os << "{\"rank\":" << rank << ",\"nranks\":" << nranks << ",\"count\":" << count << ",\"split\":" << split
      << ",\"scratch_half\":" << scratch_half << ",\"max_k\":" << max_k
      << ",\"allgather\":\"" << (allgather == FTAR_AG_COLLECTIVE ? "collective" : allgather == FTAR_AG_DIRECT ? "direct" : "stages")
-     << "\",\"stages\":[";
+     << "\",\"reduce_scatter\":\"" << (reduce_scatter == FTAR_RS_DIRECT ? "direct" : "stages") << "\",\"stages\":[";
   for (size_t i = 0; i < stages.size(); ++i) {
     const Stage& s = stages[i];
     os << (i ? "," : "") << "{\"sends\":[";
@@ -512,9 +547,10 @@ std::string Plan::json() const {
     os << "],\"reduces\":[";
     for (size_t j = 0; j < s.reduces.size(); ++j) {
       const ReduceItem& r = s.reduces[j];
-      os << (j ? "," : "") << "{\"off\":" << r.off << ",\"len\":" << r.len << ",\"own\":\"" << bn[r.own_buf]
-         << "\",\"scratch\":[";
-      for (size_t q = 0; q < r.scratch_offs.size(); ++q) os << (q ? "," : "") << r.scratch_offs[q];
+      os << (j ? "," : "") << "{\"off\":" << r.off << ",\"len\":" << r.len << ",\"round_each\":"
+         << (r.round_each ? 1 : 0) << ",\"srcs\":[";
+      for (size_t q = 0; q < r.srcs.size(); ++q)
+        os << (q ? "," : "") << "[\"" << bn[r.srcs[q].buf] << "\"," << r.srcs[q].off << "]";
       os << "]}";
     }
     os << "]}";

@@ -45,6 +45,8 @@ MPI_DTYPE = {"MPI_UINT8_T": 0, "MPI_INT8_T": 1, "MPI_UINT16_T": 2, "MPI_INT16_T"
 OP = {"sum": 0, "band": 1, "MPI_SUM": 0, "MPI_BAND": 1}
 ALLGATHER = {"stages": 0, "collective": 1, "direct": 2}   # ftar_allgather_t
 _AG_NAME = {v: k for k, v in ALLGATHER.items()}
+REDUCE_SCATTER = {"stages": 0, "direct": 1}                 # ftar_reduce_scatter_t
+_RS_NAME = {v: k for k, v in REDUCE_SCATTER.items()}
 STATUS = {0: "success", 1: "invalid argument", 2: "unsupported dtype/op", 3: "invalid FT_TOPO/FT_LONELY",
           4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout"}
 MAX_STAGES = 16
@@ -104,7 +106,9 @@ _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), 
                                       ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
 _lib.ftar_schedule_json.restype = ctypes.c_long
-_lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _int, ctypes.c_char_p, _sz]
+_lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _int, _int, ctypes.c_char_p, _sz]
+_lib.ftar_comm_set_reduce_scatter.argtypes = [_vp, _int]
+_lib.ftar_comm_get_reduce_scatter.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_comm_set_allgather.argtypes = [_vp, _int]
 _lib.ftar_comm_get_allgather.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_plan_json.restype = ctypes.c_long
@@ -239,14 +243,15 @@ def schedule_json(t, nranks, rank, count):
     return json.loads(buf.value.decode())
 
 
-def plan_json(t, nranks, rank, count, allgather="direct"):
+def plan_json(t, nranks, rank, count, allgather="direct", reduce_scatter="direct"):
     t = topo(t)
     ag = ALLGATHER[allgather] if isinstance(allgather, str) else int(allgather)
-    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, None, 0)
+    rs = REDUCE_SCATTER[reduce_scatter] if isinstance(reduce_scatter, str) else int(reduce_scatter)
+    n = _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, rs, None, 0)
     if n < 0:
         raise FtarError(-n, "ftar_plan_json")
     buf = ctypes.create_string_buffer(n + 1)
-    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, buf, n + 1)
+    _lib.ftar_plan_json(ctypes.byref(t), nranks, rank, count, ag, rs, buf, n + 1)
     return json.loads(buf.value.decode())
 
 
@@ -310,6 +315,18 @@ class Comm:
         _check(_lib.ftar_comm_set_allgather(self.handle, ALLGATHER[mode] if isinstance(mode, str) else int(mode)),
                "allgather")
 
+    @property
+    def reduce_scatter(self):
+        """Ring reduce-scatter form: "direct" (one all-links round, default) or "stages" (the reference's)."""
+        v = _int()
+        _check(_lib.ftar_comm_get_reduce_scatter(self.handle, ctypes.byref(v)), "reduce_scatter")
+        return _RS_NAME[v.value]
+
+    @reduce_scatter.setter
+    def reduce_scatter(self, mode):
+        _check(_lib.ftar_comm_set_reduce_scatter(
+            self.handle, REDUCE_SCATTER[mode] if isinstance(mode, str) else int(mode)), "reduce_scatter")
+
     def allreduce_tensor(self, tensor, out=None, op="sum", topo_=None, lonely=0, stream=None):
         """In-place (out=None) or out-of-place AllReduce of a contiguous device tensor,
         e.g. a data-parallel gradient bucket; dtype and count come from the tensor."""
@@ -355,6 +372,10 @@ class LocalGroup:
     def set_allgather(self, mode):
         for c in self.comms:
             c.allgather = mode
+
+    def set_reduce_scatter(self, mode):
+        for c in self.comms:
+            c.reduce_scatter = mode
 
     def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None):
         P = len(self.comms)

@@ -232,9 +232,12 @@ def bench_distributed(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / max(1, steps) * 1e3
 
-    def run_with(topo, chunk, ag="direct"):
+    def run_with(topo, chunk, form="direct"):
+        """form: "direct" (one-round reduce-scatter for the ring, one-round all-gather),
+        "stages" (the reference's rounds both ways) or "collective" (ncclAllGather)."""
         comm.chunk_bytes = chunk
-        comm.allgather = ag
+        comm.allgather = form
+        comm.reduce_scatter = "stages" if form == "stages" else "direct"
         return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
 
     # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
@@ -254,7 +257,7 @@ def bench_distributed(a):
         if key in seen:
             continue
         seen.add(key)
-        # all-gather form: one direct round (default), the reference's rounds, or one collective
+        # data-movement form: one direct round each way (default), the reference's rounds, or a collective all-gather
         ags = ["direct", "stages"] + (["collective"] if (not t.ring and n % world == 0 and world > 1) else [])
         for ag in ags:
             for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
@@ -263,20 +266,19 @@ def bench_distributed(a):
                 try:
                     ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
                 except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
-                    sweep.append({"topology": key, "chunk_bytes": chunk, "allgather": ag, "error": str(e)[:200]})
+                    sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "error": str(e)[:200]})
                     continue
-                sweep.append({"topology": key, "chunk_bytes": chunk, "allgather": ag, "ms": round(ms_, 4),
+                sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "ms": round(ms_, 4),
                               "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
     ok_runs = [r for r in sweep if "ms" in r]
     best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else {
-        "topology": str(default_topo), "chunk_bytes": default_chunk, "allgather": "direct"}
+        "topology": str(default_topo), "chunk_bytes": default_chunk, "form": "direct"}
     best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
 
     # headline: the swept-best configuration, K timed steps after W warmup
-    ms = timed(run_with(best_topo, best["chunk_bytes"], best["allgather"]), a.steps, a.warmup)
+    ms = timed(run_with(best_topo, best["chunk_bytes"], best["form"]), a.steps, a.warmup)
     ms_default = timed(run_with(default_topo, default_chunk), min(a.steps, 10), 1)
-    comm.chunk_bytes = best["chunk_bytes"]
-    comm.allgather = best["allgather"]
+    run_with(best_topo, best["chunk_bytes"], best["form"])
     comm.allreduce(x, y, n, a.dtype, "sum", topo_=best_topo, stream=stream)
     torch.cuda.synchronize()
 
@@ -318,8 +320,8 @@ def bench_distributed(a):
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
             "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
-                       "chunk_bytes": best["chunk_bytes"], "allgather": best["allgather"],
-                       "selection": "best of sweep (FT_TOPO x chunk x all-gather form)",
+                       "chunk_bytes": best["chunk_bytes"], "form": best["form"],
+                       "selection": "best of sweep (FT_TOPO x chunk x data-movement form)",
                        "parallelism": f"dp{world}"},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",

@@ -149,6 +149,19 @@ ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
 typedef enum { FTAR_AG_STAGES = 0, FTAR_AG_COLLECTIVE = 1, FTAR_AG_DIRECT = 2 } ftar_allgather_t;
 ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode);
 ftar_status_t ftar_comm_get_allgather(ftar_comm_t comm, ftar_allgather_t* mode);
+/* How the ring's reduce-scatter is moved.  The ring folds block b as
+ * x_b + x_{b+1} + ... + x_{b+P-1} (left to right, indices mod P; the reference's
+ * own+recv per hop is that fold since IEEE addition commutes), finishing on rank
+ * b-1 (mpi_mod.hpp:1689-1703):
+ *   FTAR_RS_STAGES  the reference's P-1 neighbour steps (one xGMI link per rank)
+ *   FTAR_RS_DIRECT  rank b-1 gathers every rank's block b in ONE round over all
+ *                   links and folds them in that order with one k=P reduce
+ *                   (bf16: rounded after every add, i.e. once per hop, as staged)
+ * Identical results.  Trees already exchange with a whole group per stage and
+ * keep their stages.  Default: FTAR_REDUCE_SCATTER=stages|direct, else DIRECT. */
+typedef enum { FTAR_RS_STAGES = 0, FTAR_RS_DIRECT = 1 } ftar_reduce_scatter_t;
+ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t mode);
+ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode);
 
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
@@ -174,9 +187,9 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
  * tests/golden/schedules.jsonl). Returns needed length, or <0 on error. */
 long ftar_schedule_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, char* buf, size_t buflen);
 /* Executable plan of `rank` (JSON): stages of transfers/reduces, scratch size,
- * and the all-gather form actually used. */
+ * and the forms actually used. */
 long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count, ftar_allgather_t allgather,
-                    char* buf, size_t buflen);
+                    ftar_reduce_scatter_t reduce_scatter, char* buf, size_t buflen);
 
 #ifdef __cplusplus
 }

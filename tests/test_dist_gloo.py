@@ -64,9 +64,8 @@ def _worker(rank, world, port, case_id, q):
                 bufs[buf][off:off + ln] = t.numpy()
             for it in st["reduces"]:
                 off, ln = it["off"], it["len"]
-                srcs = [bufs[it["own"]][off:off + ln]] + [bufs["scratch"][s:s + ln] for s in it["scratch"]]
-                bufs["dst"][off:off + ln] = oracle_lib.reduce(case["dtype"], case["op"],
-                                                              [np.ascontiguousarray(s) for s in srcs])
+                srcs = [np.ascontiguousarray(bufs[b][o:o + ln]) for b, o in it["srcs"]]
+                bufs["dst"][off:off + ln] = oracle_lib.reduce(case["dtype"], case["op"], srcs)
         gc.check_output(case, rank, bufs["dst"])
         q.put((rank, "ok"))
     except Exception as e:  # report, don't hang the parent

@@ -32,10 +32,11 @@ def group(P):
     return _groups[P]
 
 
-def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1, ag="direct"):
+def run_group(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, chunk_bytes=0, repeat=1, ag="direct", rs=None):
     g = group(len(ins))
     g.set_chunk_bytes(chunk_bytes)
     g.set_allgather(ag)
+    g.set_reduce_scatter(rs or ("stages" if ag == "stages" else "direct"))
     n = ins[0].size
     send = [to_dev(x) for x in ins]
     if outofplace:
@@ -170,3 +171,16 @@ def test_tensor_api_bf16_and_f32():
             assert got.tobytes() == ref[r].tobytes()
     with pytest.raises(ValueError):
         g.allreduce_tensors([torch.zeros(4, device="cuda"), torch.zeros(5, device="cuda")] * 2)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i16"])
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_direct_ring_matches_reference_ring(P, dt):
+    """FT_TOPO=1 with the one-round reduce-scatter (k=P fold in ring order, bf16 rounded per hop) and the
+    one-round all-gather: bit-exact with the reference ring (oracle), pieces of 4 KiB."""
+    n = 50_001 * P + 7
+    ins = [fi.fill(dt, 3, r, n) for r in range(P)]
+    outs = run_group(ins, "1", dtype=fi.BY_NAME[dt], chunk_bytes=4096, ag="direct", rs="direct")
+    ref = oracle_lib.allreduce(ins, "1", dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes()

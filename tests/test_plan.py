@@ -56,8 +56,13 @@ def simulate(plans, inputs, dtype, op, outofplace):
         for r in range(P):
             for it in plans[r]["stages"][s]["reduces"]:
                 off, ln = it["off"], it["len"]
-                srcs = [bufs[r][it["own"]][off:off + ln]] + [bufs[r]["scratch"][so:so + ln] for so in it["scratch"]]
-                out = oracle_lib.reduce(dtype, op, [np.ascontiguousarray(x) for x in srcs])
+                srcs = [np.ascontiguousarray(bufs[r][b][o:o + ln]) for b, o in it["srcs"]]
+                if it["round_each"] and dtype == 9:  # bf16 folded hop by hop: one rounding per add
+                    out = srcs[0]
+                    for x in srcs[1:]:
+                        out = oracle_lib.reduce(dtype, op, [out, x])
+                else:
+                    out = oracle_lib.reduce(dtype, op, srcs)
                 bufs[r]["dst"][off:off + ln] = out
     if plans[0]["allgather"] == "collective":  # one all-gather: rank p contributes dst[p*split : (p+1)*split]
         split = plans[0]["split"]
@@ -71,13 +76,13 @@ def simulate(plans, inputs, dtype, op, outofplace):
 CASES = gc.allreduce_cases(max_n=70000)
 
 
-@pytest.mark.parametrize("ag", ["stages", "direct"])
+@pytest.mark.parametrize("form", ["stages", "direct"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c["id"])
-def test_product_plans_reproduce_reference(case, ag):
+def test_product_plans_reproduce_reference(case, form):
     import ftar
     P = case["P"]
     t = ftar.topo(case["topo"], case["lonely"])
-    plans = [ftar.plan_json(t, P, r, case["n"], allgather=ag) for r in range(P)]
+    plans = [ftar.plan_json(t, P, r, case["n"], allgather=form, reduce_scatter=form) for r in range(P)]
     ins = gc.case_inputs(case)
     outs = None
     for _ in range(case["repeat"]):
@@ -91,8 +96,9 @@ def test_scratch_is_compact():
     """The plan's scratch is one received range per slot (the reference keeps 2*P*split)."""
     import ftar
     n = 1 << 20
-    ring = ftar.plan_json("1", 8, 0, n)
+    ring = ftar.plan_json("1", 8, 0, n, reduce_scatter="stages")
     assert ring["scratch_half"] == n // 8
+    assert ftar.plan_json("1", 8, 0, n)["scratch_half"] == 7 * (n // 8)   # direct: P-1 slots, one round
     tree = ftar.plan_json("8", 8, 3, n)
     assert tree["scratch_half"] == 7 * (n // 8)
     assert tree["max_k"] == 8
@@ -126,7 +132,8 @@ def test_random_plans_match_oracle():
     for c in random_cases.cases(seed=2024, count=200):
         P = c["P"]
         t = ftar.topo(c["topo"], c["lonely"])
-        plans = [ftar.plan_json(t, P, r, c["n"], allgather=("stages", "direct")[c["n"] % 2]) for r in range(P)]
+        form = ("stages", "direct")[c["n"] % 2]
+        plans = [ftar.plan_json(t, P, r, c["n"], allgather=form, reduce_scatter=form) for r in range(P)]
         outs = simulate(plans, c["ins"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1, c["oop"])
         for r in range(P):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"], r)
@@ -181,3 +188,22 @@ def test_direct_allgather_is_one_round():
             ag = p["stages"][-1]
             assert p["allgather"] == "direct" and not ag["reduces"]
             assert len(ag["sends"]) == P - 1 and len(ag["recvs"]) == P - 1
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "i32", "f64"])
+@pytest.mark.parametrize("P", [2, 3, 5, 8])
+def test_direct_ring_is_the_ring_bit_for_bit(P, dt):
+    """One-round ring reduce-scatter (fold x_b, x_b+1, ..., x_b+P-1 on rank b-1) == the reference's ring,
+    including bf16's per-hop rounding; one stage each way."""
+    import ftar
+    n = 7 * P + 3
+    ins = [fi.fill(dt, 66, r, n) for r in range(P)]
+    plans = [ftar.plan_json("1", P, r, n, allgather="direct", reduce_scatter="direct") for r in range(P)]
+    assert all(len(p["stages"]) == 2 and p["reduce_scatter"] == "direct" for p in plans)
+    outs = simulate(plans, ins, fi.BY_NAME[dt], 0, False)
+    staged = simulate([ftar.plan_json("1", P, r, n, "stages", "stages") for r in range(P)], ins, fi.BY_NAME[dt], 0,
+                      False)
+    ref = oracle_lib.allreduce(ins, "1", dtype=fi.BY_NAME[dt])   # the oracle's ring rounds bf16 once per hop
+    for r in range(P):
+        assert outs[r].tobytes() == staged[r].tobytes()
+        assert outs[r].tobytes() == ref[r].tobytes()
