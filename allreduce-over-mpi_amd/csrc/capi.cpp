@@ -34,9 +34,12 @@ namespace {
 // here a stage of width w on data D moves D/w to each of w-1 peers in
 // parallel, then reduces w+1 streams through HBM:
 //   stage(w, D) = 2*alpha + 2*(D/w)/link + (w+1)*(D/w)/hbm,   D /= w per stage
-//   ring        = stage(P, S): with the direct forms (default) the ring is one
-//                 gather-and-fold round plus one all-gather round, like tree(P);
-//                 its reference form would be 2(P-1)*alpha + 2(P-1)*(S/P)/link
+// That is the staged (reference) form.  The default direct forms run the ring
+// and every non-lonely tree of at most 4 stages as one gather-and-fold round
+// plus one all-gather round, i.e. exactly what tree(P) moves and folds, so
+// they cost stage(P, S); the ring's reference form would be
+// 2(P-1)*alpha + 2(P-1)*(S/P)/link.  ftar_topo_choose keeps the fewest stages
+// on a tie (the flat fold; bf16 rounds once).
 // alpha = one p2p group (launch + handshake), link = one peer's unidirectional
 // xGMI bandwidth, hbm = achieved reduce bandwidth.  Defaults are MI355X
 // figures (DESIGN.md §Cost model); FTAR_COST_{ALPHA_US,LINK_GBPS,HBM_GBPS}
@@ -55,11 +58,14 @@ double model_cost(const Topology& t, int P, size_t bytes) {
   CostConsts k;
   const double S = (double)bytes;
   if (P <= 1) return 0.0;
-  if (t.ring) {  // direct forms (the default): one gather-and-fold round + one all-gather round, = tree(P)
+  const bool one_round = P <= FTAR_MAX_K && (t.ring || (t.lonely == 0 && t.widths.size() >= 2 &&
+                                                         t.widths.size() <= (size_t)kMaxFoldLevels));
+  if (one_round) {  // direct forms (the default): = tree(P), see schedule.cpp
     Topology one;
     one.widths = {(size_t)P};
     return model_cost(one, P, bytes);
   }
+  if (t.ring) return 2.0 * (P - 1) * (k.alpha + (S / P) / k.link) + (P - 1) * 3.0 * (S / P) / k.hbm;
   double D = S, cost = 0.0;
   for (size_t w : t.widths) {
     const double piece = D / (double)w;
@@ -118,6 +124,21 @@ ftar_status_t ftar_reduce(const void* const* srcs, int k, void* dst, size_t coun
   return ftar::launch_reduce(srcs, k, dst, count, dtype, op, static_cast<hipStream_t>(stream));
 }
 
+ftar_status_t ftar_reduce_nested(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dtype,
+                                 ftar_op_t op, const int* shape, int nlevels, void* stream) {
+  if (nlevels < 0 || nlevels > ftar::kMaxFoldLevels || (nlevels > 0 && !shape)) return FTAR_ERR_INVALID_ARG;
+  if (nlevels > 1) {  // validate the shape for every dtype (only float sums use it)
+    long long prod = 1;
+    for (int l = 0; l < nlevels; ++l) {
+      if (shape[l] < 1) return FTAR_ERR_INVALID_ARG;
+      prod *= shape[l];
+    }
+    if (prod != k) return FTAR_ERR_INVALID_ARG;
+  }
+  return ftar::launch_reduce(srcs, k, dst, count, dtype, op, static_cast<hipStream_t>(stream), false, shape,
+                             nlevels);
+}
+
 // get_stages (mpi_mod.hpp:1419-1486), minus its two bugs: an unset FT_TOPO
 // is reported (the reference exit(1)s for every P > 1) and a trailing comma
 // does not repeat the last width (the reference's `while(!ss.eof())` does).
@@ -168,18 +189,22 @@ ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
   ring.widths = {1};
   ftar::Topology best = ring;
   if (nranks > 1) {
-    // trees first, the ring last: on a tie (the direct ring costs what tree(P) costs)
-    // keep the tree, whose bf16 fold rounds once instead of once per hop
+    // trees first, the ring last; on a tie keep the tree with the fewest stages
+    // (the direct forms make the ring and multi-stage trees cost what tree(P)
+    // costs; its flat fold rounds bf16 once instead of once per hop / node)
     double best_cost = 1e300;
     std::vector<size_t> cur;
     std::vector<std::vector<size_t>> cands;
     ftar::factorizations((size_t)nranks, cur, cands);
     for (auto& c : cands) {
       if (c.size() > FTAR_MAX_STAGES) continue;
+      bool fits = true;  // one stage folds w sources: at most FTAR_MAX_K (engine.cpp)
+      for (size_t w : c) fits = fits && w <= FTAR_MAX_K;
+      if (!fits) continue;
       ftar::Topology t;
       t.widths = c;
       double cost = ftar::model_cost(t, nranks, bytes);
-      if (cost < best_cost) {
+      if (cost < best_cost || (cost == best_cost && c.size() < best.widths.size())) {
         best_cost = cost;
         best = t;
       }

@@ -196,7 +196,8 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
           srcs.clear();
           for (const Operand& o : r.srcs) srcs.push_back(bufs[o.buf] + (o.off + lo) * esz);
           FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), bufs[BUF_DST] + (r.off + lo) * esz,
-                                       std::min(chunk, r.len - lo), dt, op, c->red_s, r.round_each));
+                                       std::min(chunk, r.len - lo), dt, op, c->red_s, r.round_each,
+                                       r.shape.data(), (int)r.shape.size()));
         }
         FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
       }

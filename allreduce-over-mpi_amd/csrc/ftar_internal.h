@@ -65,6 +65,7 @@ struct ReduceItem {
   size_t len;                   // elements (> 0)
   std::vector<Operand> srcs;    // fold order: dst = ((srcs[0] OP srcs[1]) OP srcs[2]) ...
   bool round_each = false;      // bf16: round after every add (one hop per add)
+  std::vector<int> shape;       // nested fold of srcs (launch_reduce); empty = flat
 };
 
 struct Stage {
@@ -100,8 +101,14 @@ ftar_status_t check_world(const Topology& t, int nranks, size_t count, Form form
 // ---------------------------------------------------------------------------
 // srcs: host array of k device pointers. k == 1 copies.
 // round_each: bf16 sums round to bf16 after every add (no effect on other dtypes).
+// shape: bottom-up widths of a nested fold (srcs in depth-first leaf order,
+// product == k, at most kMaxFoldLevels levels; bf16 inner nodes rounded);
+// nlevels <= 1 = flat.  Only float sums depend on it: integer sums and AND are
+// associative and take the flat kernel.
+constexpr int kMaxFoldLevels = 4;
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                            hipStream_t stream, bool round_each = false);
+                            hipStream_t stream, bool round_each = false, const int* shape = nullptr,
+                            int nlevels = 0);
 bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op);
 size_t dtype_size(ftar_dtype_t dt);
 

@@ -29,6 +29,13 @@ namespace ftar {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kTreeLevels = kMaxFoldLevels;
+// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32, DESIGN.md §3):
+// nontemporal loads + plain stores, 2 vectors per lane, 256-thread workgroups
+// is the best of the variants at k = 2 (6.96 TB/s) and among the best at k = 8;
+// nontemporal STORES cost 6-8 % (they also evict what the next ring step sends).
+constexpr int kUnroll = 2;
+constexpr bool kNtLoads = true, kNtStores = false;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -67,6 +74,10 @@ struct F32Sum {
   __device__ static VA v_init(u32x4 x) { return __builtin_bit_cast(f32x4, x); }
   __device__ static VA v_comb(VA a, u32x4 x) { return a + __builtin_bit_cast(f32x4, x); }
   __device__ static u32x4 v_fin(VA a) { return __builtin_bit_cast(u32x4, a); }
+  __device__ static SA s_add(SA a, SA b) { return a + b; }
+  __device__ static SA s_rnd(SA a) { return a; }
+  __device__ static VA v_add(VA a, VA b) { return a + b; }
+  __device__ static VA v_rnd(VA a) { return a; }
 };
 struct F64Sum {
   using S = double;
@@ -78,6 +89,10 @@ struct F64Sum {
   __device__ static VA v_init(u32x4 x) { return __builtin_bit_cast(f64x2, x); }
   __device__ static VA v_comb(VA a, u32x4 x) { return a + __builtin_bit_cast(f64x2, x); }
   __device__ static u32x4 v_fin(VA a) { return __builtin_bit_cast(u32x4, a); }
+  __device__ static SA s_add(SA a, SA b) { return a + b; }
+  __device__ static SA s_rnd(SA a) { return a; }
+  __device__ static VA v_add(VA a, VA b) { return a + b; }
+  __device__ static VA v_rnd(VA a) { return a; }
 };
 struct BF16Sum {
   using S = unsigned short;
@@ -107,16 +122,23 @@ struct BF16Sum {
   __device__ static u32x4 v_fin(VA a) {
     return u32x4{pack(a.lo.x, a.lo.y), pack(a.lo.z, a.lo.w), pack(a.hi.x, a.hi.y), pack(a.hi.z, a.hi.w)};
   }
+  // nested folds: an inner node's value is stored as bf16 by the staged
+  // schedule, so it is rounded before its parent adds it
+  __device__ static float rnd(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+  __device__ static f32x4 rnd4(f32x4 v) { return f32x4{rnd(v.x), rnd(v.y), rnd(v.z), rnd(v.w)}; }
+  __device__ static SA s_add(SA a, SA b) { return a + b; }
+  __device__ static SA s_rnd(SA a) { return rnd(a); }
+  __device__ static VA v_add(VA a, VA b) { return {a.lo + b.lo, a.hi + b.hi}; }
+  __device__ static VA v_rnd(VA a) { return {rnd4(a.lo), rnd4(a.hi)}; }
 };
 // bf16 folded hop by hop: every add rounds to bf16 (the one-round ring fold has
 // to reproduce the staged ring, which rounds once per hop)
 struct BF16SumHop : BF16Sum {
-  __device__ static float rnd(float f) { return bf16_to_f32(f32_to_bf16(f)); }
   __device__ static SA s_comb(SA a, S x) { return rnd(a + bf16_to_f32(x)); }
   __device__ static VA v_comb(VA a, u32x4 x) {
     VA b = v_init(x);
     const f32x4 lo = a.lo + b.lo, hi = a.hi + b.hi;
-    return {f32x4{rnd(lo.x), rnd(lo.y), rnd(lo.z), rnd(lo.w)}, f32x4{rnd(hi.x), rnd(hi.y), rnd(hi.z), rnd(hi.w)}};
+    return {rnd4(lo), rnd4(hi)};
   }
 };
 // modular integer sums on packed lanes (SWAR for 8/16-bit lanes)
@@ -325,14 +347,130 @@ __global__ void __launch_bounds__(kThreads)
 }
 
 // ---------------------------------------------------------------------------
+// nested-fold kernel: the one-round reduce-scatter of a multi-stage tree.
+// The k sources are the P copies of one block in depth-first leaf order of the
+// block's mixed-radix fold tree (schedule.cpp tree_leaves), so every inner
+// node folds a run of consecutive values: level 0 folds leaves w0 at a time,
+// level 1 folds those results w1 at a time, ...  Per leaf j the host packs one
+// code byte (make_tree_code): bits 0-2 = how many levels complete after leaf
+// j, bit 3+l = the value entering level l opens a new node.  The codes are
+// uniform across the grid (kernarg, scalar branches); accumulators are indexed
+// only by unrolled loop counters, so they stay in VGPRs.  Float sums only:
+// integer sums and AND are associative, the flat kernel is exact for them.
+// ---------------------------------------------------------------------------
+struct TreeCode {
+  unsigned char c[FTAR_MAX_K];
+};
+
+template <class Tr, bool VEC>
+struct TreeOps;
+template <class Tr>
+struct TreeOps<Tr, true> {
+  using A = typename Tr::VA;
+  __device__ static A add(A a, A b) { return Tr::v_add(a, b); }
+  __device__ static A rnd(A a) { return Tr::v_rnd(a); }
+};
+template <class Tr>
+struct TreeOps<Tr, false> {
+  using A = typename Tr::SA;
+  __device__ static A add(A a, A b) { return Tr::s_add(a, b); }
+  __device__ static A rnd(A a) { return Tr::s_rnd(a); }
+};
+
+// push leaf values v[0..U) (one per vector slot) up the tree; on the last leaf
+// v ends up holding the root
+template <class O, int U>
+__device__ __forceinline__ void tree_push(typename O::A (&acc)[kTreeLevels][U], typename O::A (&v)[U], unsigned code) {
+  const unsigned done = code & 7u;
+#pragma unroll
+  for (int l = 0; l < kTreeLevels; ++l) {
+    const bool fresh = (code >> (3 + l)) & 1u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[l][u] = fresh ? v[u] : O::add(acc[l][u], v[u]);
+    if (done <= (unsigned)l) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = O::rnd(acc[l][u]);
+  }
+}
+
+template <class Tr>
+__device__ __forceinline__ typename Tr::S tree_elem(const void* const* p, int k, const TreeCode& tc, size_t e) {
+  using S = typename Tr::S;
+  using O = TreeOps<Tr, false>;
+  typename O::A acc[kTreeLevels][1], v[1];
+  for (int j = 0; j < k; ++j) {
+    v[0] = Tr::s_init(static_cast<const S*>(p[j])[e]);
+    tree_push<O, 1>(acc, v, tc.c[j]);
+  }
+  return Tr::s_fin(v[0]);
+}
+
+template <class Tr, int K, int U>
+__global__ void __launch_bounds__(kThreads)
+    reduce_tree_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, TreeCode tc, void* __restrict__ dst, size_t nvec,
+                       int head, int tail) {
+  using S = typename Tr::S;
+  using O = TreeOps<Tr, true>;
+  const int k = K > 0 ? K : kr;
+  constexpr int VE = 16 / sizeof(S);
+  const size_t tile_stride = (size_t)gridDim.x * (U * kThreads);
+  size_t v0 = (size_t)blockIdx.x * (U * kThreads) + threadIdx.x;
+
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {
+    const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
+    static_cast<S*>(dst)[e] = tree_elem<Tr>(src.p, k, tc, e);
+  }
+  auto sp = [&](int j) { return reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head); };
+  u32x4* d = reinterpret_cast<u32x4*>(static_cast<S*>(dst) + head);
+  for (; v0 + (U - 1) * kThreads < nvec; v0 += tile_stride) {
+    typename O::A acc[kTreeLevels][U], v[U];
+    if constexpr (K > 0) {  // every source in flight before the first add
+      u32x4 x[K][U];
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[j][u] = ld16<kNtLoads>(sp(j) + v0 + u * kThreads);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = Tr::v_init(x[j][u]);
+        tree_push<O, U>(acc, v, tc.c[j]);
+      }
+    } else {
+      for (int j = 0; j < k; ++j) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = Tr::v_init(ld16<kNtLoads>(sp(j) + v0 + u * kThreads));
+        tree_push<O, U>(acc, v, tc.c[j]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) d[v0 + u * kThreads] = Tr::v_fin(v[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // the one partial tile (if any)
+    const size_t vi = v0 + u * kThreads;
+    if (vi >= nvec) break;
+    typename O::A acc[kTreeLevels][1], v[1];
+    for (int j = 0; j < k; ++j) {
+      v[0] = Tr::v_init(ld16<kNtLoads>(sp(j) + vi));
+      tree_push<O, 1>(acc, v, tc.c[j]);
+    }
+    d[vi] = Tr::v_fin(v[0]);
+  }
+}
+
+template <class Tr>
+__global__ void __launch_bounds__(kThreads)
+    reduce_tree_elem_kernel(Srcs<FTAR_MAX_K> src, int k, TreeCode tc, void* __restrict__ dst, size_t n) {
+  using S = typename Tr::S;
+  const size_t stride = (size_t)gridDim.x * kThreads;
+  for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < n; e += stride)
+    static_cast<S*>(dst)[e] = tree_elem<Tr>(src.p, k, tc, e);
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch
 // ---------------------------------------------------------------------------
-// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32, DESIGN.md §3):
-// nontemporal loads + plain stores, 2 vectors per lane, 256-thread workgroups
-// is the best of the variants at k = 2 (6.96 TB/s) and among the best at k = 8;
-// nontemporal STORES cost 6-8 % (they also evict what the next ring step sends).
-constexpr int kUnroll = 2;
-constexpr bool kNtLoads = true, kNtStores = false;
 
 template <class Tr, int K, int U, bool NTL, bool NTS, int BS>
 hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s,
@@ -353,6 +491,74 @@ hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, in
 template <class Tr, int K>
 hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
   return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kThreads>(srcs, k, dst, nvec, head, tail, s, 0);
+}
+
+// Leaf codes of a nested fold with bottom-up widths shape[0..nlevels) over k
+// leaves (see reduce_tree_kernel).
+bool make_tree_code(const int* shape, int nlevels, int k, TreeCode* tc) {
+  if (nlevels < 1 || nlevels > kTreeLevels || k > FTAR_MAX_K) return false;
+  size_t W[kTreeLevels];
+  size_t prod = 1;
+  for (int l = 0; l < nlevels; ++l) {
+    if (shape[l] < 1) return false;
+    prod *= (size_t)shape[l];
+    W[l] = prod;
+  }
+  if (prod != (size_t)k) return false;
+  for (int j = 0; j < k; ++j) {
+    unsigned done = 0;
+    while (done < (unsigned)nlevels && (j + 1) % W[done] == 0) ++done;
+    unsigned code = done;
+    if (j % shape[0] == 0) code |= 1u << 3;
+    for (unsigned l = 1; l <= done && l < (unsigned)nlevels; ++l)
+      if (((j + 1) / W[l - 1] - 1) % (size_t)shape[l] == 0) code |= 1u << (3 + l);
+    if (done == (unsigned)nlevels && nlevels < kTreeLevels) code |= 1u << (3 + nlevels);  // root slot: write-only
+    tc->c[j] = (unsigned char)code;
+  }
+  return true;
+}
+
+template <class Tr, int K, int U>
+hipError_t launch_tree_k(const void* const* srcs, int k, const TreeCode& tc, void* dst, size_t nvec, int head,
+                         int tail, hipStream_t s) {
+  constexpr int KK = K > 0 ? K : FTAR_MAX_K;
+  Srcs<KK> a{};
+  for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
+  size_t blocks = (nvec + (size_t)U * kThreads - 1) / ((size_t)U * kThreads);
+  if (blocks == 0) blocks = 1;
+  if (blocks > 0x7fffffffull) blocks = 0x7fffffffull;
+  hipLaunchKernelGGL((reduce_tree_kernel<Tr, K, U>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
+                     nvec, head, tail);
+  return hipGetLastError();
+}
+
+template <class Tr>
+hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, void* dst, size_t count, hipStream_t s) {
+  using S = typename Tr::S;
+  constexpr size_t VE = 16 / sizeof(S);
+  const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
+  bool co_aligned = (mis % sizeof(S)) == 0;
+  for (int j = 0; j < k && co_aligned; ++j) co_aligned = (reinterpret_cast<uintptr_t>(srcs[j]) & 15) == mis;
+  if (!co_aligned) {
+    Srcs<FTAR_MAX_K> a{};
+    for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
+    size_t blocks = (count + kThreads - 1) / kThreads;
+    blocks = blocks > 8192 ? 8192 : blocks;
+    hipLaunchKernelGGL((reduce_tree_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
+                       count);
+    return hipGetLastError();
+  }
+  size_t head = mis ? (16 - mis) / sizeof(S) : 0;
+  if (head > count) head = count;
+  const size_t nvec = (count - head) / VE;
+  const int tail = (int)(count - head - nvec * VE);
+  switch (k) {  // the P of the common multi-stage trees; 16 sources fit one vector per lane
+    case 4: return launch_tree_k<Tr, 4, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+    case 6: return launch_tree_k<Tr, 6, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+    case 8: return launch_tree_k<Tr, 8, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+    case 16: return launch_tree_k<Tr, 16, 1>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+    default: return launch_tree_k<Tr, 0, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  }
 }
 
 template <class Tr>
@@ -450,7 +656,7 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
 }
 
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                            hipStream_t s, bool round_each) {
+                            hipStream_t s, bool round_each, const int* shape, int nlevels) {
   if (k < 1 || k > FTAR_MAX_K || !srcs || !dst) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
   if (count == 0) return FTAR_SUCCESS;
@@ -461,6 +667,17 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
     return FTAR_SUCCESS;
   }
   hipError_t e = hipErrorInvalidValue;
+  if (nlevels > 1 && op == FTAR_SUM && (dt == FTAR_FLOAT32 || dt == FTAR_FLOAT64 || dt == FTAR_BFLOAT16)) {
+    TreeCode tc;
+    if (!shape || !make_tree_code(shape, nlevels, k, &tc)) return FTAR_ERR_INVALID_ARG;
+    switch (dt) {
+      case FTAR_FLOAT32: e = launch_tree<F32Sum>(srcs, k, tc, dst, count, s); break;
+      case FTAR_FLOAT64: e = launch_tree<F64Sum>(srcs, k, tc, dst, count, s); break;
+      default: e = launch_tree<BF16Sum>(srcs, k, tc, dst, count, s); break;
+    }
+    FTAR_CHECK_HIP(e);
+    return FTAR_SUCCESS;
+  }
   if (op == FTAR_SUM) {
     switch (dt) {
       case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, true); break;

@@ -362,6 +362,56 @@ Stage direct_allgather_stage(size_t P, size_t me, size_t count, bool ring) {
   }
   return st;
 }
+// Depth-first leaf order of block n's fold tree after s stages: the stage-s
+// reduce at rank n folds its own partial, then its stage group's partials in
+// ascending rank order (mpi_mod.hpp:1316-1358); every partial is itself the
+// fold of the previous stage's group.  Rank n's group at stage s is
+// {left + j*g : j < w_s}, g = w_0...w_{s-1}, left = n's window start + n mod g
+// (mpi_mod.hpp:80-140).
+void tree_leaves(const std::vector<size_t>& w, size_t n, size_t s, std::vector<size_t>* out) {
+  if (s == 0) {
+    out->push_back(n);
+    return;
+  }
+  tree_leaves(w, n, s - 1, out);
+  size_t g = 1;
+  for (size_t i = 0; i + 1 < s; ++i) g *= w[i];
+  const size_t G = g * w[s - 1], left = n / G * G + n % g;
+  for (size_t j = 0; j < w[s - 1]; ++j)
+    if (left + j * g != n) tree_leaves(w, left + j * g, s - 1, out);
+}
+
+// One-round reduce-scatter of a multi-stage tree without lonely ranks: every
+// rank sends its copy of block q to rank q and folds the P copies of its own
+// block in one nested k = P fold (leaves in tree_leaves order, shape = the
+// stage widths): the staged tree's values, bit for bit, with all links busy
+// at once instead of one stage group at a time.
+Stage direct_tree_stage(const Topology& t, size_t P, size_t me, size_t count) {
+  Stage st;
+  for (size_t q = 0; q < P; ++q) {
+    if (q == me) continue;
+    const Range c = block_range(q, P, count);
+    if (c.len) st.sends.push_back({(int)q, BUF_SRC, c.actual, c.len});
+  }
+  const Range mine = block_range(me, P, count);
+  if (!mine.len) return st;
+  std::vector<size_t> leaves;
+  tree_leaves(t.widths, me, t.widths.size(), &leaves);
+  ReduceItem it{mine.actual, mine.len, {}, false, {}};
+  for (size_t w : t.widths) it.shape.push_back((int)w);
+  size_t slot = 0;
+  for (size_t q : leaves) {
+    if (q == me) {
+      it.srcs.push_back({BUF_SRC, mine.actual});
+      continue;
+    }
+    st.recvs.push_back({(int)q, BUF_SCRATCH, slot, mine.len});
+    it.srcs.push_back({BUF_SCRATCH, slot});
+    slot += mine.len;
+  }
+  st.reduces.push_back(std::move(it));
+  return st;
+}
 }  // namespace
 
 ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, Plan* out, Form form) {
@@ -384,7 +434,7 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
     // dst = own(sendbuf) + recv, own always from the caller's send buffer.
     const int right = (int)((me + 1) % P), left = (int)((me + P - 1) % P);
     size_t bs = me, br = (me + P - 1) % P;
-    if (form.reduce_scatter == FTAR_RS_DIRECT) {
+    if (form.reduce_scatter == FTAR_RS_DIRECT && P <= FTAR_MAX_K) {  // one k = P fold
       // one round: block b = (me+1) mod P is folded here from every rank's copy,
       // in the ring's order b, b+1, ..., b+P-1 (= me, the caller's own copy last)
       Stage st;
@@ -454,17 +504,25 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
     if (!good) return FTAR_ERR_INVALID_TOPO;
     const size_t k = t.widths.size();
     auto at = [](const std::vector<MemStage>& v, size_t i) -> const MemStage* { return i < v.size() ? &v[i] : nullptr; };
+    int max_k = 0;
+    const bool direct_rs = form.reduce_scatter == FTAR_RS_DIRECT && t.lonely == 0 && k >= 2 &&
+                           k <= (size_t)kMaxFoldLevels && P <= FTAR_MAX_K;
+    if (direct_rs) {
+      p.stages.push_back(direct_tree_stage(t, P, me, count));
+      p.reduce_scatter = FTAR_RS_DIRECT;
+      half = (P - 1) * p.split;
+      max_k = (int)P;
+    }
     // pass 1: scratch needed per reduce-scatter stage
     std::vector<Stage> rs(k);
     std::vector<size_t> used(k, 0);
-    int max_k = 0;
-    for (size_t i = 0; i < k; ++i) {
+    for (size_t i = 0; i < k && !direct_rs; ++i) {
       add_tree_stage(rs[i], me, at(f.send, i), at(f.send_l, i), at(f.recv, i), at(f.recv_l, i), i == 0, 0, &used[i],
                      &max_k);
       half = std::max(half, used[i]);
     }
     // pass 2: rebuild with each stage in its half (stages alternate halves)
-    for (size_t i = 0; i < k; ++i) {
+    for (size_t i = 0; i < k && !direct_rs; ++i) {
       Stage st;
       size_t u = 0;
       add_tree_stage(st, me, at(f.send, i), at(f.send_l, i), at(f.recv, i), at(f.recv_l, i), i == 0, (i % 2) * half,
@@ -548,7 +606,9 @@ std::string Plan::json() const {
     for (size_t j = 0; j < s.reduces.size(); ++j) {
       const ReduceItem& r = s.reduces[j];
       os << (j ? "," : "") << "{\"off\":" << r.off << ",\"len\":" << r.len << ",\"round_each\":"
-         << (r.round_each ? 1 : 0) << ",\"srcs\":[";
+         << (r.round_each ? 1 : 0) << ",\"shape\":[";
+      for (size_t q = 0; q < r.shape.size(); ++q) os << (q ? "," : "") << r.shape[q];
+      os << "],\"srcs\":[";
       for (size_t q = 0; q < r.srcs.size(); ++q)
         os << (q ? "," : "") << "[\"" << bn[r.srcs[q].buf] << "\"," << r.srcs[q].off << "]";
       os << "]}";

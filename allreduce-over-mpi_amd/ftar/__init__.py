@@ -87,6 +87,7 @@ _lib.ftar_last_error.restype = ctypes.c_char_p
 _lib.ftar_dtype_size.restype = _sz
 _lib.ftar_dtype_size.argtypes = [_int]
 _lib.ftar_reduce.argtypes = [ctypes.POINTER(_vp), _int, _vp, _sz, _int, _int, _vp]
+_lib.ftar_reduce_nested.argtypes = [ctypes.POINTER(_vp), _int, _vp, _sz, _int, _int, ctypes.POINTER(_int), _int, _vp]
 _lib.ftar_topo_parse.argtypes = [ctypes.c_char_p, ctypes.c_char_p, _int, ctypes.POINTER(Topo)]
 _lib.ftar_topo_from_env.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
 _lib.ftar_topo_choose.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
@@ -169,10 +170,17 @@ def dtype_size(dtype):
 
 
 # ---- L3: one-device reduce ----------------------------------------------------
-def reduce(srcs, dst, count, dtype="f32", op="sum", stream=None):
-    """dst[i] = srcs[0][i] op srcs[1][i] op ... (left to right), enqueued on `stream`."""
+def reduce(srcs, dst, count, dtype="f32", op="sum", stream=None, shape=None):
+    """dst[i] = srcs[0][i] op srcs[1][i] op ... (left to right), enqueued on `stream`.
+    shape=[w0, w1, ...]: nested fold of the sources in depth-first leaf order (ftar_reduce_nested)."""
     arr = (_vp * len(srcs))(*[_ptr(s) for s in srcs])
-    _check(_lib.ftar_reduce(arr, len(srcs), _ptr(dst), count, _dt(dtype), _op(op), _stream(stream)), "ftar_reduce")
+    if shape is None:
+        _check(_lib.ftar_reduce(arr, len(srcs), _ptr(dst), count, _dt(dtype), _op(op), _stream(stream)),
+               "ftar_reduce")
+    else:
+        sh = (_int * max(1, len(shape)))(*shape)
+        _check(_lib.ftar_reduce_nested(arr, len(srcs), _ptr(dst), count, _dt(dtype), _op(op), sh, len(shape),
+                                       _stream(stream)), "ftar_reduce_nested")
 
 
 # ---- topology -------------------------------------------------------------------
@@ -317,7 +325,8 @@ class Comm:
 
     @property
     def reduce_scatter(self):
-        """Ring reduce-scatter form: "direct" (one all-links round, default) or "stages" (the reference's)."""
+        """Reduce-scatter form of the ring and of multi-stage trees: "direct" (one all-links round, default) or
+        "stages" (the reference's)."""
         v = _int()
         _check(_lib.ftar_comm_get_reduce_scatter(self.handle, ctypes.byref(v)), "reduce_scatter")
         return _RS_NAME[v.value]

@@ -97,6 +97,16 @@ size_t ftar_dtype_size(ftar_dtype_t dt);
  * k == 1 copies (vector_add/reduce_sum.h:36-47).  stream: hipStream_t. */
 ftar_status_t ftar_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dtype,
                           ftar_op_t op, void* stream);
+/* Nested fold (extension; the one-round reduce-scatter of a multi-stage tree):
+ * the k sources are the leaves, in depth-first order, of a mixed-radix tree
+ * with bottom-up widths shape[0..nlevels) (product == k, nlevels <= 4).  Level
+ * 0 folds shape[0] consecutive leaves, level 1 folds shape[1] consecutive
+ * level-0 results, ... each node left to right; bf16 inner nodes are rounded
+ * to bf16 (what a staged tree stores between its stages).  Integer sums and
+ * AND are associative: the result equals ftar_reduce's.  nlevels <= 1 is
+ * ftar_reduce. */
+ftar_status_t ftar_reduce_nested(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dtype,
+                                 ftar_op_t op, const int* shape, int nlevels, void* stream);
 
 /* ---- topology ------------------------------------------------------------
  * ftar_topo_parse: FT_TOPO / FT_LONELY strings (NULL = unset) for nranks.
@@ -157,8 +167,11 @@ ftar_status_t ftar_comm_get_allgather(ftar_comm_t comm, ftar_allgather_t* mode);
  *   FTAR_RS_DIRECT  rank b-1 gathers every rank's block b in ONE round over all
  *                   links and folds them in that order with one k=P reduce
  *                   (bf16: rounded after every add, i.e. once per hop, as staged)
- * Identical results.  Trees already exchange with a whole group per stage and
- * keep their stages.  Default: FTAR_REDUCE_SCATTER=stages|direct, else DIRECT. */
+ * Identical results.  Multi-stage trees without lonely ranks (at most 4
+ * stages) likewise: FTAR_RS_DIRECT gathers the P copies of block r on rank r
+ * in one round and folds them as the tree would (ftar_reduce_nested), bit for
+ * bit; lonely layouts and single-stage trees keep their stages.
+ * Default: FTAR_REDUCE_SCATTER=stages|direct, else DIRECT. */
 typedef enum { FTAR_RS_STAGES = 0, FTAR_RS_DIRECT = 1 } ftar_reduce_scatter_t;
 ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t mode);
 ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode);

@@ -70,8 +70,13 @@ def test_cost_model_prefers_all_links_on_8_gpus():
     big = 1 << 30
     t = ftar.topo_choose(8, big)
     assert str(t) == "8"
-    assert ftar.topo_cost("8", 8, big) < ftar.topo_cost("2,4", 8, big)
-    assert ftar.topo_cost("ring", 8, big) == ftar.topo_cost("8", 8, big)   # direct forms: one round each way
+    # direct forms (default): the ring and multi-stage trees are one round each way, like tree(P)
+    assert ftar.topo_cost("ring", 8, big) == ftar.topo_cost("8", 8, big)
+    assert ftar.topo_cost("2,4", 8, big) == ftar.topo_cost("8", 8, big)
+    assert ftar.topo_cost("2,2,2", 8, big) == ftar.topo_cost("8", 8, big)
+    # lonely layouts and trees deeper than 4 stages keep the staged cost
+    assert ftar.topo_cost("2,2,2,2,2", 32, big) > ftar.topo_cost("32", 32, big)
+    assert ftar.topo_cost(ftar.topo("2,2", 1), 5, big) > ftar.topo_cost("5", 5, big)
     assert str(ftar.topo_choose(2, big)) == "2"          # ties keep the tree
     # every candidate is a valid factorization of P
     for P in range(2, 17):

@@ -3,7 +3,7 @@
 Each process builds ONLY its own rank's plan with libftar (exactly what
 ftar_allreduce does on its GPU), then executes it with gloo point-to-point
 messages instead of RCCL (same per-pair posting order), folding with the
-pinned oracle's reduce.  Every rank must end with the reference's golden
+pinned oracle's reduce (tests/plan_fold.py).  Every rank must end with the reference's golden
 output: the independently compiled per-rank plans form a consistent
 distributed protocol.  Also checks the unique-id bootstrap of ftar.dist.
 """
@@ -34,7 +34,7 @@ def _worker(rank, world, port, case_id, q):
     import ftar
     import ftar.dist
     import golden_cases as gc
-    import oracle_lib
+    import plan_fold
 
     try:
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
@@ -65,7 +65,7 @@ def _worker(rank, world, port, case_id, q):
             for it in st["reduces"]:
                 off, ln = it["off"], it["len"]
                 srcs = [np.ascontiguousarray(bufs[b][o:o + ln]) for b, o in it["srcs"]]
-                bufs["dst"][off:off + ln] = oracle_lib.reduce(case["dtype"], case["op"], srcs)
+                bufs["dst"][off:off + ln] = plan_fold.fold(it, srcs, case["dtype"], case["op"])
         gc.check_output(case, rank, bufs["dst"])
         q.put((rank, "ok"))
     except Exception as e:  # report, don't hang the parent
@@ -77,7 +77,10 @@ def _worker(rank, world, port, case_id, q):
 
 
 CASES = ["ar_P2_t1_l0_f32_op0_n1003", "ar_P2_t2_l0_f32_op0_n65541", "ar_P4_t2-2_l0_f32_op0_n1003",
-         "ar_P4_t1_l0_f32_op0_n17", "ar_P5_t2-2_l1_f32_op0_n1003", "ar_P4_t2-2_l0_f32_op0_n1003_oop"]
+         "ar_P4_t1_l0_f32_op0_n17", "ar_P5_t2-2_l1_f32_op0_n1003", "ar_P4_t2-2_l0_f32_op0_n1003_oop",
+         # the one-round forms at a node's size: direct ring and direct multi-stage trees, 8 processes
+         "ar_P4_t2-2_l0_f64_op0_n1003", "ar_P8_t2-2-2_l0_f32_op0_n1003", "ar_P8_t2-4_l0_f32_op0_n65541",
+         "ar_P8_t1_l0_f32_op0_n1003"]
 
 
 @pytest.mark.parametrize("case_id", CASES)

@@ -184,3 +184,18 @@ def test_direct_ring_matches_reference_ring(P, dt):
     ref = oracle_lib.allreduce(ins, "1", dtype=fi.BY_NAME[dt])
     for r in range(P):
         assert outs[r].tobytes() == ref[r].tobytes()
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i16"])
+@pytest.mark.parametrize("P,topo", [(4, "2,2"), (6, "3,2"), (8, "2,4"), (8, "4,2"), (8, "2,2,2"), (9, "3,3"),
+                                    (16, "2,2,2,2"), (16, "4,4")])
+def test_direct_tree_matches_reference_tree(P, topo, dt):
+    """Multi-stage trees with the one-round reduce-scatter (gather + nested fold in depth-first leaf order)
+    and the one-round all-gather: bit-exact with the reference's staged tree (oracle), pieces of 4 KiB and
+    ragged blocks."""
+    n = 30_001 * P + 5
+    ins = [fi.fill(dt, 4, r, n) for r in range(P)]
+    outs = run_group(ins, topo, dtype=fi.BY_NAME[dt], chunk_bytes=4096, ag="direct", rs="direct")
+    ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes()

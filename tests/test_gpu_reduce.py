@@ -136,3 +136,39 @@ def test_reduce_beyond_int32_index():
         np.testing.assert_array_equal(out[lo:hi].cpu().numpy(), exp)
     # full-size property: sum of all bytes is preserved mod 2^8 per element -> compare checksums
     assert int(((a.to(torch.int64) + b.to(torch.int64)) % 256).sum()) == int(out.to(torch.int64).sum())
+
+
+def nested_oracle(dt, op, ins, shape):
+    """Nested fold, every node one oracle reduce (what the staged tree computes)."""
+    vals = ins
+    for w in shape:
+        vals = [oracle_lib.reduce(dt, op, vals[i:i + w]) if w > 1 else vals[i] for i in range(0, len(vals), w)]
+    return vals[0]
+
+
+@pytest.mark.parametrize("shape", [[2, 2], [2, 3], [3, 2], [2, 4], [4, 2], [2, 2, 2], [3, 3], [2, 3, 2], [4, 4],
+                                   [2, 2, 2, 2], [3, 3, 3], [1, 4, 2], [8, 1]])
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i32", "u8"])
+@pytest.mark.parametrize("n,off", [(100_003, 0), (4099, 1)])
+def test_reduce_nested_vs_oracle(shape, dt, n, off):
+    """ftar_reduce_nested (the one-round tree reduce-scatter's fold): bit-exact vs per-node oracle reduces,
+    compile-time k (4, 6, 8, 16) and runtime k (9, 12, 27), co-aligned and element-wise (off=1, dst aligned)."""
+    import ftar
+    k = int(np.prod(shape))
+    ins = [fi.fill(dt, 2000 + k, j, n) for j in range(k)]
+    offs = [off if j % 2 else 0 for j in range(k)]
+    devs = [to_dev(x, offset_elems=o) for x, o in zip(ins, offs)]
+    dst_t, dst = filled_dev(n * ins[0].itemsize)
+    ftar.reduce([p for _, p in devs], dst, n, dt, "sum", shape=shape)
+    got = from_dev(dst_t, ins[0].dtype, n)
+    exp = nested_oracle(fi.BY_NAME[dt], 0, ins, shape)
+    np.testing.assert_array_equal(got.view(np.uint8), exp.view(np.uint8))
+
+
+def test_reduce_nested_rejects_bad_shapes():
+    import ftar
+    t, p = filled_dev(64)
+    for shape in ([2, 3], [0, 4], [2, 2, 2, 2, 1], [-1, -4]):
+        with pytest.raises(ftar.FtarError):
+            ftar.reduce([p] * 4, p, 4, "f32", "sum", shape=shape)
+    ftar.reduce([p] * 4, p, 0, "f32", "sum", shape=[2, 2])   # zero count: no-op

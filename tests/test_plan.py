@@ -18,6 +18,7 @@ import pytest
 import ftar_inputs as fi
 import golden_cases as gc
 import oracle_lib
+import plan_fold
 
 
 def _schedules():
@@ -57,12 +58,7 @@ def simulate(plans, inputs, dtype, op, outofplace):
             for it in plans[r]["stages"][s]["reduces"]:
                 off, ln = it["off"], it["len"]
                 srcs = [np.ascontiguousarray(bufs[r][b][o:o + ln]) for b, o in it["srcs"]]
-                if it["round_each"] and dtype == 9:  # bf16 folded hop by hop: one rounding per add
-                    out = srcs[0]
-                    for x in srcs[1:]:
-                        out = oracle_lib.reduce(dtype, op, [out, x])
-                else:
-                    out = oracle_lib.reduce(dtype, op, srcs)
+                out = plan_fold.fold(it, srcs, dtype, op)
                 bufs[r]["dst"][off:off + ln] = out
     if plans[0]["allgather"] == "collective":  # one all-gather: rank p contributes dst[p*split : (p+1)*split]
         split = plans[0]["split"]
@@ -112,13 +108,15 @@ def test_collective_allgather_plans_match_oracle(P, topo):
     import ftar
     n = P * 1001
     ins = [fi.fill("f32", 404, r, n) for r in range(P)]
-    plans = [ftar.plan_json(topo, P, r, n, allgather="collective") for r in range(P)]
-    assert all(p["allgather"] == "collective" for p in plans)
-    assert len(plans[0]["stages"]) == len(topo.split(","))      # reduce-scatter stages only
-    outs = simulate(plans, ins, 6, 0, False)
     ref = oracle_lib.allreduce(ins, topo)
-    for r in range(P):
-        np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
+    for rs in ("stages", "direct"):
+        plans = [ftar.plan_json(topo, P, r, n, allgather="collective", reduce_scatter=rs) for r in range(P)]
+        assert all(p["allgather"] == "collective" for p in plans)
+        # reduce-scatter stages only: one per tree stage, or one round
+        assert len(plans[0]["stages"]) == (len(topo.split(",")) if rs == "stages" else 1)
+        outs = simulate(plans, ins, 6, 0, False)
+        for r in range(P):
+            np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
     # not applicable: ragged counts, lonely ranks and the ring keep their stages
     # not applicable: ragged counts and the ring (its final blocks sit one rank off) fall back to direct
     assert ftar.plan_json(topo, P, 0, n + 1, allgather="collective")["allgather"] == "direct"
@@ -207,3 +205,75 @@ def test_direct_ring_is_the_ring_bit_for_bit(P, dt):
     for r in range(P):
         assert outs[r].tobytes() == staged[r].tobytes()
         assert outs[r].tobytes() == ref[r].tobytes()
+
+
+def tree_leaves_py(w, n, s):
+    """Depth-first leaf order of block n's fold tree (restated independently of schedule.cpp)."""
+    if s == 0:
+        return [n]
+    g = int(np.prod(w[:s - 1], dtype=np.int64))
+    G = g * w[s - 1]
+    left = n // G * G + n % g
+    out = tree_leaves_py(w, n, s - 1)
+    for j in range(w[s - 1]):
+        if left + j * g != n:
+            out += tree_leaves_py(w, left + j * g, s - 1)
+    return out
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i16", "u8", "bool"])
+@pytest.mark.parametrize("P,topo", [(4, "2,2"), (6, "2,3"), (6, "3,2"), (8, "2,4"), (8, "4,2"), (8, "2,2,2"),
+                                    (9, "3,3"), (12, "2,3,2"), (16, "2,2,2,2"), (16, "4,4"), (27, "3,3,3")])
+def test_direct_tree_is_the_tree_bit_for_bit(P, topo, dt):
+    """One-round reduce-scatter of a multi-stage tree: rank b gathers every copy of block b and folds them in
+    depth-first order of b's fold tree (shape = stage widths, bf16 rounded per inner node) == the staged tree
+    and the reference (oracle), one stage each way."""
+    import ftar
+    n = 7 * P + 3
+    w = [int(x) for x in topo.split(",")]
+    ins = [fi.fill(dt, 67, r, n) for r in range(P)]
+    plans = [ftar.plan_json(topo, P, r, n, allgather="direct", reduce_scatter="direct") for r in range(P)]
+    for r, p in enumerate(plans):
+        assert len(p["stages"]) == 2 and p["reduce_scatter"] == "direct" and p["max_k"] == P
+        if not p["stages"][0]["reduces"]:  # ragged tail: this rank's block is empty
+            assert r * ((n + P - 1) // P) >= n
+            continue
+        (red,) = p["stages"][0]["reduces"]
+        assert red["shape"] == w
+        # leaf order: own copy where the tree has it, every peer's copy once
+        order = [r if b == "src" else None for b, _ in red["srcs"]]
+        leaves = tree_leaves_py(w, r, len(w))
+        assert [q for q in order if q is not None] == [r] and order.index(r) == leaves.index(r)
+        recv_peers = [peer for peer, _, _, _ in p["stages"][0]["recvs"]]
+        assert recv_peers == [q for q in leaves if q != r]
+    outs = simulate(plans, ins, fi.BY_NAME[dt], 0, False)
+    staged = simulate([ftar.plan_json(topo, P, r, n, "stages", "stages") for r in range(P)], ins, fi.BY_NAME[dt], 0,
+                      False)
+    ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        assert outs[r].tobytes() == staged[r].tobytes()
+        assert outs[r].tobytes() == ref[r].tobytes()
+
+
+def test_direct_tree_eligibility():
+    """Lonely ranks, single-stage trees and trees deeper than the fold kernel's 4 levels keep their stages."""
+    import ftar
+    assert ftar.plan_json(ftar.topo("2,2", 1), 5, 0, 500)["reduce_scatter"] == "stages"
+    assert ftar.plan_json("8", 8, 0, 800)["reduce_scatter"] == "stages"       # already one round
+    assert ftar.plan_json("2,2,2,2,2", 32, 0, 3200)["reduce_scatter"] == "stages"
+    assert ftar.plan_json("2,2,2,2", 16, 0, 1600)["reduce_scatter"] == "direct"
+
+
+def test_direct_forms_fall_back_beyond_max_k():
+    """More ranks than one reduce takes (FTAR_MAX_K = 64): the ring keeps its neighbour steps."""
+    import ftar
+    p = ftar.plan_json("1", 65, 3, 65 * 10)
+    assert p["reduce_scatter"] == "stages" and p["max_k"] == 2
+    assert ftar.plan_json("1", 64, 3, 64 * 10)["reduce_scatter"] == "direct"
+    assert ftar.topo_cost("ring", 65, 1 << 30) > ftar.topo_cost("65", 65, 1 << 30)
+    # a 65-wide stage is more sources than one reduce takes: the choice never proposes it
+    assert str(ftar.topo_choose(67, 1 << 30)) == "ring"     # prime > 64: no tree fits
+    for P in (96, 128, 130):
+        t = ftar.topo_choose(P, 1 << 30)
+        assert t.ring or max(t.widths) <= 64, (P, str(t))
+        assert ftar.plan_json(t, P, 1, P * 10)["max_k"] <= 64

@@ -27,6 +27,7 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--variants", default="0,1,2,3,4,5,6,7,8,9,10,11")
 ap.add_argument("--ks", default="2,4,8")
 ap.add_argument("--dtypes", default="f32,bf16")
+ap.add_argument("--shapes", default="", help='nested folds instead of variants, e.g. "8;2,4;2,2,2" ("8" = flat)')
 a = ap.parse_args()
 lib = ftar.lib()
 lib.ftar_debug_reduce_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
@@ -73,6 +74,29 @@ for r in range(a.rounds):
     e1.record(stream)
     torch.cuda.synchronize()
     res.setdefault(("copy", 0, 0), []).append(e0.elapsed_time(e1) / a.reps)
+
+if a.shapes:  # flat k-way (ftar_reduce) vs nested folds (ftar_reduce_nested) of the same k, interleaved
+    shapes = [[int(w) for w in sh.split(",")] for sh in a.shapes.split(";")]
+    res = {}
+    kmax = max(int(torch.tensor(sh).prod()) for sh in shapes)
+    for d in dts:
+        while len(srcs[d]) < kmax:
+            srcs[d].append((torch.rand(n, device=dev) * 2 - 1).to(tdt[d]))
+    for r in range(a.rounds):
+        for d in dts:
+            for sh in shapes:
+                k = int(torch.tensor(sh).prod())
+                ptrs = [s_.data_ptr() for s_ in srcs[d][:k]]
+                call = lambda: ftar.reduce(ptrs, dst[d].data_ptr(), n, d, "sum", stream=stream.cuda_stream,
+                                           shape=sh if len(sh) > 1 else None)
+                call()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(a.reps):
+                    call()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                res.setdefault((d, k, ",".join(map(str, sh))), []).append(e0.elapsed_time(e1) / a.reps)
 
 for (d, k, v), ts in sorted(res.items(), key=lambda kv: str(kv[0])):
     esz = 4 if d in ("f32", "copy") else 2
