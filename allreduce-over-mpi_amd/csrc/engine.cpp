@@ -29,9 +29,13 @@ struct ftar_comm {
   int rank = 0, nranks = 1, device = 0;
   std::unique_ptr<ftar::Transport> tp;
   hipStream_t comm_s = nullptr, red_s = nullptr;
+  hipStream_t h2d_s = nullptr, d2h_s = nullptr;  // host mode (ftar_allreduce_host)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* staging = nullptr;  // host mode: the device copy of the bucket, grow-only
+  size_t staging_bytes = 0;
   size_t chunk_bytes = 0;
+  size_t host_chunk_bytes = 0;
   bool auto_topo = true;
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
@@ -45,6 +49,9 @@ namespace ftar {
 
 namespace {
 constexpr size_t kDefaultChunkBytes = 16u << 20;
+// host mode pieces: small enough that the PCIe pipeline fills fast, large
+// enough for full-rate DMA (a piece of P blocks is P copies per direction)
+constexpr size_t kDefaultHostChunkBytes = 4u << 20;
 
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
   while (c->events.size() < n) {
@@ -60,6 +67,11 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
+  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
+  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  const char* hcb = getenv("FTAR_HOST_CHUNK_BYTES");
+  c->host_chunk_bytes = hcb ? strtoull(hcb, nullptr, 0) : kDefaultHostChunkBytes;
+  if (c->host_chunk_bytes < 256) c->host_chunk_bytes = kDefaultHostChunkBytes;
   if (const char* rs = getenv("FTAR_REDUCE_SCATTER"))
     c->reduce_scatter = std::string(rs) == "stages" ? FTAR_RS_STAGES : FTAR_RS_DIRECT;
   if (const char* ag = getenv("FTAR_ALLGATHER")) {
@@ -80,17 +92,24 @@ ftar_status_t comm_setup(ftar_comm* c) {
 
 void comm_teardown(ftar_comm* c) {
   (void)hipSetDevice(c->device);
-  if (c->comm_s) (void)hipStreamSynchronize(c->comm_s);
-  if (c->red_s) (void)hipStreamSynchronize(c->red_s);
+  for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
+    if (st) (void)hipStreamSynchronize(st);
   c->tp.reset();
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->scratch) (void)hipFree(c->scratch);
-  if (c->comm_s) (void)hipStreamDestroy(c->comm_s);
-  if (c->red_s) (void)hipStreamDestroy(c->red_s);
+  if (c->staging) (void)hipFree(c->staging);
+  for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
+    if (st) (void)hipStreamDestroy(st);
 }
 
+// Host mode: sendbuf/recvbuf of the call are host memory (pinned for overlap).
+struct HostIO {
+  const char* src;
+  char* dst;
+};
+
 ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                        const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream) {
+                        const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr) {
   if (!c || !recvbuf) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
   const size_t esz = dtype_size(dt);
@@ -98,7 +117,9 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   if (sendbuf == recvbuf) sendbuf = nullptr;
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
-    if (sendbuf && count) FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, hipMemcpyDeviceToDevice, stream));
+    if (sendbuf && count)
+      FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, host ? hipMemcpyHostToHost : hipMemcpyDeviceToDevice,
+                                    stream));
     return FTAR_SUCCESS;
   }
   if (count == 0) return FTAR_SUCCESS;
@@ -116,8 +137,9 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   Form form;
   form.allgather = c->allgather;
   form.reduce_scatter = c->reduce_scatter;
-  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(c->allgather) + "/rs" +
-                          std::to_string(c->reduce_scatter);
+  if (host && form.allgather == FTAR_AG_COLLECTIVE) form.allgather = FTAR_AG_DIRECT;  // D2H needs pieces
+  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(form.allgather) + "/rs" +
+                          std::to_string(form.reduce_scatter);
   auto it = c->plans.find(key);
   if (it == c->plans.end()) {
     auto p = std::make_shared<Plan>();
@@ -128,8 +150,76 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   }
   const Plan& plan = *it->second;
   if (plan.max_k > FTAR_MAX_K) return FTAR_ERR_UNSUPPORTED;
+  const size_t nst = plan.stages.size();
 
-  const size_t need = 2 * plan.scratch_half * esz;
+  // Host mode: the buffers are in host memory and move through a device
+  // staging buffer, piece by piece, so H2D (PCIe in), the exchange, and D2H
+  // (PCIe out) run at the same time.  Every src/dst transfer and reduce of a
+  // plan covers whole blocks from their start (tests/test_plan.py), so piece
+  // k of every stage touches exactly piece k of each block: the same bytes,
+  // the same partition, the same bits as the device path.
+  size_t chunk_bytes = host ? c->host_chunk_bytes : c->chunk_bytes;
+  if (host) {
+    if (count * esz > c->staging_bytes) {
+      if (c->staging) {
+        FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
+        FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
+        FTAR_CHECK_HIP(hipStreamSynchronize(c->d2h_s));
+        FTAR_CHECK_HIP(hipFree(c->staging));
+        c->staging = nullptr;
+        c->staging_bytes = 0;
+      }
+      FTAR_CHECK_HIP(hipMalloc(&c->staging, count * esz));
+      c->staging_bytes = count * esz;
+    }
+    sendbuf = nullptr;
+    recvbuf = c->staging;
+  }
+  size_t chunk = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63));
+  const size_t nchunks = std::max<size_t>(1, (plan.split + chunk - 1) / chunk);
+
+  // per-stage facts: the latest reducing stage before it (its data), and in
+  // the device (stage-major) order the last reader of the scratch half it
+  // receives into
+  std::vector<char> moves(nst), reduces(nst), to_scratch(nst);
+  std::vector<long> prev_red(nst, -1), war(nst, -1);
+  {
+    long last = -1, owner[2] = {-1, -1};
+    for (size_t s = 0; s < nst; ++s) {
+      const Stage& st = plan.stages[s];
+      moves[s] = !st.sends.empty() || !st.recvs.empty();
+      reduces[s] = !st.reduces.empty();
+      for (const Transfer& x : st.recvs) to_scratch[s] |= x.buf == BUF_SCRATCH;
+      prev_red[s] = last;
+      war[s] = to_scratch[s] ? owner[s % 2] : -1;
+      if (reduces[s]) {
+        last = (long)s;
+        if (to_scratch[s]) owner[s % 2] = (long)s;
+      }
+    }
+  }
+  // Order of the (stage, piece) steps, identical on every rank.  Device:
+  // stage-major.  Host: stage s+1 trails stage s by one piece, so the
+  // all-gather of piece k (and its D2H) runs while later pieces are still
+  // coming in over PCIe.  Skewed steps of stages two apart may overlap in
+  // time, so there every stage gets its own scratch region instead of
+  // alternating halves (scratch offsets remapped by delta[s]).
+  const bool skew = host != nullptr;
+  std::vector<long> delta(nst, 0);
+  size_t scratch_elems = 2 * plan.scratch_half;
+  if (skew) {
+    size_t base = 0;
+    for (size_t s = 0; s < nst; ++s) {
+      const size_t half_base = (s % 2) * plan.scratch_half;
+      size_t used = 0;
+      for (const Transfer& x : plan.stages[s].recvs)
+        if (x.buf == BUF_SCRATCH) used = std::max(used, x.off - half_base + x.len);
+      delta[s] = (long)base - (long)half_base;
+      base += used;
+    }
+    scratch_elems = base;
+  }
+  const size_t need = scratch_elems * esz;
   if (need > c->scratch_bytes) {
     if (c->scratch) {  // work of earlier calls may still read it
       FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
@@ -141,73 +231,114 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_CHECK_HIP(hipMalloc(&c->scratch, need));
     c->scratch_bytes = need;
   }
+  std::vector<std::pair<size_t, size_t>> order;
+  order.reserve(nst * nchunks);
+  if (!skew) {
+    for (size_t s = 0; s < nst; ++s)
+      for (size_t k = 0; k < nchunks; ++k) order.emplace_back(s, k);
+  } else {
+    for (size_t tt = 0; tt < nchunks + nst - 1; ++tt)
+      for (size_t s = 0; s < nst && s <= tt; ++s)
+        if (tt - s < nchunks) order.emplace_back(s, tt - s);
+  }
 
-  size_t chunk = std::max<size_t>(1, (c->chunk_bytes / esz) & ~size_t(63));
-  if (chunk == 0) chunk = 64;
-  const size_t nchunks = std::max<size_t>(1, (plan.split + chunk - 1) / chunk);
-  const size_t nst = plan.stages.size();
-  FTAR_RETURN_IF(grow_events(c, 2 * nst * nchunks + 3));
+  FTAR_RETURN_IF(grow_events(c, 2 * nst * nchunks + 2 * nchunks + 5));
   hipEvent_t* ev = c->events.data();
-  auto ev_x = [&](size_t s, size_t k) { return ev[3 + (s * nchunks + k) * 2]; };
-  auto ev_r = [&](size_t s, size_t k) { return ev[3 + (s * nchunks + k) * 2 + 1]; };
+  auto ev_x = [&](size_t s, size_t k) { return ev[5 + (s * nchunks + k) * 2]; };
+  auto ev_r = [&](size_t s, size_t k) { return ev[5 + (s * nchunks + k) * 2 + 1]; };
+  auto ev_h = [&](size_t k) { return ev[5 + 2 * nst * nchunks + 2 * k]; };
+  auto ev_d = [&](size_t k) { return ev[5 + 2 * nst * nchunks + 2 * k + 1]; };
 
   char* bufs[3] = {static_cast<char*>(const_cast<void*>(sendbuf ? sendbuf : recvbuf)), static_cast<char*>(recvbuf),
                    static_cast<char*>(c->scratch)};
   Transport* tp = c->tp.get();
+  const size_t P = (size_t)c->nranks, split = plan.split;
+  // piece k of every block: [b*split + k*chunk, ...) clipped to the block and to count
+  auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {
+    for (size_t b = 0; b < P; ++b) {
+      const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
+      if (lo < end) FTAR_RETURN_IF(fn(lo, std::min(chunk, end - lo)));
+    }
+    return FTAR_SUCCESS;
+  };
 
   FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev[0], 0));
-
-  long last_red = -1;
-  long half_owner[2] = {-1, -1};  // last reducing stage that read each scratch half
-  std::vector<const void*> srcs;
-  for (size_t s = 0; s < nst; ++s) {
-    const Stage& st = plan.stages[s];
-    const bool moves = !st.sends.empty() || !st.recvs.empty();
-    bool to_scratch = false;
-    for (const Transfer& x : st.recvs) to_scratch |= x.buf == BUF_SCRATCH;
-    // WAR on the scratch half this stage receives into: every reduce that read it
-    // (stage s-2, or earlier when stages in between were empty) must be done.
-    // When stage s-1 reduced, its piece-0 event already implies this (the reduce
-    // stream runs in order), so the wait is free; it matters when s-1 was empty.
-    if (to_scratch && half_owner[s % 2] >= 0)
-      FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)half_owner[s % 2], nchunks - 1), 0));
+  if (host) {  // all pieces in, in order, on their own stream (the DMA engines run ahead)
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->h2d_s, ev[0], 0));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev[0], 0));
     for (size_t k = 0; k < nchunks; ++k) {
-      const size_t lo = k * chunk;
-      if (moves) {
-        if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, k), 0));
-        FTAR_RETURN_IF(tp->group_start());
-        for (const Transfer& x : st.sends)
-          if (x.len > lo)
-            FTAR_RETURN_IF(tp->send(bufs[x.buf] + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz, x.peer,
-                                    c->comm_s));
-        for (const Transfer& x : st.recvs)
-          if (x.len > lo)
-            FTAR_RETURN_IF(tp->recv(bufs[x.buf] + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz, x.peer,
-                                    c->comm_s));
-        FTAR_RETURN_IF(tp->group_end());
-      }
-      if (!st.reduces.empty()) {
-        FTAR_CHECK_HIP(hipEventRecord(ev_x(s, k), c->comm_s));
-        FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev_x(s, k), 0));
-        for (const ReduceItem& r : st.reduces) {
-          if (r.len <= lo) continue;
-          srcs.clear();
-          for (const Operand& o : r.srcs) srcs.push_back(bufs[o.buf] + (o.off + lo) * esz);
-          FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), bufs[BUF_DST] + (r.off + lo) * esz,
-                                       std::min(chunk, r.len - lo), dt, op, c->red_s, r.round_each,
-                                       r.shape.data(), (int)r.shape.size()));
-        }
-        FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
-      }
+      FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(hipMemcpyAsync(bufs[BUF_DST] + lo * esz, host->src + lo * esz, n * esz,
+                                      hipMemcpyHostToDevice, c->h2d_s));
+        return FTAR_SUCCESS;
+      }));
+      FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
     }
-    if (!st.reduces.empty()) {
-      last_red = (long)s;
-      if (to_scratch) half_owner[s % 2] = (long)s;
+  }
+  std::vector<char> comm_has_input(host ? nchunks : 0), red_has_input(host ? nchunks : 0);
+  std::vector<const void*> srcs;
+  auto sbuf = [&](int buf, size_t off, size_t s) -> char* {
+    return bufs[buf] + (buf == BUF_SCRATCH ? (size_t)((long)off + delta[s]) : off) * esz;
+  };
+  for (const auto& step : order) {
+    const size_t s = step.first, k = step.second, lo = k * chunk;
+    const Stage& st = plan.stages[s];
+    if (moves[s]) {
+      if (host && !comm_has_input[k]) {
+        FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k), 0));
+        comm_has_input[k] = 1;
+      }
+      // WAR on the scratch half this stage receives into (stage-major only):
+      // every reduce that read it (stage s-2, or earlier when stages in between
+      // were empty) must be done.  When stage s-1 reduced, its piece-0 event
+      // already implies this (the reduce stream runs in order), so the wait is
+      // free; it matters when s-1 was empty.
+      if (!skew && k == 0 && war[s] >= 0)
+        FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)war[s], nchunks - 1), 0));
+      if (prev_red[s] >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)prev_red[s], k), 0));
+      FTAR_RETURN_IF(tp->group_start());
+      for (const Transfer& x : st.sends)
+        if (x.len > lo)
+          FTAR_RETURN_IF(tp->send(sbuf(x.buf, x.off + lo, s), std::min(chunk, x.len - lo) * esz, x.peer, c->comm_s));
+      for (const Transfer& x : st.recvs)
+        if (x.len > lo)
+          FTAR_RETURN_IF(tp->recv(sbuf(x.buf, x.off + lo, s), std::min(chunk, x.len - lo) * esz, x.peer, c->comm_s));
+      FTAR_RETURN_IF(tp->group_end());
+    }
+    if (reduces[s]) {
+      FTAR_CHECK_HIP(hipEventRecord(ev_x(s, k), c->comm_s));
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev_x(s, k), 0));
+      if (host && !red_has_input[k]) {
+        FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev_h(k), 0));
+        red_has_input[k] = 1;
+      }
+      for (const ReduceItem& r : st.reduces) {
+        if (r.len <= lo) continue;
+        srcs.clear();
+        for (const Operand& o : r.srcs) srcs.push_back(sbuf(o.buf, o.off + lo, s));
+        FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), bufs[BUF_DST] + (r.off + lo) * esz,
+                                     std::min(chunk, r.len - lo), dt, op, c->red_s, r.round_each, r.shape.data(),
+                                     (int)r.shape.size()));
+      }
+      FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
+    }
+    if (host && s == nst - 1) {  // piece k is final everywhere: out over PCIe while later pieces come in
+      FTAR_CHECK_HIP(hipEventRecord(ev_d(k), reduces[s] ? c->red_s : c->comm_s));
+      if (reduces[s]) FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_x(s, k), 0));
+      else if (prev_red[s] >= 0)  // a rank idle in the last stage: its block's final fold
+        FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_r((size_t)prev_red[s], k), 0));
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_d(k), 0));
+      FTAR_RETURN_IF(for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(hipMemcpyAsync(host->dst + lo2 * esz, bufs[BUF_DST] + lo2 * esz, n * esz,
+                                      hipMemcpyDeviceToHost, c->d2h_s));
+        return FTAR_SUCCESS;
+      }));
     }
   }
   if (plan.allgather == FTAR_AG_COLLECTIVE) {  // the whole all-gather phase as one collective, in place
+    const long last_red = nst ? (reduces[nst - 1] ? (long)nst - 1 : prev_red[nst - 1]) : -1;
     if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, nchunks - 1), 0));
     FTAR_RETURN_IF(tp->allgather(bufs[BUF_DST] + (size_t)c->rank * plan.split * esz, bufs[BUF_DST], plan.split * esz,
                                  c->rank, c->nranks, c->comm_s));
@@ -216,6 +347,12 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   FTAR_CHECK_HIP(hipEventRecord(ev[2], c->red_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[2], 0));
+  if (host) {
+    FTAR_CHECK_HIP(hipEventRecord(ev[3], c->h2d_s));
+    FTAR_CHECK_HIP(hipEventRecord(ev[4], c->d2h_s));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[3], 0));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[4], 0));
+  }
   return FTAR_SUCCESS;
 }
 
@@ -349,6 +486,27 @@ ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
   return ftar::allreduce(sendbuf, recvbuf, count, dtype, op, topo, comm, static_cast<hipStream_t>(stream));
 }
 
+ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
+                                  const ftar_topo_t* topo, ftar_comm_t comm, void* stream) {
+  if (!recvbuf && count) return FTAR_ERR_INVALID_ARG;
+  const ftar::HostIO io{static_cast<const char*>(sendbuf ? sendbuf : recvbuf), static_cast<char*>(recvbuf)};
+  return ftar::allreduce(sendbuf, recvbuf ? recvbuf : io.dst, count, dtype, op, topo, comm,
+                         static_cast<hipStream_t>(stream), &io);
+}
+
+ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->host_chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : ftar::kDefaultHostChunkBytes;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_get_host_chunk_bytes(ftar_comm_t comm, size_t* bytes) {
+  if (!comm || !bytes) return FTAR_ERR_INVALID_ARG;
+  *bytes = comm->host_chunk_bytes;
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
                                   ftar_comm_t comm, void* stream) {
   if (!comm || !recvbuf) return FTAR_ERR_INVALID_ARG;
@@ -358,16 +516,19 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
                                     static_cast<hipStream_t>(stream));
 }
 
-ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
-                                   ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
-                                   int nranks, void* const* streams) {
+namespace {
+ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size_t count, ftar_dtype_t dtype,
+                        ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms, int nranks,
+                        void* const* streams, bool host) {
   if (!recvbufs || !comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
   std::vector<ftar_status_t> st(nranks, FTAR_SUCCESS);
   std::vector<std::thread> th;
   for (int r = 0; r < nranks; ++r)
     th.emplace_back([&, r] {
       hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;
-      st[r] = ftar::allreduce(sendbufs ? sendbufs[r] : nullptr, recvbufs[r], count, dtype, op, topo, comms[r], s);
+      const void* sb = sendbufs ? sendbufs[r] : nullptr;
+      st[r] = host ? ftar_allreduce_host(sb, recvbufs[r], count, dtype, op, topo, comms[r], s)
+                   : ftar::allreduce(sb, recvbufs[r], count, dtype, op, topo, comms[r], s);
       if (st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
           hipStreamSynchronize(s) != hipSuccess)
         st[r] = FTAR_ERR_HIP;
@@ -376,6 +537,19 @@ ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* rec
   for (int r = 0; r < nranks; ++r)
     if (st[r] != FTAR_SUCCESS) return st[r];
   return FTAR_SUCCESS;
+}
+}  // namespace
+
+ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
+                                   ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
+                                   int nranks, void* const* streams) {
+  return run_group(sendbufs, recvbufs, count, dtype, op, topo, comms, nranks, streams, false);
+}
+
+ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
+                                        ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo,
+                                        ftar_comm_t* comms, int nranks, void* const* streams) {
+  return run_group(sendbufs, recvbufs, count, dtype, op, topo, comms, nranks, streams, true);
 }
 
 }  // extern "C"

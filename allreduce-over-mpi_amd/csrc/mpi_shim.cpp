@@ -5,10 +5,10 @@
 //   get_stages() every call (:1732)         FT_TOPO/FT_LONELY read once per communicator
 //   FlexTree_Context (:1734)                ftar plan cache (per topology, count)
 //   P <= 1 -> memcpy (:1739-1746)           same, on the host
-//   static grow-only host recv_buffer       grow-only DEVICE buffer per communicator
+//   static grow-only host recv_buffer       grow-only DEVICE staging buffer per communicator
 //   (:1489-1507, never freed)               (freed by MPI_Allreduce_FT_finalize)
-//   ring/tree over MPI_Isend/Irecv          H2D -> ftar_allreduce (RCCL p2p + HIP reduce) -> D2H
-//   + 14-thread OpenMP reduce
+//   ring/tree over MPI_Isend/Irecv          ftar_allreduce_host: H2D, RCCL p2p + HIP reduce and
+//   + 14-thread OpenMP reduce               D2H pipelined piece by piece (PCIe in and out overlap)
 //   MPI_Comm_split every call, leaked       nothing per call; RCCL comm built once
 //   (:1541-1548)
 // The caller's buffers are page-locked on first use (hipHostRegister, cached)
@@ -29,8 +29,6 @@ struct Entry {
   ftar_comm_t comm = nullptr;
   int rank = 0, size = 1, device = 0;
   hipStream_t stream = nullptr;
-  void* dbuf = nullptr;
-  size_t dbuf_bytes = 0;
 };
 
 std::mutex g_mu;
@@ -146,21 +144,12 @@ int MPI_Allreduce_FT(const void* sendbuf, void* recvbuf, int count, MPI_Datatype
     return MPI_SUCCESS;
   }
   if ((rc = ensure_stream(e)) != MPI_SUCCESS) return rc;
-  if (bytes > e->dbuf_bytes) {
-    if (e->dbuf) (void)hipFree(e->dbuf);
-    e->dbuf = nullptr;
-    e->dbuf_bytes = 0;
-    if (hipMalloc(&e->dbuf, bytes) != hipSuccess) return MPI_ERR_NO_MEM;
-    e->dbuf_bytes = bytes;
-  }
   maybe_register(src, bytes);
   maybe_register(recvbuf, bytes);
-  if (bytes && hipMemcpyAsync(e->dbuf, src, bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess)
-    return MPI_ERR_OTHER;
-  if (ftar_allreduce(nullptr, e->dbuf, (size_t)count, dt, fo, nullptr, e->comm, e->stream) != FTAR_SUCCESS)
-    return MPI_ERR_OTHER;
-  if (bytes && hipMemcpyAsync(recvbuf, e->dbuf, bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
-    return MPI_ERR_OTHER;
+  const ftar_status_t st = ftar_allreduce_host(src == recvbuf ? nullptr : src, recvbuf, (size_t)count, dt, fo,
+                                               nullptr, e->comm, e->stream);
+  if (st == FTAR_ERR_HIP && hipGetLastError() == hipErrorOutOfMemory) return MPI_ERR_NO_MEM;
+  if (st != FTAR_SUCCESS) return MPI_ERR_OTHER;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return MPI_ERR_OTHER;
   return MPI_SUCCESS;
 }
@@ -197,7 +186,6 @@ int MPI_Allreduce_FT_finalize(void) {
     (void)hipSetDevice(e.device);
     if (e.stream) (void)hipStreamSynchronize(e.stream);
     if (e.comm) ftar_comm_destroy(e.comm);
-    if (e.dbuf) (void)hipFree(e.dbuf);
     if (e.stream) (void)hipStreamDestroy(e.stream);
   }
   g_entries.clear();

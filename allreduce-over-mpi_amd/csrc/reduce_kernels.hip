@@ -54,12 +54,15 @@ __device__ __forceinline__ void st16(u32x4* p, u32x4 v) {
 }
 
 __device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
-__device__ __forceinline__ unsigned short f32_to_bf16(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+// RNE to bf16; NaN stays NaN (quieted, sign and top payload kept).  Written as
+// a select, not an early return: a per-element NaN branch compiles to exec-mask
+// save/restore around every conversion.
+__device__ __forceinline__ unsigned bf16_round_bits(float f) {  // result in the high half
+  const unsigned u = __float_as_uint(f);
+  const unsigned rne = u + 0x7fffu + ((u >> 16) & 1u);
+  return ((u & 0x7fffffffu) > 0x7f800000u ? (u | 0x00400000u) : rne) & 0xffff0000u;
 }
+__device__ __forceinline__ unsigned short f32_to_bf16(float f) { return (unsigned short)(bf16_round_bits(f) >> 16); }
 
 // ---------------------------------------------------------------------------
 // element traits: scalar (S*) and 16-byte vector (V*) forms of one (dtype, op)
@@ -116,15 +119,13 @@ struct BF16Sum {
     VA b = v_init(x);
     return {a.lo + b.lo, a.hi + b.hi};
   }
-  __device__ static unsigned pack(float lo, float hi) {
-    return (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
-  }
+  __device__ static unsigned pack(float lo, float hi) { return (bf16_round_bits(lo) >> 16) | bf16_round_bits(hi); }
   __device__ static u32x4 v_fin(VA a) {
     return u32x4{pack(a.lo.x, a.lo.y), pack(a.lo.z, a.lo.w), pack(a.hi.x, a.hi.y), pack(a.hi.z, a.hi.w)};
   }
   // nested folds: an inner node's value is stored as bf16 by the staged
   // schedule, so it is rounded before its parent adds it
-  __device__ static float rnd(float f) { return bf16_to_f32(f32_to_bf16(f)); }
+  __device__ static float rnd(float f) { return __uint_as_float(bf16_round_bits(f)); }
   __device__ static f32x4 rnd4(f32x4 v) { return f32x4{rnd(v.x), rnd(v.y), rnd(v.z), rnd(v.w)}; }
   __device__ static SA s_add(SA a, SA b) { return a + b; }
   __device__ static SA s_rnd(SA a) { return rnd(a); }

@@ -105,6 +105,11 @@ _lib.ftar_allreduce.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(Topo),
 _lib.ftar_rccl_allreduce.argtypes = [_vp, _vp, _sz, _int, _int, _vp, _vp]
 _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int, ctypes.POINTER(Topo),
                                       ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
+_lib.ftar_allreduce_host.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(Topo), _vp, _vp]
+_lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int,
+                                           ctypes.POINTER(Topo), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
+_lib.ftar_comm_set_host_chunk_bytes.argtypes = [_vp, _sz]
+_lib.ftar_comm_get_host_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
 _lib.ftar_schedule_json.restype = ctypes.c_long
 _lib.ftar_plan_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, _int, _int, ctypes.c_char_p, _sz]
@@ -152,7 +157,9 @@ def _ptr(x):
         return x
     if hasattr(x, "data_ptr"):
         return x.data_ptr()
-    raise TypeError(f"not a device pointer: {type(x)}")
+    if hasattr(x, "__array_interface__"):  # numpy (host buffers of the host-mode calls)
+        return x.__array_interface__["data"][0]
+    raise TypeError(f"not a buffer pointer: {type(x)}")
 
 
 def _stream(s):
@@ -311,6 +318,23 @@ class Comm:
                                  _stream(stream))
         _check(st, "ftar_allreduce")
 
+    def allreduce_host(self, sendbuf, recvbuf, count, dtype="f32", op="sum", topo_=None, lonely=0, stream=None):
+        """AllReduce of HOST buffers (pinned for overlap), H2D/exchange/D2H pipelined (ftar_allreduce_host)."""
+        t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
+        st = _lib.ftar_allreduce_host(_ptr(sendbuf), _ptr(recvbuf), count, _dt(dtype), _op(op), t, self.handle,
+                                      _stream(stream))
+        _check(st, "ftar_allreduce_host")
+
+    @property
+    def host_chunk_bytes(self):
+        v = _sz()
+        _check(_lib.ftar_comm_get_host_chunk_bytes(self.handle, ctypes.byref(v)), "host_chunk_bytes")
+        return v.value
+
+    @host_chunk_bytes.setter
+    def host_chunk_bytes(self, b):
+        _check(_lib.ftar_comm_set_host_chunk_bytes(self.handle, b), "host_chunk_bytes")
+
     @property
     def allgather(self):
         """All-gather form: "direct" (default), "stages" (the reference's rounds) or "collective"."""
@@ -382,19 +406,26 @@ class LocalGroup:
         for c in self.comms:
             c.allgather = mode
 
+    def set_host_chunk_bytes(self, b):
+        for c in self.comms:
+            c.host_chunk_bytes = b
+
     def set_reduce_scatter(self, mode):
         for c in self.comms:
             c.reduce_scatter = mode
 
-    def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None):
+    def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None,
+                  host=False):
+        """Every rank at once; host=True: the buffers are host memory (ftar_allreduce_host_group)."""
         P = len(self.comms)
         t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
         sb = None if sendbufs is None else (_vp * P)(*[_ptr(x) for x in sendbufs])
         rb = (_vp * P)(*[_ptr(x) for x in recvbufs])
         hs = (_vp * P)(*[c.handle for c in self.comms])
         ss = None if streams is None else (_vp * P)(*[_stream(s) for s in streams])
-        st = _lib.ftar_allreduce_group(sb, rb, count, _dt(dtype), _op(op), t, hs, P, ss)
-        _check(st, "ftar_allreduce_group")
+        fn = _lib.ftar_allreduce_host_group if host else _lib.ftar_allreduce_group
+        st = fn(sb, rb, count, _dt(dtype), _op(op), t, hs, P, ss)
+        _check(st, "ftar_allreduce_host_group" if host else "ftar_allreduce_group")
 
     def allreduce_tensors(self, tensors, op="sum", topo_=None, lonely=0):
         """In-place AllReduce of one contiguous device tensor per rank (same shape and dtype)."""

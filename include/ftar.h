@@ -188,6 +188,26 @@ ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* rec
                                    ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
                                    int nranks, void* const* streams);
 
+/* ---- AllReduce of HOST buffers (the reference's own setting) ---------------
+ * Replaces MPI_Allreduce_FT's host-memory contract (mpi_mod.hpp:1723-1778).
+ * sendbuf/recvbuf are host memory (sendbuf == NULL or == recvbuf: in place);
+ * page-lock them (hipHostRegister / hipHostMalloc) or the copies are not
+ * asynchronous.  The bucket moves through a grow-only device staging buffer in
+ * pieces of host_chunk_bytes per block: H2D of later pieces, the exchange and
+ * reduce of the current ones, and D2H of finished ones run at once (stage s+1
+ * trails stage s by one piece), so PCIe in and out overlap.  Same blocks,
+ * same fold order, same bits as ftar_allreduce.  Enqueued on `stream`; the
+ * host buffers must stay untouched until it completes. */
+ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype,
+                                  ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t comm, void* stream);
+ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
+                                        ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo,
+                                        ftar_comm_t* comms, int nranks, void* const* streams);
+/* Host-mode piece size per block (bytes, rounded to 256 B); 0 = default 4 MiB
+ * (FTAR_HOST_CHUNK_BYTES at init). */
+ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes);
+ftar_status_t ftar_comm_get_host_chunk_bytes(ftar_comm_t comm, size_t* bytes);
+
 /* ---- diagnostics ---------------------------------------------------------------
  * RCCL's own ncclAllReduce on the communicator's RCCL comm (ring/tree of the
  * vendor library, reduction inside RCCL): the yardstick bench.py reports next

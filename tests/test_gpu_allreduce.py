@@ -199,3 +199,82 @@ def test_direct_tree_matches_reference_tree(P, topo, dt):
     ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
     for r in range(P):
         assert outs[r].tobytes() == ref[r].tobytes()
+
+
+# ---- host buffers (ftar_allreduce_host: H2D / exchange / D2H pipelined) --------------------------------
+def run_group_host(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, host_chunk=0, ag="direct", rs="direct",
+                   pinned=True, repeat=1):
+    import torch
+    g = group(len(ins))
+    g.set_host_chunk_bytes(host_chunk)
+    g.set_allgather(ag)
+    g.set_reduce_scatter(rs)
+    n = ins[0].size
+
+    def host(x):
+        if not pinned:
+            return x.copy()
+        t = torch.from_numpy(x.view(np.uint8).copy()).pin_memory()
+        return t
+
+    send = [host(x) for x in ins]
+    recv = [host(np.frombuffer(b"\xa5" * x.nbytes, dtype=np.uint8)) for x in ins] if outofplace else send
+    for it in range(repeat):
+        g.allreduce(send if outofplace else None, recv, n, dtype, op, topo_=topo, lonely=lonely, host=True)
+        if outofplace and it + 1 < repeat:
+            send, recv = recv, send
+    out = []
+    for r in recv:
+        a = r.numpy() if hasattr(r, "numpy") else r
+        out.append(np.ascontiguousarray(a).view(np.uint8).view(ins[0].dtype)[:n].copy())
+    return out
+
+
+@pytest.mark.parametrize("case", [c for c in gc.allreduce_cases(max_n=70000) if c["n"] >= 1003 or c["P"] <= 4],
+                         ids=lambda c: c["id"])
+def test_host_allreduce_matches_reference_golden(case):
+    """MPI_Allreduce_FT's own setting (host buffers): every golden case, bit-exact per rank."""
+    ins = gc.case_inputs(case)
+    outs = run_group_host(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                          repeat=case["repeat"])
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
+@pytest.mark.parametrize("P,topo,lonely", [(2, "1", 0), (8, "1", 0), (4, "2,2", 0), (8, "8", 0), (8, "2,2,2", 0),
+                                           (5, "2,2", 1), (8, "3,2", 2), (13, "2,2,3", 1)])
+@pytest.mark.parametrize("form", ["direct", "stages"])
+@pytest.mark.parametrize("host_chunk", [256, 4096])
+def test_host_allreduce_skewed_pieces(P, topo, lonely, form, host_chunk):
+    """Many pieces: stage s+1 trails stage s by one piece, per-stage scratch regions, D2H of piece k while
+    piece k+1.. is still coming in; staged forms (many stages) included.  Bit-exact vs the oracle."""
+    n = 50_003
+    ins = [fi.fill("f32", 41, r, n) for r in range(P)]
+    outs = run_group_host(ins, topo, lonely, host_chunk=host_chunk, ag=form, rs=form)
+    ref = oracle_lib.allreduce(ins, topo, lonely)
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes(), r
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f64", "i16", "u8"])
+def test_host_allreduce_dtypes_pageable_and_out_of_place(dt):
+    """Pageable (unpinned) host memory still gives the right bits; out of place; non-float dtypes."""
+    P, n = 4, 77_777
+    ins = [fi.fill(dt, 42, r, n) for r in range(P)]
+    ref = oracle_lib.allreduce(ins, "2,2", dtype=fi.BY_NAME[dt])
+    for pinned in (True, False):
+        outs = run_group_host(ins, "2,2", dtype=fi.BY_NAME[dt], outofplace=True, host_chunk=8192, pinned=pinned)
+        for r in range(P):
+            assert outs[r].tobytes() == ref[r].tobytes(), (pinned, r)
+
+
+def test_host_allreduce_then_device_allreduce_share_a_comm():
+    """Host-mode and device-mode calls interleave on one communicator (different scratch layouts)."""
+    P, n = 8, 100_000
+    ins = [fi.fill("f32", 43, r, n) for r in range(P)]
+    ref = oracle_lib.allreduce(ins, "2,4")
+    for _ in range(2):
+        outs = run_group_host(ins, "2,4", host_chunk=4096, ag="stages", rs="stages")
+        assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P))
+        outs = run_group(ins, "2,4", chunk_bytes=4096, ag="stages", rs="stages")
+        assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P))

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: smoke, GPU tests, bench, rocprof. Every GPU step has its
 # own time limit; a fault/abort/timeout (exit >= 124) stops the script there.
-# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree dist1
+# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host dist1
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -29,6 +29,7 @@ for s in "${steps[@]}"; do
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ktree) run kbench_tree 600 python tools/kbench.py --rounds 8 --dtypes f32,bf16 --shapes "8;2,4;4,2;2,2,2;4;2,2;16;4,4;2,2,2,2" ;;
+    host) run hostpath 600 python tools/hostpath.py ;;
     dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 --elements 16777216 ;;
     *) echo "unknown step $s" ;;
   esac

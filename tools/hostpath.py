@@ -2,9 +2,12 @@
 """Host-memory end-to-end rate of the AllReduce path (DESIGN.md §Host path).
 
 The reference's buffers live in host memory (MPI send/recv buffers,
-benchmark.cpp:125-131); MPI_Allreduce_FT here does H2D -> device AllReduce ->
-D2H.  Measured on one MI355X: pinned H2D and D2H of one bucket, the device
-AllReduce of P in-process ranks, and the whole host->host call, per bucket size.
+benchmark.cpp:125-131).  Measured on one MI355X: pinned H2D and D2H of one
+bucket alone and both directions at once, the device AllReduce of P
+in-process ranks, the serial host->host call (H2D, AllReduce, D2H), and
+ftar_allreduce_host (H2D / exchange / D2H pipelined per piece; the
+MPI_Allreduce_FT path) at several piece sizes.  With P ranks on one GPU all
+ranks share this GPU's PCIe link, so pcie_GBps = P * bucket / t per direction.
 """
 import json
 import os
@@ -41,8 +44,18 @@ for n in (1 << 20, 1 << 26, 1 << 28):
     t_h2d = timeit(lambda: d.copy_(h, non_blocking=True))
     t_d2h = timeit(lambda: hp.copy_(d, non_blocking=True))
     t_d2h_pageable = timeit(lambda: hpg.copy_(d))
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    d2 = torch.empty(n, device=dev)
+
+    def both():
+        with torch.cuda.stream(s1):
+            d.copy_(h, non_blocking=True)
+        with torch.cuda.stream(s2):
+            hp.copy_(d2, non_blocking=True)
+    t_both = timeit(both)
     row = {"bytes": nbytes, "h2d_GBps": round(nbytes / t_h2d / 1e9, 2), "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
-           "d2h_pageable_GBps": round(nbytes / t_d2h_pageable / 1e9, 2)}
+           "d2h_pageable_GBps": round(nbytes / t_d2h_pageable / 1e9, 2),
+           "h2d_and_d2h_concurrent_GBps_per_dir": round(nbytes / t_both / 1e9, 2)}
     for P, topo in ((2, "2"), (8, "8")):
         if n > (1 << 26) and P > 2:
             continue
@@ -60,6 +73,12 @@ for n in (1 << 20, 1 << 26, 1 << 28):
         t_e2e = timeit(e2e)
         row[f"P{P}_device_ms"] = round(t_dev * 1e3, 3)
         row[f"P{P}_host_e2e_ms"] = round(t_e2e * 1e3, 3)
+        for chunk in (1 << 30, 16 << 20, 4 << 20, 1 << 20):  # 1 GiB = one piece per block: serial
+            g.set_host_chunk_bytes(chunk)
+            t_h = timeit(lambda: g.allreduce(None, hs, n, "f32", topo_=topo, host=True))
+            row[f"P{P}_host_pipelined_c{chunk >> 20}MiB_ms"] = round(t_h * 1e3, 3)
+            row[f"P{P}_host_pipelined_c{chunk >> 20}MiB_pcie_GBps"] = round(P * nbytes / t_h / 1e9, 2)
+        g.set_host_chunk_bytes(0)
         g.destroy()
         del ds, hs
     out.append(row)
