@@ -4,7 +4,9 @@
     rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d OUT -o run -- \
         python3 tools/engine_trace.py --ranks 8 --topo 8 --elements 67108864
 then `python tools/engine_trace.py --analyze OUT/run_kernel_trace.csv OUT/run_memory_copy_trace.csv`
-reports how much reduce-kernel time overlaps the transfers (copies).
+reports how much reduce-kernel time overlaps the transfers (copies), and per
+copy direction the busy time and how much host->device and device->host
+copies overlap each other (--host: ftar_allreduce_host on pinned buffers).
 """
 import argparse
 import csv
@@ -18,6 +20,8 @@ ap.add_argument("--topo", default="8")
 ap.add_argument("--elements", type=int, default=1 << 26)
 ap.add_argument("--chunk-bytes", type=int, default=16 << 20)
 ap.add_argument("--iters", type=int, default=3)
+ap.add_argument("--host", action="store_true", help="host buffers (ftar_allreduce_host)")
+ap.add_argument("--host-chunk-bytes", type=int, default=0)
 ap.add_argument("--analyze", nargs=2, metavar=("KERNEL_CSV", "COPY_CSV"))
 a = ap.parse_args()
 
@@ -64,9 +68,25 @@ if a.analyze:
     cu = union(sorted(copies))
     red_t = sum(e - s for s, e in red)
     ov = overlap(red, cu)
-    print(json.dumps({"reduce_kernels": len(red), "reduce_ns": red_t, "copy_ops": len(copies),
-                      "copy_busy_ns": sum(e - s for s, e in cu), "reduce_overlapped_ns": ov,
-                      "reduce_overlap_frac": round(ov / red_t, 4) if red_t else None}))
+    res = {"reduce_kernels": len(red), "reduce_ns": red_t, "copy_ops": len(copies),
+           "copy_busy_ns": sum(e - s for s, e in cu), "reduce_overlapped_ns": ov,
+           "reduce_overlap_frac": round(ov / red_t, 4) if red_t else None}
+    if os.path.exists(ccsv):
+        kinds = {}
+        for r in rows:
+            kinds.setdefault(r.get("Direction", r.get("Operation", "?")), []).append(
+                (int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        for kd, iv in kinds.items():
+            u = union(sorted(iv))
+            res[f"{kd}_ops"] = len(iv)
+            res[f"{kd}_busy_ns"] = sum(e - s for s, e in u)
+            res[f"{kd}_span_ns"] = u[-1][1] - u[0][0]
+        h2d = [k for k in kinds if "HOST_TO_DEVICE" in k.upper()]
+        d2h = [k for k in kinds if "DEVICE_TO_HOST" in k.upper()]
+        if h2d and d2h:
+            uh, ud = union(sorted(kinds[h2d[0]])), union(sorted(kinds[d2h[0]]))
+            res["h2d_d2h_overlap_ns"] = overlap([tuple(x) for x in uh], ud)
+    print(json.dumps(res))
     sys.exit(0)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -76,9 +96,13 @@ import ftar  # noqa: E402
 
 g = ftar.Comm.init_local(a.ranks)
 g.set_chunk_bytes(a.chunk_bytes)
-bufs = [torch.rand(a.elements, device="cuda") for _ in range(a.ranks)]
+g.set_host_chunk_bytes(a.host_chunk_bytes)
+if a.host:
+    bufs = [torch.rand(a.elements).pin_memory() for _ in range(a.ranks)]
+else:
+    bufs = [torch.rand(a.elements, device="cuda") for _ in range(a.ranks)]
 for _ in range(a.iters):
-    g.allreduce(None, bufs, a.elements, "f32", topo_=a.topo)
+    g.allreduce(None, bufs, a.elements, "f32", topo_=a.topo, host=a.host)
 torch.cuda.synchronize()
 g.destroy()
 print("done")

@@ -33,9 +33,15 @@ def timeit(fn, reps=5):
     return best
 
 
+import argparse  # noqa: E402
+ap = argparse.ArgumentParser()
+ap.add_argument("--sizes", default="20,26,28", help="log2 elements per bucket")
+ap.add_argument("--chunks", default="1024,16,4,1", help="host piece sizes in MiB (1024 = one piece: serial)")
+ap.add_argument("--ranks", default="2,8")
+a = ap.parse_args()
 dev = torch.device("cuda:0")
 out = []
-for n in (1 << 20, 1 << 26, 1 << 28):
+for n in [1 << int(x) for x in a.sizes.split(",")]:
     nbytes = n * 4
     h = torch.rand(n).pin_memory()
     hp = torch.empty(n).pin_memory()
@@ -56,7 +62,8 @@ for n in (1 << 20, 1 << 26, 1 << 28):
     row = {"bytes": nbytes, "h2d_GBps": round(nbytes / t_h2d / 1e9, 2), "d2h_GBps": round(nbytes / t_d2h / 1e9, 2),
            "d2h_pageable_GBps": round(nbytes / t_d2h_pageable / 1e9, 2),
            "h2d_and_d2h_concurrent_GBps_per_dir": round(nbytes / t_both / 1e9, 2)}
-    for P, topo in ((2, "2"), (8, "8")):
+    for P in [int(x) for x in a.ranks.split(",")]:
+        topo = str(P)
         if n > (1 << 26) and P > 2:
             continue
         g = ftar.Comm.init_local(P)
@@ -73,7 +80,7 @@ for n in (1 << 20, 1 << 26, 1 << 28):
         t_e2e = timeit(e2e)
         row[f"P{P}_device_ms"] = round(t_dev * 1e3, 3)
         row[f"P{P}_host_e2e_ms"] = round(t_e2e * 1e3, 3)
-        for chunk in (1 << 30, 16 << 20, 4 << 20, 1 << 20):  # 1 GiB = one piece per block: serial
+        for chunk in [int(c) << 20 for c in a.chunks.split(",")]:
             g.set_host_chunk_bytes(chunk)
             t_h = timeit(lambda: g.allreduce(None, hs, n, "f32", topo_=topo, host=True))
             row[f"P{P}_host_pipelined_c{chunk >> 20}MiB_ms"] = round(t_h * 1e3, 3)
