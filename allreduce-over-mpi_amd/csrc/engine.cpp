@@ -49,14 +49,13 @@ namespace ftar {
 
 namespace {
 constexpr size_t kDefaultChunkBytes = 16u << 20;
-// Host mode pieces (0 = auto): about 8 pieces per block, 4..64 MiB.  Fewer,
-// larger pieces copy faster (a 4 MiB device->host copy runs at ~33 GB/s, a
-// 64 MiB one near the link's 57 GB/s); more pieces shorten the pipeline's fill
-// and drain (one piece of every block each).  Measured in profiles/r01/host/.
+// Host mode pieces (0 = auto): 16 MiB per block, at least split/64 (bounds the
+// number of copies for huge buckets).  4 MiB device->host copies run at only
+// ~33 GB/s; larger pieces lengthen the pipeline's fill and drain (one piece of
+// every block each).  16 MiB was the best or near-best size in every sweep
+// (profiles/r01/host/): 8 pieces per block at P = 8 x 1 GiB.
 constexpr size_t kDefaultHostChunkBytes = 0;
-size_t auto_host_chunk(size_t split_bytes) {
-  return std::min<size_t>(64u << 20, std::max<size_t>(4u << 20, split_bytes / 8));
-}
+size_t auto_host_chunk(size_t split_bytes) { return std::max<size_t>(16u << 20, split_bytes / 64); }
 
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
   while (c->events.size() < n) {

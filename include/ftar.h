@@ -203,8 +203,8 @@ ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t cou
 ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
                                         ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo,
                                         ftar_comm_t* comms, int nranks, void* const* streams);
-/* Host-mode piece size per block (bytes, rounded to 256 B); 0 = auto: about 8
- * pieces per block, 4..64 MiB (FTAR_HOST_CHUNK_BYTES at init). */
+/* Host-mode piece size per block (bytes, rounded to 256 B); 0 = auto: 16 MiB,
+ * at least 1/64 of a block (FTAR_HOST_CHUNK_BYTES at init). */
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes);
 ftar_status_t ftar_comm_get_host_chunk_bytes(ftar_comm_t comm, size_t* bytes);
 
