@@ -310,7 +310,15 @@ def bench_distributed(a):
         return alg, (alg * 2 * (world - 1) / world if world > 1 else alg)
 
     algbw, busbw = bws(ms)
-    links = max(1, 1 if best_topo.ring else min(XGMI_LINKS, world - 1))
+    # links one rank drives at once: every peer in the one-round (direct/collective) forms; in the reference's
+    # rounds, one neighbour (ring) or the widest stage's group (tree)
+    if best["form"] != "stages":
+        links = min(XGMI_LINKS, world - 1)
+    elif best_topo.ring:
+        links = 1
+    else:
+        links = min(XGMI_LINKS, max(best_topo.widths) - 1)
+    links = max(1, links)
     peak = links * XGMI_LINK_GBPS
     if rank == 0:
         res = {
