@@ -260,7 +260,10 @@ def bench_distributed(a):
         # data-movement form: one direct round each way (default), the reference's rounds, or a collective all-gather
         ags = ["direct", "stages"] + (["collective"] if (not t.ring and n % world == 0 and world > 1) else [])
         for ag in ags:
-            for chunk in sorted({4 << 20, 16 << 20, 64 << 20, default_chunk}):
+            chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
+            if key == str(default_topo) and ag == "direct":  # 256 KiB ... 64 MiB
+                chunks |= {256 << 10, 1 << 20}
+            for chunk in sorted(chunks):
                 if world > 1 and ag == "stages" and t.ring and chunk != default_chunk:
                     continue  # the reference's ring rounds: one point is enough
                 try:
