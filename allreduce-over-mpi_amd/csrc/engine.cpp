@@ -166,7 +166,8 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   if (host) chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
   if (host) {
     if (count * esz > c->staging_bytes) {
-      if (c->staging) {
+      if (c->staging) {  // earlier calls may still copy into or out of it
+        FTAR_CHECK_HIP(hipStreamSynchronize(c->h2d_s));
         FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
         FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
         FTAR_CHECK_HIP(hipStreamSynchronize(c->d2h_s));
