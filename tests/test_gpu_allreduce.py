@@ -278,3 +278,13 @@ def test_host_allreduce_then_device_allreduce_share_a_comm():
         assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P))
         outs = run_group(ins, "2,4", chunk_bytes=4096, ag="stages", rs="stages")
         assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P))
+
+
+def test_host_allreduce_growing_buckets():
+    """Staging and scratch regrow between host-mode calls on one communicator (earlier calls drained first)."""
+    P = 4
+    for n in (1000, 70_001, 300_007, 5_000):
+        ins = [fi.fill("f32", 44, r, n) for r in range(P)]
+        outs = run_group_host(ins, "2,2", host_chunk=65536, ag="stages", rs="stages")
+        ref = oracle_lib.allreduce(ins, "2,2")
+        assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P)), n
