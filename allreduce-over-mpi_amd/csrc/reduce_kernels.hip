@@ -23,6 +23,10 @@
 //       bool sum = OR of non-zero, bf16 (extension) = fp32 accumulate + one RNE.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <initializer_list>
+#include <type_traits>
+
 #include "ftar_internal.h"
 
 namespace ftar {
@@ -363,6 +367,40 @@ struct TreeCode {
   unsigned char c[FTAR_MAX_K];
 };
 
+// Code byte of leaf j of a nested fold with bottom-up widths w[0..L): bits 0-2
+// = levels completed after leaf j, bit 3+l = the value entering level l opens
+// a new node (level L's bit marks the root slot, written but never read).
+__host__ __device__ constexpr unsigned leaf_code(const int* w, int L, int j) {
+  int prod[kTreeLevels] = {};
+  int p = 1;
+  for (int l = 0; l < L; ++l) {
+    p *= w[l];
+    prod[l] = p;
+  }
+  unsigned done = 0;
+  while (done < (unsigned)L && (j + 1) % prod[done] == 0) ++done;
+  unsigned code = done;
+  if (j % w[0] == 0) code |= 1u << 3;
+  for (unsigned l = 1; l <= done && l < (unsigned)L; ++l)
+    if (((j + 1) / prod[l - 1] - 1) % w[l] == 0) code |= 1u << (3 + l);
+  if (done == (unsigned)L && L < kTreeLevels) code |= 1u << (3 + L);
+  return code;
+}
+
+// The common shapes at compile time: with the leaf codes constant after
+// unrolling, every select and level branch of tree_push folds away and the
+// nested fold is straight-line adds (and bf16 rounds).
+template <int... W>
+struct StaticShape {
+  static constexpr int L = sizeof...(W);
+  static constexpr int K = (W * ... * 1);
+  __device__ static constexpr unsigned code(int j) {
+    constexpr int w[L] = {W...};
+    return leaf_code(w, L, j);
+  }
+};
+struct RuntimeShape {};
+
 template <class Tr, bool VEC>
 struct TreeOps;
 template <class Tr>
@@ -406,7 +444,7 @@ __device__ __forceinline__ typename Tr::S tree_elem(const void* const* p, int k,
   return Tr::s_fin(v[0]);
 }
 
-template <class Tr, int K, int U>
+template <class Tr, int K, int U, class Sh = RuntimeShape>
 __global__ void __launch_bounds__(kThreads)
     reduce_tree_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, TreeCode tc, void* __restrict__ dst, size_t nvec,
                        int head, int tail) {
@@ -435,7 +473,8 @@ __global__ void __launch_bounds__(kThreads)
       for (int j = 0; j < K; ++j) {
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = Tr::v_init(x[j][u]);
-        tree_push<O, U>(acc, v, tc.c[j]);
+        if constexpr (std::is_same_v<Sh, RuntimeShape>) tree_push<O, U>(acc, v, tc.c[j]);
+        else tree_push<O, U>(acc, v, Sh::code(j));
       }
     } else {
       for (int j = 0; j < k; ++j) {
@@ -498,28 +537,17 @@ hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int 
 // leaves (see reduce_tree_kernel).
 bool make_tree_code(const int* shape, int nlevels, int k, TreeCode* tc) {
   if (nlevels < 1 || nlevels > kTreeLevels || k > FTAR_MAX_K) return false;
-  size_t W[kTreeLevels];
   size_t prod = 1;
   for (int l = 0; l < nlevels; ++l) {
     if (shape[l] < 1) return false;
     prod *= (size_t)shape[l];
-    W[l] = prod;
   }
   if (prod != (size_t)k) return false;
-  for (int j = 0; j < k; ++j) {
-    unsigned done = 0;
-    while (done < (unsigned)nlevels && (j + 1) % W[done] == 0) ++done;
-    unsigned code = done;
-    if (j % shape[0] == 0) code |= 1u << 3;
-    for (unsigned l = 1; l <= done && l < (unsigned)nlevels; ++l)
-      if (((j + 1) / W[l - 1] - 1) % (size_t)shape[l] == 0) code |= 1u << (3 + l);
-    if (done == (unsigned)nlevels && nlevels < kTreeLevels) code |= 1u << (3 + nlevels);  // root slot: write-only
-    tc->c[j] = (unsigned char)code;
-  }
+  for (int j = 0; j < k; ++j) tc->c[j] = (unsigned char)leaf_code(shape, nlevels, j);
   return true;
 }
 
-template <class Tr, int K, int U>
+template <class Tr, int K, int U, class Sh = RuntimeShape>
 hipError_t launch_tree_k(const void* const* srcs, int k, const TreeCode& tc, void* dst, size_t nvec, int head,
                          int tail, hipStream_t s) {
   constexpr int KK = K > 0 ? K : FTAR_MAX_K;
@@ -528,13 +556,14 @@ hipError_t launch_tree_k(const void* const* srcs, int k, const TreeCode& tc, voi
   size_t blocks = (nvec + (size_t)U * kThreads - 1) / ((size_t)U * kThreads);
   if (blocks == 0) blocks = 1;
   if (blocks > 0x7fffffffull) blocks = 0x7fffffffull;
-  hipLaunchKernelGGL((reduce_tree_kernel<Tr, K, U>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
+  hipLaunchKernelGGL((reduce_tree_kernel<Tr, K, U, Sh>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
                      nvec, head, tail);
   return hipGetLastError();
 }
 
 template <class Tr>
-hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, void* dst, size_t count, hipStream_t s) {
+hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const int* shape, int nlevels, void* dst,
+                       size_t count, hipStream_t s) {
   using S = typename Tr::S;
   constexpr size_t VE = 16 / sizeof(S);
   const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
@@ -553,7 +582,18 @@ hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, void*
   if (head > count) head = count;
   const size_t nvec = (count - head) / VE;
   const int tail = (int)(count - head - nvec * VE);
-  switch (k) {  // the P of the common multi-stage trees; 16 sources fit one vector per lane
+  auto is = [&](std::initializer_list<int> w) {
+    return (int)w.size() == nlevels && std::equal(w.begin(), w.end(), shape);
+  };
+  // the multi-stage trees of 4, 8 and 16 ranks: compile-time shapes
+  if (is({2, 2})) return launch_tree_k<Tr, 4, 2, StaticShape<2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  if (is({2, 4})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 4>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  if (is({4, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<4, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  if (is({2, 2, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  if (is({4, 4})) return launch_tree_k<Tr, 16, 1, StaticShape<4, 4>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  if (is({2, 2, 2, 2}))
+    return launch_tree_k<Tr, 16, 1, StaticShape<2, 2, 2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  switch (k) {  // other shapes: runtime leaf codes; 16 sources fit one vector per lane
     case 4: return launch_tree_k<Tr, 4, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
     case 6: return launch_tree_k<Tr, 6, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
     case 8: return launch_tree_k<Tr, 8, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
@@ -672,9 +712,9 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
     TreeCode tc;
     if (!shape || !make_tree_code(shape, nlevels, k, &tc)) return FTAR_ERR_INVALID_ARG;
     switch (dt) {
-      case FTAR_FLOAT32: e = launch_tree<F32Sum>(srcs, k, tc, dst, count, s); break;
-      case FTAR_FLOAT64: e = launch_tree<F64Sum>(srcs, k, tc, dst, count, s); break;
-      default: e = launch_tree<BF16Sum>(srcs, k, tc, dst, count, s); break;
+      case FTAR_FLOAT32: e = launch_tree<F32Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
+      case FTAR_FLOAT64: e = launch_tree<F64Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
+      default: e = launch_tree<BF16Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
     }
     FTAR_CHECK_HIP(e);
     return FTAR_SUCCESS;
