@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Per-launch HBM bytes of the bench kernel from rocprofv3 PMC passes -> profiles/pmc_summary.json.
+
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [--elements N] [--k K]
+
+FETCH_SIZE and WRITE_SIZE come from separate `rocprofv3 --pmc` passes (tools/gpu_run.sh pmc).  Per the
+gfx950 correction in MI355X_MICROARCH.md: read bytes = 2 x FETCH_SIZE x 1024, write bytes = WRITE_SIZE x 1024.
+"""
+import argparse
+import csv
+import json
+import os
+import statistics
+
+ap = argparse.ArgumentParser()
+ap.add_argument("fetch_csv")
+ap.add_argument("write_csv")
+ap.add_argument("--elements", type=int, default=1 << 26)
+ap.add_argument("--k", type=int, default=2)
+ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                              "profiles", "pmc_summary.json"))
+ap.add_argument("--source", default="")
+a = ap.parse_args()
+
+
+def values(path, counter):
+    with open(path) as f:
+        return [float(r["Counter_Value"]) for r in csv.DictReader(f)
+                if r["Counter_Name"] == counter and "reduce_vec_kernel" in r["Kernel_Name"]]
+
+
+fetch = statistics.median(values(a.fetch_csv, "FETCH_SIZE"))
+write = statistics.median(values(a.write_csv, "WRITE_SIZE"))
+rd, wr = 2 * fetch * 1024, write * 1024
+key = f"reduce_k{a.k}_f32_n{a.elements}"
+res = {key: {
+    "kernel": f"reduce_vec_kernel<F32Sum, {a.k}, 2, NTL=true, NTS=false, 256>",
+    "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write,
+    "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+    "algorithmic_bytes_per_launch": (a.k + 1) * a.elements * 4,
+    "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_run.sh pmc); "
+              "read bytes = 2 x FETCH_SIZE x 1024 per the gfx950 correction, write bytes = WRITE_SIZE x 1024",
+    "source": a.source or f"{a.fetch_csv}, {a.write_csv}"}}
+with open(a.out, "w") as f:
+    json.dump(res, f, indent=1)
+print(json.dumps(res[key]))
