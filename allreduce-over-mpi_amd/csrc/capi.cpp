@@ -311,3 +311,32 @@ long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count,
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// IPC primitives of the peer-direct transport, exported for tests (not part of
+// ftar.h): the 2-process test maps one process's buffer into another on the
+// same device and reduces through the mapping, as RcclTransport::map_peers does
+// across devices.
+// ---------------------------------------------------------------------------
+extern "C" ftar_status_t ftar_debug_ipc_handle(const void* base, void* handle64) {
+  if (!base || !handle64) return FTAR_ERR_INVALID_ARG;
+  hipIpcMemHandle_t h;
+  FTAR_CHECK_HIP(hipIpcGetMemHandle(&h, const_cast<void*>(base)));
+  static_assert(sizeof h == 64, "IPC handle size");
+  memcpy(handle64, &h, sizeof h);
+  return FTAR_SUCCESS;
+}
+
+extern "C" ftar_status_t ftar_debug_ipc_open(const void* handle64, void** ptr) {
+  if (!handle64 || !ptr) return FTAR_ERR_INVALID_ARG;
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle64, sizeof h);
+  FTAR_CHECK_HIP(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return FTAR_SUCCESS;
+}
+
+extern "C" ftar_status_t ftar_debug_ipc_close(void* ptr) {
+  if (!ptr) return FTAR_ERR_INVALID_ARG;
+  FTAR_CHECK_HIP(hipIpcCloseMemHandle(ptr));
+  return FTAR_SUCCESS;
+}

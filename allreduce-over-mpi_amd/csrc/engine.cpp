@@ -36,6 +36,10 @@ struct ftar_comm {
   size_t staging_bytes = 0;
   size_t chunk_bytes = 0;
   size_t host_chunk_bytes = 0;
+  bool peer_direct = false;        // FTAR_PEER_DIRECT / ftar_comm_set_peer_direct
+  void* xbuf = nullptr;            // peer-direct exchange buffer (IPC-exported), grow-only
+  size_t xbuf_bytes = 0;
+  std::vector<char*> xpeers;       // every rank's exchange buffer, mapped here
   bool auto_topo = true;
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
@@ -73,6 +77,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  if (const char* pd = getenv("FTAR_PEER_DIRECT")) c->peer_direct = atoi(pd) != 0;
   const char* hcb = getenv("FTAR_HOST_CHUNK_BYTES");
   c->host_chunk_bytes = hcb ? strtoull(hcb, nullptr, 0) : kDefaultHostChunkBytes;
   if (c->host_chunk_bytes && c->host_chunk_bytes < 256) c->host_chunk_bytes = 256;
@@ -98,12 +103,96 @@ void comm_teardown(ftar_comm* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) (void)hipStreamSynchronize(st);
+  if (c->tp) c->tp->unmap_peers(&c->xpeers, c->rank);
+  if (c->xbuf) (void)hipFree(c->xbuf);
   c->tp.reset();
   for (auto e : c->events) (void)hipEventDestroy(e);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->staging) (void)hipFree(c->staging);
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) (void)hipStreamDestroy(st);
+}
+
+// ---------------------------------------------------------------------------
+// Peer-direct execution of a one-round plan (ring or tree, direct forms):
+// instead of RCCL moving blocks into scratch and a fold reading scratch, every
+// rank's fold reads the other ranks' copies straight out of their exchange
+// buffers over xGMI (IPC-mapped), and the all-gather pulls every final block
+// the same way.  The plan's own fold (operand order, nested shape, bf16
+// rounding) is executed unchanged, so the bits are the plan's.
+//   in -> X (local copy) | barrier | fold into X[own block] | barrier |
+//   gather every owner's block from X_q -> recvbuf | barrier
+// The barriers are stream-ordered (Transport::barrier), nothing spins on the
+// device; the last one keeps X intact until every peer has read it.
+// ---------------------------------------------------------------------------
+bool peer_eligible(const Plan& plan) {
+  if (plan.stages.size() != 2 || plan.allgather != FTAR_AG_DIRECT || plan.nranks > FTAR_MAX_K) return false;
+  const Stage& rs = plan.stages[0];
+  const Stage& ag = plan.stages[1];
+  for (const Transfer& x : rs.recvs)
+    if (x.buf != BUF_SCRATCH) return false;
+  for (const ReduceItem& r : rs.reduces)
+    for (const Operand& o : r.srcs)
+      if (o.buf == BUF_DST) return false;
+  for (const Transfer& x : ag.recvs)
+    if (x.buf != BUF_DST) return false;
+  return ag.reduces.empty();
+}
+
+ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                             const Plan& plan, ftar_comm* c, hipStream_t stream) {
+  const size_t esz = dtype_size(dt), bytes = count * esz;
+  Transport* tp = c->tp.get();
+  if (bytes > c->xbuf_bytes) {  // collective: every rank sees the same counts, so all grow together
+    FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still reads the old X
+    FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
+    tp->unmap_peers(&c->xpeers, c->rank);
+    if (c->xbuf) FTAR_CHECK_HIP(hipFree(c->xbuf));
+    c->xbuf = nullptr;
+    c->xbuf_bytes = 0;
+    FTAR_CHECK_HIP(hipMalloc(&c->xbuf, bytes));
+    c->xbuf_bytes = bytes;
+    FTAR_RETURN_IF(tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers));
+  }
+  char* X = static_cast<char*>(c->xbuf);
+  const std::vector<char*>& Xq = c->xpeers;
+  hipEvent_t* ev = c->events.data();
+  FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
+  const void* in = sendbuf ? sendbuf : recvbuf;
+  FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
+  FTAR_RETURN_IF(tp->barrier(c->comm_s));
+  // reduce-scatter: scratch slot -> the rank that would have sent it
+  const Stage& rs = plan.stages[0];
+  std::map<size_t, int> slot_peer;
+  for (const Transfer& x : rs.recvs) slot_peer[x.off] = x.peer;
+  std::vector<const void*> srcs;
+  for (const ReduceItem& r : rs.reduces) {
+    srcs.clear();
+    for (const Operand& o : r.srcs) {
+      if (o.buf == BUF_SRC) {
+        srcs.push_back(X + o.off * esz);
+      } else {
+        auto it = slot_peer.find(o.off);
+        if (it == slot_peer.end()) return FTAR_ERR_INTERNAL;
+        srcs.push_back(Xq[it->second] + r.off * esz);  // that rank's copy of this block
+      }
+    }
+    FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), X + r.off * esz, r.len, dt, op, c->comm_s,
+                                 r.round_each, r.shape.data(), (int)r.shape.size()));
+  }
+  FTAR_RETURN_IF(tp->barrier(c->comm_s));
+  // all-gather: every owner's final block from its exchange buffer, one launch
+  std::vector<Segment> segs;
+  for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, static_cast<char*>(recvbuf) + r.off * esz,
+                                                         r.len * esz});
+  for (const Transfer& x : plan.stages[1].recvs)
+    segs.push_back({Xq[x.peer] + x.off * esz, static_cast<char*>(recvbuf) + x.off * esz, x.len * esz});
+  FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+  FTAR_RETURN_IF(tp->barrier(c->comm_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
+  FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
+  return FTAR_SUCCESS;
 }
 
 // Host mode: sendbuf/recvbuf of the call are host memory (pinned for overlap).
@@ -155,6 +244,10 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   const Plan& plan = *it->second;
   if (plan.max_k > FTAR_MAX_K) return FTAR_ERR_UNSUPPORTED;
   const size_t nst = plan.stages.size();
+  if (!host && c->peer_direct && peer_eligible(plan)) {
+    FTAR_RETURN_IF(grow_events(c, 5));
+    return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
+  }
 
   // Host mode: the buffers are in host memory and move through a device
   // staging buffer, piece by piece, so H2D (PCIe in), the exchange, and D2H
@@ -498,6 +591,19 @@ ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t cou
   const ftar::HostIO io{static_cast<const char*>(sendbuf ? sendbuf : recvbuf), static_cast<char*>(recvbuf)};
   return ftar::allreduce(sendbuf, recvbuf ? recvbuf : io.dst, count, dtype, op, topo, comm,
                          static_cast<hipStream_t>(stream), &io);
+}
+
+ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int enable) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->peer_direct = enable != 0;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* enable) {
+  if (!comm || !enable) return FTAR_ERR_INVALID_ARG;
+  *enable = comm->peer_direct ? 1 : 0;
+  return FTAR_SUCCESS;
 }
 
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {

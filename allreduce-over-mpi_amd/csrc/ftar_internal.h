@@ -110,6 +110,14 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
                             hipStream_t stream, bool round_each = false, const int* shape = nullptr,
                             int nlevels = 0);
 bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op);
+// dst_i[0..bytes_i) = src_i[0..bytes_i) for up to FTAR_MAX_K segments in one
+// launch (the peer-direct all-gather: each segment pulls one rank's block).
+struct Segment {
+  const void* src;
+  void* dst;
+  size_t bytes;
+};
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream);
 size_t dtype_size(ftar_dtype_t dt);
 
 // ---------------------------------------------------------------------------
@@ -133,6 +141,14 @@ class Transport {
       if (p != rank) FTAR_RETURN_IF(this->recv(static_cast<char*>(recv) + (size_t)p * bytes, bytes, p, s));
     return group_end();
   }
+  // Peer-direct mode (engine.cpp peer_allreduce).  barrier: stream-ordered,
+  // work after it on `s` starts once every rank's stream reached it.
+  // map_peers: collective and host-blocking; every rank passes the base of a
+  // hipMalloc allocation and gets every rank's base as a pointer usable by
+  // kernels on its own device (peers[rank] == mine).  unmap_peers undoes it.
+  virtual ftar_status_t barrier(hipStream_t s) = 0;
+  virtual ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) = 0;
+  virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {

@@ -509,6 +509,47 @@ __global__ void __launch_bounds__(kThreads)
 }
 
 // ---------------------------------------------------------------------------
+// multi-segment copy: the peer-direct all-gather pulls every rank's final block
+// (over xGMI) into the caller's buffer in ONE launch, grid.y = segment, so all
+// links stream at once.  16 B per lane per access when source and destination
+// share their address mod 16 (always, in the all-gather: both sit at the same
+// block offset of 256-B aligned buffers); bytes otherwise.
+// ---------------------------------------------------------------------------
+struct SegArgs {
+  const char* src[FTAR_MAX_K];
+  char* dst[FTAR_MAX_K];
+  size_t bytes[FTAR_MAX_K];
+};
+
+__global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a) {
+  const int sgi = blockIdx.y;
+  const char* src = a.src[sgi];
+  char* dst = a.dst[sgi];
+  const size_t n = a.bytes[sgi];
+  const size_t tid = (size_t)blockIdx.x * kThreads + threadIdx.x, nthr = (size_t)gridDim.x * kThreads;
+  const uintptr_t ms = reinterpret_cast<uintptr_t>(src) & 15, md = reinterpret_cast<uintptr_t>(dst) & 15;
+  if (ms != md) {
+    for (size_t i = tid; i < n; i += nthr) dst[i] = src[i];
+    return;
+  }
+  size_t head = ms ? 16 - ms : 0;
+  if (head > n) head = n;
+  const size_t nvec = (n - head) / 16, tail_at = head + nvec * 16;
+  if (tid < head) dst[tid] = src[tid];
+  if (tid < n - tail_at) dst[tail_at + tid] = src[tail_at + tid];
+  const u32x4* s4 = reinterpret_cast<const u32x4*>(src + head);
+  u32x4* d4 = reinterpret_cast<u32x4*>(dst + head);
+  size_t v = (size_t)blockIdx.x * (2 * kThreads) + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * (2 * kThreads);
+  for (; v + kThreads < nvec; v += stride) {
+    const u32x4 x0 = s4[v], x1 = s4[v + kThreads];
+    d4[v] = x0;
+    d4[v + kThreads] = x1;
+  }
+  if (v < nvec) d4[v] = s4[v];
+}
+
+// ---------------------------------------------------------------------------
 // host-side launch
 // ---------------------------------------------------------------------------
 
@@ -694,6 +735,27 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
     return dt == FTAR_UINT8 || dt == FTAR_INT8 || dt == FTAR_UINT16 || dt == FTAR_INT16 || dt == FTAR_INT32 ||
            dt == FTAR_INT64;
   return false;
+}
+
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream) {
+  if (nsegs < 0 || nsegs > FTAR_MAX_K) return FTAR_ERR_INVALID_ARG;
+  SegArgs a{};
+  int m = 0;
+  size_t most = 0;
+  for (int i = 0; i < nsegs; ++i) {
+    if (!segs[i].bytes) continue;
+    a.src[m] = static_cast<const char*>(segs[i].src);
+    a.dst[m] = static_cast<char*>(segs[i].dst);
+    a.bytes[m] = segs[i].bytes;
+    most = std::max(most, segs[i].bytes);
+    ++m;
+  }
+  if (!m) return FTAR_SUCCESS;
+  size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
+  bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)bx, (unsigned)m), dim3(kThreads), 0, stream, a);
+  FTAR_CHECK_HIP(hipGetLastError());
+  return FTAR_SUCCESS;
 }
 
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,

@@ -48,6 +48,57 @@ class RcclTransport final : public Transport {
   explicit RcclTransport(ncclComm_t c) : comm_(c) {}
   ~RcclTransport() override {
     if (comm_) ncclCommDestroy(comm_);
+    if (scratch_) (void)hipFree(scratch_);
+  }
+  // a 4-byte all-reduce: complete on any rank's stream only once every rank's
+  // stream has reached it
+  ftar_status_t barrier(hipStream_t s) override {
+    FTAR_RETURN_IF(ensure_scratch());
+    FTAR_CHECK_NCCL(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, s));
+    return FTAR_SUCCESS;
+  }
+  // IPC handles of every rank's allocation, all-gathered over RCCL, opened here
+  // (dmabuf IPC; peer access enabled lazily by the runtime)
+  ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    FTAR_RETURN_IF(ensure_scratch());
+    hipIpcMemHandle_t h;
+    FTAR_CHECK_HIP(hipIpcGetMemHandle(&h, mine));
+    std::vector<hipIpcMemHandle_t> all(nranks);
+    char* dev = static_cast<char*>(scratch_) + 256;  // nranks handles after the barrier word
+    hipStream_t s;
+    FTAR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    ftar_status_t st = FTAR_SUCCESS;
+    if (hipMemcpyAsync(dev + (size_t)rank * sizeof h, &h, sizeof h, hipMemcpyHostToDevice, s) != hipSuccess ||
+        ncclAllGather(dev + (size_t)rank * sizeof h, dev, sizeof h, ncclUint8, comm_, s) != ncclSuccess ||
+        hipMemcpyAsync(all.data(), dev, (size_t)nranks * sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+      set_error("peer map: handle exchange failed", __FILE__, __LINE__);
+      st = FTAR_ERR_RCCL;
+    }
+    (void)hipStreamDestroy(s);
+    FTAR_RETURN_IF(st);
+    peers->assign(nranks, nullptr);
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) {
+        (*peers)[q] = static_cast<char*>(mine);
+        continue;
+      }
+      void* p = nullptr;
+      hipError_t e = hipIpcOpenMemHandle(&p, all[q], hipIpcMemLazyEnablePeerAccess);
+      if (e != hipSuccess) {
+        unmap_peers(peers, rank);
+        set_error(std::string("hipIpcOpenMemHandle(rank ") + std::to_string(q) + "): " + hipGetErrorString(e),
+                  __FILE__, __LINE__);
+        return FTAR_ERR_HIP;
+      }
+      (*peers)[q] = static_cast<char*>(p);
+    }
+    return FTAR_SUCCESS;
+  }
+  void unmap_peers(std::vector<char*>* peers, int rank) override {
+    for (int q = 0; q < (int)peers->size(); ++q)
+      if (q != rank && (*peers)[q]) (void)hipIpcCloseMemHandle((*peers)[q]);
+    peers->clear();
   }
   ftar_status_t group_start() override {
     FTAR_CHECK_NCCL(ncclGroupStart());
@@ -91,7 +142,12 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  ftar_status_t ensure_scratch() {  // barrier word + FTAR_MAX_K IPC handles
+    if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)FTAR_MAX_K * sizeof(hipIpcMemHandle_t)));
+    return FTAR_SUCCESS;
+  }
   ncclComm_t comm_;
+  void* scratch_ = nullptr;
 };
 
 }  // namespace
@@ -126,11 +182,45 @@ struct LocalHub {
       if (done) (void)hipEventDestroy(done);
     }
   };
-  explicit LocalHub(int n) : nranks(n) {}
+  // every rank's value of one rendezvous (barriers, peer pointers)
+  struct Round {
+    std::vector<const void*> ptr;
+    std::vector<std::shared_ptr<hipEvent_t>> ev;
+  };
+  explicit LocalHub(int n) : nranks(n), pending(std::make_shared<Round>()) {
+    pending->ptr.resize(n);
+    pending->ev.resize(n);
+  }
+  // Host-side all-gather of one (pointer, event) per rank.  A generation
+  // completes only when every rank arrived, so the finished Round cannot be
+  // replaced before each of its ranks has taken it.
+  ftar_status_t rendezvous(int rank, const void* p, std::shared_ptr<hipEvent_t> e, std::shared_ptr<Round>* out) {
+    std::unique_lock<std::mutex> g(mu);
+    const long my_gen = gen;
+    pending->ptr[rank] = p;
+    pending->ev[rank] = std::move(e);
+    if (++arrived == nranks) {
+      done = pending;
+      pending = std::make_shared<Round>();
+      pending->ptr.resize(nranks);
+      pending->ev.resize(nranks);
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else if (!cv.wait_for(g, std::chrono::seconds(120), [&] { return gen != my_gen; })) {
+      set_error("local transport: rendezvous timed out", __FILE__, __LINE__);
+      return FTAR_ERR_TIMEOUT;
+    }
+    *out = done;
+    return FTAR_SUCCESS;
+  }
   int nranks;
   std::mutex mu;
   std::condition_variable cv;
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Posted>>> wire;  // (from, to)
+  std::shared_ptr<Round> pending, done;
+  int arrived = 0;
+  long gen = 0;
 };
 
 std::shared_ptr<LocalHub> make_local_hub(int nranks) { return std::make_shared<LocalHub>(nranks); }
@@ -166,6 +256,29 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "local"; }
+  // each rank's stream waits for every other rank's event recorded at the barrier
+  ftar_status_t barrier(hipStream_t s) override {
+    auto e = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [](hipEvent_t* p) {
+      if (*p) (void)hipEventDestroy(*p);
+      delete p;
+    });
+    FTAR_RETURN_IF(event(e.get()));
+    FTAR_CHECK_HIP(hipEventRecord(*e, s));
+    std::shared_ptr<LocalHub::Round> r;
+    FTAR_RETURN_IF(hub_->rendezvous(rank_, nullptr, e, &r));
+    for (int q = 0; q < hub_->nranks; ++q)
+      if (q != rank_) FTAR_CHECK_HIP(hipStreamWaitEvent(s, *r->ev[q], 0));
+    return FTAR_SUCCESS;
+  }
+  // one address space: the peers' allocations are usable as they are
+  ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    (void)rank;
+    std::shared_ptr<LocalHub::Round> r;
+    FTAR_RETURN_IF(hub_->rendezvous(rank_, mine, nullptr, &r));
+    peers->assign(nranks, nullptr);
+    for (int q = 0; q < nranks; ++q) (*peers)[q] = static_cast<char*>(const_cast<void*>(r->ptr[q]));
+    return FTAR_SUCCESS;
+  }
 
  private:
   static ftar_status_t event(hipEvent_t* e) {

@@ -108,6 +108,8 @@ _lib.ftar_allreduce_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), 
 _lib.ftar_allreduce_host.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(Topo), _vp, _vp]
 _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int,
                                            ctypes.POINTER(Topo), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
+_lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
+_lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_comm_set_host_chunk_bytes.argtypes = [_vp, _sz]
 _lib.ftar_comm_get_host_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
@@ -326,6 +328,17 @@ class Comm:
         _check(st, "ftar_allreduce_host")
 
     @property
+    def peer_direct(self):
+        """Peer-direct data movement (IPC-mapped exchange buffers, no RCCL data path) for one-round plans."""
+        v = _int()
+        _check(_lib.ftar_comm_get_peer_direct(self.handle, ctypes.byref(v)), "peer_direct")
+        return bool(v.value)
+
+    @peer_direct.setter
+    def peer_direct(self, on):
+        _check(_lib.ftar_comm_set_peer_direct(self.handle, 1 if on else 0), "peer_direct")
+
+    @property
     def host_chunk_bytes(self):
         v = _sz()
         _check(_lib.ftar_comm_get_host_chunk_bytes(self.handle, ctypes.byref(v)), "host_chunk_bytes")
@@ -409,6 +422,10 @@ class LocalGroup:
     def set_host_chunk_bytes(self, b):
         for c in self.comms:
             c.host_chunk_bytes = b
+
+    def set_peer_direct(self, on):
+        for c in self.comms:
+            c.peer_direct = on
 
     def set_reduce_scatter(self, mode):
         for c in self.comms:

@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--chunk-bytes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct form out of the sweep")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     return ap.parse_args()
@@ -233,12 +234,33 @@ def bench_distributed(a):
         return t.item() / max(1, steps) * 1e3
 
     def run_with(topo, chunk, form="direct"):
-        """form: "direct" (one-round reduce-scatter for the ring, one-round all-gather),
-        "stages" (the reference's rounds both ways) or "collective" (ncclAllGather)."""
+        """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
+        rounds both ways), "collective" (ncclAllGather) or "peer" (one-round plan, IPC-mapped peer reads)."""
         comm.chunk_bytes = chunk
-        comm.allgather = form
+        comm.peer_direct = form == "peer"
+        comm.allgather = "direct" if form == "peer" else form
         comm.reduce_scatter = "stages" if form == "stages" else "direct"
         return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
+
+    # correctness of y: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
+    idx = torch.linspace(0, n - 1, 4096, device=dev).long()
+    xs = x[idx].float().cpu()
+    allx = [torch.empty_like(xs) for _ in range(world)]
+    dist.all_gather(allx, xs)
+    ref64 = sum(t.double() for t in allx)
+    absum = sum(t.double().abs() for t in allx)
+    eps = 2.0 ** -24 if a.dtype == "f32" else 2.0 ** -8
+    tol = (world - 1) * eps * absum + 1e-30
+
+    def check_y():
+        torch.cuda.synchronize()
+        mine = y[idx].float().cpu()
+        ally = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(ally, mine)
+        ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item())
 
     # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
     if a.topo:
@@ -259,21 +281,27 @@ def bench_distributed(a):
         seen.add(key)
         # data-movement form: one direct round each way (default), the reference's rounds, or a collective all-gather
         ags = ["direct", "stages"] + (["collective"] if (not t.ring and n % world == 0 and world > 1) else [])
+        if world > 1 and not a.no_peer and t.lonely == 0:
+            ags.append("peer")
         for ag in ags:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
             if key == str(default_topo) and ag == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
+            if ag == "peer":
+                chunks = {default_chunk}  # no pieces: one fold and one gather kernel per call
             for chunk in sorted(chunks):
                 if world > 1 and ag == "stages" and t.ring and chunk != default_chunk:
                     continue  # the reference's ring rounds: one point is enough
                 try:
                     ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
+                    ok_ = check_y()   # every configuration's own output, before it may be chosen
                 except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
                     sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "error": str(e)[:200]})
                     continue
                 sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "ms": round(ms_, 4),
-                              "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2)})
-    ok_runs = [r for r in sweep if "ms" in r]
+                              "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2),
+                              "check": "ok" if ok_ else "MISMATCH"})
+    ok_runs = [r for r in sweep if "ms" in r and r.get("check") == "ok"]
     best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else {
         "topology": str(default_topo), "chunk_bytes": default_chunk, "form": "direct"}
     best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
@@ -294,19 +322,7 @@ def bench_distributed(a):
         ms_rccl = None
         sys.stderr.write(f"rccl yardstick failed: {e}\n")
 
-    # correctness: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
-    idx = torch.linspace(0, n - 1, 4096, device=dev).long()
-    mine = y[idx].float().cpu()
-    xs = x[idx].float().cpu()
-    allx = [torch.empty_like(xs) for _ in range(world)]
-    ally = [torch.empty_like(mine) for _ in range(world)]
-    dist.all_gather(allx, xs)
-    dist.all_gather(ally, mine)
-    ref64 = sum(t.double() for t in allx)
-    absum = sum(t.double().abs() for t in allx)
-    eps = 2.0 ** -24 if a.dtype == "f32" else 2.0 ** -8
-    tol = (world - 1) * eps * absum + 1e-30
-    ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
+    ok = check_y()   # the headline configuration's output (run just above)
 
     def bws(m):
         alg = bucket / (m * 1e-3) / 1e9
@@ -329,7 +345,9 @@ def bench_distributed(a):
             "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
-            "config": {"workload": f"{world}xMI355X FlexTree AllReduce over RCCL p2p/xGMI (BASELINE configs[2-3])",
+            "config": {"workload": f"{world}xMI355X FlexTree AllReduce over xGMI, "
+                                   f"{'IPC-mapped peer reads' if best['form'] == 'peer' else 'RCCL p2p'} "
+                                   "(BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
                        "chunk_bytes": best["chunk_bytes"], "form": best["form"],
                        "selection": "best of sweep (FT_TOPO x chunk x data-movement form)",

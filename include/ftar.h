@@ -176,6 +176,16 @@ typedef enum { FTAR_RS_STAGES = 0, FTAR_RS_DIRECT = 1 } ftar_reduce_scatter_t;
 ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t mode);
 ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode);
 
+/* Peer-direct data movement (extension; default off, FTAR_PEER_DIRECT=1 at
+ * init).  For one-round plans (the ring, and trees without lonely ranks, under
+ * FTAR_RS_DIRECT-or-single-stage + FTAR_AG_DIRECT), each rank's fold reads the
+ * other ranks' copies of its block straight from their IPC-mapped exchange
+ * buffers over xGMI, and the all-gather pulls every final block the same way:
+ * no RCCL data movement, no scratch pass, three stream-ordered barriers.  The
+ * plan's fold is executed unchanged: same bits.  Other plans keep RCCL p2p. */
+ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int enable);
+ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* enable);
+
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
  * communicator's topology (FT_TOPO/FT_LONELY from the environment at init,

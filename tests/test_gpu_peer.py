@@ -1,0 +1,166 @@
+"""Peer-direct data movement (ftar_comm_set_peer_direct): the plan's fold reads the other ranks'
+exchange buffers directly, the all-gather pulls every final block; barriers are stream-ordered.
+
+* in-process groups on cuda:0 (local transport: the peers' buffers are plain pointers): every golden
+  case, the one-round ring and trees, ragged and larger buckets, all bit-exact vs the oracle; plans
+  that are not one-round (lonely ranks, staged forms) fall back to the RCCL-style executor;
+* the IPC primitive itself across two processes on one device (dmabuf IPC, what RcclTransport
+  uses to map peers on other GPUs): process B reduces through a mapping of process A's buffer.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import ftar_inputs as fi
+import golden_cases as gc
+import oracle_lib
+from gpu_util import filled_dev, from_dev, to_dev
+
+pytestmark = pytest.mark.gpu
+
+_groups = {}
+
+
+def group(P):
+    import ftar
+    if P not in _groups:
+        _groups[P] = ftar.Comm.init_local(P)
+    return _groups[P]
+
+
+def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", rs="direct", repeat=1):
+    g = group(len(ins))
+    g.set_peer_direct(True)
+    g.set_allgather(ag)
+    g.set_reduce_scatter(rs)
+    try:
+        n = ins[0].size
+        send = [to_dev(x) for x in ins]
+        recv = [filled_dev(x.nbytes) for x in ins] if outofplace else send
+        for it in range(repeat):
+            sb = [p for _, p in send] if outofplace else None
+            g.allreduce(sb, [p for _, p in recv], n, dtype, op, topo_=topo, lonely=lonely)
+            if outofplace and it + 1 < repeat:
+                send, recv = recv, send
+        return [from_dev(t, ins[0].dtype, n) for t, _ in recv]
+    finally:
+        g.set_peer_direct(False)
+
+
+@pytest.mark.parametrize("case", gc.allreduce_cases(max_n=70000), ids=lambda c: c["id"])
+def test_peer_direct_matches_reference_golden(case):
+    ins = gc.case_inputs(case)
+    outs = run_peer(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                    repeat=case["repeat"])
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i16"])
+@pytest.mark.parametrize("P,topo", [(2, "1"), (8, "1"), (5, "1"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3"),
+                                    (16, "4,4"), (16, "2,2,2,2")])
+def test_peer_direct_one_round_plans(P, topo, dt):
+    n = 40_009 * P + 3       # ragged blocks, unaligned block offsets
+    ins = [fi.fill(dt, 9, r, n) for r in range(P)]
+    outs = run_peer(ins, topo, dtype=fi.BY_NAME[dt])
+    ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes(), r
+
+
+@pytest.mark.parametrize("P,topo,lonely,form", [(5, "2,2", 1, "direct"), (8, "2,4", 0, "stages"),
+                                                (8, "1", 0, "stages")])
+def test_peer_direct_falls_back_for_multi_round_plans(P, topo, lonely, form):
+    n = 30_001
+    ins = [fi.fill("f32", 10, r, n) for r in range(P)]
+    outs = run_peer(ins, topo, lonely, ag=form, rs=form)
+    ref = oracle_lib.allreduce(ins, topo, lonely)
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes(), r
+
+
+def test_peer_direct_growing_buckets_and_mode_switches():
+    """Exchange buffers regrow (unmap, free, remap) and calls alternate with the p2p executor."""
+    import ftar
+    P = 4
+    g = group(P)
+    for n in (1000, 200_003, 7, 600_001):
+        ins = [fi.fill("f32", 11, r, n) for r in range(P)]
+        ref = oracle_lib.allreduce(ins, "2,2")
+        outs = run_peer(ins, "2,2")
+        assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P)), n
+        g.set_chunk_bytes(4096)
+        bufs = [to_dev(x) for x in ins]
+        g.allreduce(None, [p for _, p in bufs], n, "f32", topo_="2,2")
+        assert all(from_dev(t, np.float32, n).tobytes() == ref[r].tobytes() for r, (t, _) in enumerate(bufs)), n
+    assert not g[0].peer_direct and isinstance(ftar.Comm.peer_direct, property)
+
+
+# ---- the IPC primitive across processes ---------------------------------------------------------
+def _ipc_owner(n, q_handle, q_done):
+    import sys, os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    import ftar  # noqa: F401  (loads the HIP runtime torch uses)
+    import ftar_inputs as fi
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    lib = ftar.lib()
+    p = ctypes.c_void_p()
+    assert hip.hipSetDevice(0) == 0
+    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n * 4)) == 0
+    x = fi.fill("f32", 12, 0, n)
+    assert hip.hipMemcpy(p, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n * 4), 1) == 0   # H2D
+    h = ctypes.create_string_buffer(64)
+    lib.ftar_debug_ipc_handle.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert lib.ftar_debug_ipc_handle(p, h) == 0
+    q_handle.put(h.raw)
+    ok = q_done.get(timeout=240)
+    assert hip.hipFree(p) == 0
+    q_handle.put(("owner", ok))
+
+
+def _ipc_user(n, q_handle, q_done, q_res):
+    import sys, os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    import ftar
+    import ftar_inputs as fi
+    import torch
+    try:
+        raw = q_handle.get(timeout=240)
+        lib = ftar.lib()
+        lib.ftar_debug_ipc_open.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
+        lib.ftar_debug_ipc_close.argtypes = [ctypes.c_void_p]
+        h = ctypes.create_string_buffer(raw, 64)
+        mapped = ctypes.c_void_p()
+        assert lib.ftar_debug_ipc_open(h, ctypes.byref(mapped)) == 0
+        mine = fi.fill("f32", 12, 1, n)
+        t = torch.from_numpy(mine).cuda()
+        out = torch.empty_like(t)
+        ftar.reduce([mapped.value, t.data_ptr()], out.data_ptr(), n, "f32", "sum")
+        torch.cuda.synchronize()
+        exp = (fi.fill("f32", 12, 0, n) + mine).astype(np.float32)
+        ok = out.cpu().numpy().tobytes() == exp.tobytes()
+        assert lib.ftar_debug_ipc_close(mapped) == 0
+        q_res.put(("user", ok))
+    except Exception as e:  # report, don't hang the parent
+        q_res.put(("user", repr(e)))
+    finally:
+        q_done.put(True)
+
+
+def test_ipc_mapping_across_processes():
+    ctx = mp.get_context("spawn")
+    qh, qd, qr = ctx.Queue(), ctx.Queue(), ctx.Queue()
+    n = (1 << 20) + 7
+    a = ctx.Process(target=_ipc_owner, args=(n, qh, qd))
+    b = ctx.Process(target=_ipc_user, args=(n, qh, qd, qr))
+    a.start()
+    b.start()
+    res = qr.get(timeout=300)
+    b.join(timeout=120)
+    a.join(timeout=120)
+    assert res == ("user", True), res
+    assert a.exitcode == 0 and b.exitcode == 0
