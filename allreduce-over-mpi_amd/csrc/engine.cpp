@@ -593,6 +593,26 @@ ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t cou
                          static_cast<hipStream_t>(stream), &io);
 }
 
+// Test hook (not in ftar.h): the transport's peer plumbing on a real
+// communicator -- map a fresh allocation (IPC handle exchange), barrier on the
+// comm stream, unmap.  On a 1-rank RCCL communicator this runs every RCCL and
+// IPC call of the peer path except opening another rank's handle.
+ftar_status_t ftar_debug_peer_selftest(ftar_comm_t comm) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  void* buf = nullptr;
+  FTAR_CHECK_HIP(hipMalloc(&buf, 1 << 20));
+  std::vector<char*> peers;
+  ftar_status_t st = comm->tp->map_peers(buf, comm->rank, comm->nranks, &peers);
+  if (st == FTAR_SUCCESS && (peers.size() != (size_t)comm->nranks || peers[comm->rank] != buf)) st = FTAR_ERR_INTERNAL;
+  if (st == FTAR_SUCCESS) st = comm->tp->barrier(comm->comm_s);
+  if (st == FTAR_SUCCESS && hipStreamSynchronize(comm->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
+  comm->tp->unmap_peers(&peers, comm->rank);
+  (void)hipFree(buf);
+  return st;
+}
+
 ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int enable) {
   if (!comm) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);

@@ -164,3 +164,18 @@ def test_ipc_mapping_across_processes():
     a.join(timeout=120)
     assert res == ("user", True), res
     assert a.exitcode == 0 and b.exitcode == 0
+
+
+def test_rccl_peer_plumbing_single_rank():
+    """RcclTransport's barrier (4-byte ncclAllReduce) and map_peers (IPC handle all-gather over RCCL) on a
+    1-rank RCCL communicator: every call of the multi-GPU peer path except opening another rank's handle."""
+    import ftar
+    comm = ftar.Comm.init_rank(1, ftar.get_unique_id(), 0, 0)
+    try:
+        lib = ftar.lib()
+        lib.ftar_debug_peer_selftest.argtypes = [ctypes.c_void_p]
+        assert lib.ftar_debug_peer_selftest(comm.handle) == 0, lib.ftar_last_error()
+        comm.peer_direct = True
+        assert comm.peer_direct
+    finally:
+        comm.destroy()
