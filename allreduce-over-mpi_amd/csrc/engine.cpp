@@ -19,6 +19,7 @@
 // is stream-ordered like any other HIP operation.
 #include <algorithm>
 #include <cstdlib>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -201,6 +202,117 @@ struct HostIO {
   char* dst;
 };
 
+namespace {
+
+// The call's topology (argument, FT_TOPO at init, or the cost model) and its
+// cached plan; check_world once per (topology, count, form).
+ftar_status_t resolve_plan(ftar_comm* c, const ftar_topo_t* topo, size_t count, size_t esz, const Form& form,
+                           const Plan** out) {
+  Topology t;
+  if (topo) {
+    FTAR_RETURN_IF(to_topology(topo, c->nranks, &t));
+  } else if (!c->auto_topo) {
+    t = c->topo;
+  } else {
+    ftar_topo_t ch;
+    FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
+    FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
+  }
+  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(form.allgather) + "/rs" +
+                          std::to_string(form.reduce_scatter);
+  auto it = c->plans.find(key);
+  if (it == c->plans.end()) {
+    auto p = std::make_shared<Plan>();
+    FTAR_RETURN_IF(check_world(t, c->nranks, count, form));
+    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), form));
+    if (c->plans.size() > 64) c->plans.clear();
+    it = c->plans.emplace(key, p).first;
+  }
+  if (it->second->max_k > FTAR_MAX_K) return FTAR_ERR_UNSUPPORTED;
+  *out = it->second.get();
+  return FTAR_SUCCESS;
+}
+
+// Grow-only device buffer; before freeing the old one, drain the streams whose
+// earlier work may still touch it.
+ftar_status_t ensure_buffer(void** buf, size_t* have, size_t need, std::initializer_list<hipStream_t> users) {
+  if (need <= *have) return FTAR_SUCCESS;
+  if (*buf) {
+    for (hipStream_t st : users) FTAR_CHECK_HIP(hipStreamSynchronize(st));
+    FTAR_CHECK_HIP(hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+  }
+  FTAR_CHECK_HIP(hipMalloc(buf, need));
+  *have = need;
+  return FTAR_SUCCESS;
+}
+
+// Per-stage dependency facts of a plan: does it move / reduce / receive into
+// scratch, the latest reducing stage before it (its data), and in the
+// stage-major order the last reader of the scratch half it receives into.
+struct StageFacts {
+  std::vector<char> moves, reduces, to_scratch;
+  std::vector<long> prev_red, war;
+  explicit StageFacts(const Plan& plan) {
+    const size_t nst = plan.stages.size();
+    moves.assign(nst, 0);
+    reduces.assign(nst, 0);
+    to_scratch.assign(nst, 0);
+    prev_red.assign(nst, -1);
+    war.assign(nst, -1);
+    long last = -1, owner[2] = {-1, -1};
+    for (size_t s = 0; s < nst; ++s) {
+      const Stage& st = plan.stages[s];
+      moves[s] = !st.sends.empty() || !st.recvs.empty();
+      reduces[s] = !st.reduces.empty();
+      for (const Transfer& x : st.recvs) to_scratch[s] |= x.buf == BUF_SCRATCH;
+      prev_red[s] = last;
+      war[s] = to_scratch[s] ? owner[s % 2] : -1;
+      if (reduces[s]) {
+        last = (long)s;
+        if (to_scratch[s]) owner[s % 2] = (long)s;
+      }
+    }
+  }
+};
+
+// Skewed execution gives every stage its own scratch region: delta[s] moves a
+// stage's scratch offsets from its alternating half to that region.  Returns
+// the scratch elements needed.
+size_t per_stage_scratch(const Plan& plan, std::vector<long>* delta) {
+  const size_t nst = plan.stages.size();
+  delta->assign(nst, 0);
+  size_t base = 0;
+  for (size_t s = 0; s < nst; ++s) {
+    const size_t half_base = (s % 2) * plan.scratch_half;
+    size_t used = 0;
+    for (const Transfer& x : plan.stages[s].recvs)
+      if (x.buf == BUF_SCRATCH) used = std::max(used, x.off - half_base + x.len);
+    (*delta)[s] = (long)base - (long)half_base;
+    base += used;
+  }
+  return base;
+}
+
+// Order of the (stage, piece) steps, identical on every rank.  Stage-major, or
+// skewed: stage s+1 trails stage s by one piece.
+std::vector<std::pair<size_t, size_t>> step_order(size_t nst, size_t nchunks, bool skew) {
+  std::vector<std::pair<size_t, size_t>> order;
+  order.reserve(nst * nchunks);
+  if (!skew) {
+    for (size_t s = 0; s < nst; ++s)
+      for (size_t k = 0; k < nchunks; ++k) order.emplace_back(s, k);
+  } else {
+    for (size_t tt = 0; tt < nchunks + nst - 1; ++tt)
+      for (size_t s = 0; s < nst && s <= tt; ++s)
+        if (tt - s < nchunks) order.emplace_back(s, tt - s);
+  }
+  return order;
+}
+
+}  // namespace
+
 ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                         const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr) {
   if (!c || !recvbuf) return FTAR_ERR_INVALID_ARG;
@@ -217,32 +329,13 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   }
   if (count == 0) return FTAR_SUCCESS;
 
-  Topology t;
-  if (topo) {
-    FTAR_RETURN_IF(to_topology(topo, c->nranks, &t));
-  } else if (!c->auto_topo) {
-    t = c->topo;
-  } else {
-    ftar_topo_t ch;
-    FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
-    FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
-  }
   Form form;
   form.allgather = c->allgather;
   form.reduce_scatter = c->reduce_scatter;
   if (host && form.allgather == FTAR_AG_COLLECTIVE) form.allgather = FTAR_AG_DIRECT;  // D2H needs pieces
-  const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(form.allgather) + "/rs" +
-                          std::to_string(form.reduce_scatter);
-  auto it = c->plans.find(key);
-  if (it == c->plans.end()) {
-    auto p = std::make_shared<Plan>();
-    FTAR_RETURN_IF(check_world(t, c->nranks, count, form));  // once per (topology, count, form)
-    FTAR_RETURN_IF(build_plan(t, c->nranks, c->rank, count, p.get(), form));
-    if (c->plans.size() > 64) c->plans.clear();
-    it = c->plans.emplace(key, p).first;
-  }
-  const Plan& plan = *it->second;
-  if (plan.max_k > FTAR_MAX_K) return FTAR_ERR_UNSUPPORTED;
+  const Plan* planp = nullptr;
+  FTAR_RETURN_IF(resolve_plan(c, topo, count, esz, form, &planp));
+  const Plan& plan = *planp;
   const size_t nst = plan.stages.size();
   if (!host && c->peer_direct && peer_eligible(plan)) {
     FTAR_RETURN_IF(grow_events(c, 5));
@@ -256,90 +349,28 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   // k of every stage touches exactly piece k of each block: the same bytes,
   // the same partition, the same bits as the device path.
   size_t chunk_bytes = c->chunk_bytes;
-  if (host) chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
   if (host) {
-    if (count * esz > c->staging_bytes) {
-      if (c->staging) {  // earlier calls may still copy into or out of it
-        FTAR_CHECK_HIP(hipStreamSynchronize(c->h2d_s));
-        FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
-        FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-        FTAR_CHECK_HIP(hipStreamSynchronize(c->d2h_s));
-        FTAR_CHECK_HIP(hipFree(c->staging));
-        c->staging = nullptr;
-        c->staging_bytes = 0;
-      }
-      FTAR_CHECK_HIP(hipMalloc(&c->staging, count * esz));
-      c->staging_bytes = count * esz;
-    }
+    chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
+    FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, count * esz, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     sendbuf = nullptr;
     recvbuf = c->staging;
   }
-  size_t chunk = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63));
+  const size_t chunk = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63));
   const size_t nchunks = std::max<size_t>(1, (plan.split + chunk - 1) / chunk);
-
-  // per-stage facts: the latest reducing stage before it (its data), and in
-  // the device (stage-major) order the last reader of the scratch half it
-  // receives into
-  std::vector<char> moves(nst), reduces(nst), to_scratch(nst);
-  std::vector<long> prev_red(nst, -1), war(nst, -1);
-  {
-    long last = -1, owner[2] = {-1, -1};
-    for (size_t s = 0; s < nst; ++s) {
-      const Stage& st = plan.stages[s];
-      moves[s] = !st.sends.empty() || !st.recvs.empty();
-      reduces[s] = !st.reduces.empty();
-      for (const Transfer& x : st.recvs) to_scratch[s] |= x.buf == BUF_SCRATCH;
-      prev_red[s] = last;
-      war[s] = to_scratch[s] ? owner[s % 2] : -1;
-      if (reduces[s]) {
-        last = (long)s;
-        if (to_scratch[s]) owner[s % 2] = (long)s;
-      }
-    }
-  }
-  // Order of the (stage, piece) steps, identical on every rank.  Device:
-  // stage-major.  Host: stage s+1 trails stage s by one piece, so the
-  // all-gather of piece k (and its D2H) runs while later pieces are still
-  // coming in over PCIe.  Skewed steps of stages two apart may overlap in
-  // time, so there every stage gets its own scratch region instead of
-  // alternating halves (scratch offsets remapped by delta[s]).
+  const StageFacts f(plan);
+  const std::vector<char>& moves = f.moves;
+  const std::vector<char>& reduces = f.reduces;
+  const std::vector<long>& prev_red = f.prev_red;
+  const std::vector<long>& war = f.war;
+  // Device: stage-major.  Host: skewed, so the all-gather of piece k (and its
+  // D2H) runs while later pieces are still coming in over PCIe; skewed steps
+  // of stages two apart may overlap in time, so every stage gets its own
+  // scratch region instead of alternating halves.
   const bool skew = host != nullptr;
   std::vector<long> delta(nst, 0);
-  size_t scratch_elems = 2 * plan.scratch_half;
-  if (skew) {
-    size_t base = 0;
-    for (size_t s = 0; s < nst; ++s) {
-      const size_t half_base = (s % 2) * plan.scratch_half;
-      size_t used = 0;
-      for (const Transfer& x : plan.stages[s].recvs)
-        if (x.buf == BUF_SCRATCH) used = std::max(used, x.off - half_base + x.len);
-      delta[s] = (long)base - (long)half_base;
-      base += used;
-    }
-    scratch_elems = base;
-  }
-  const size_t need = scratch_elems * esz;
-  if (need > c->scratch_bytes) {
-    if (c->scratch) {  // work of earlier calls may still read it
-      FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
-      FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-      FTAR_CHECK_HIP(hipFree(c->scratch));
-      c->scratch = nullptr;
-      c->scratch_bytes = 0;
-    }
-    FTAR_CHECK_HIP(hipMalloc(&c->scratch, need));
-    c->scratch_bytes = need;
-  }
-  std::vector<std::pair<size_t, size_t>> order;
-  order.reserve(nst * nchunks);
-  if (!skew) {
-    for (size_t s = 0; s < nst; ++s)
-      for (size_t k = 0; k < nchunks; ++k) order.emplace_back(s, k);
-  } else {
-    for (size_t tt = 0; tt < nchunks + nst - 1; ++tt)
-      for (size_t s = 0; s < nst && s <= tt; ++s)
-        if (tt - s < nchunks) order.emplace_back(s, tt - s);
-  }
+  const size_t scratch_elems = skew ? per_stage_scratch(plan, &delta) : 2 * plan.scratch_half;
+  FTAR_RETURN_IF(ensure_buffer(&c->scratch, &c->scratch_bytes, scratch_elems * esz, {c->comm_s, c->red_s}));
+  const std::vector<std::pair<size_t, size_t>> order = step_order(nst, nchunks, skew);
 
   FTAR_RETURN_IF(grow_events(c, 2 * nst * nchunks + 2 * nchunks + 5));
   hipEvent_t* ev = c->events.data();
