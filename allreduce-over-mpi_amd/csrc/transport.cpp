@@ -78,20 +78,28 @@ class RcclTransport final : public Transport {
     (void)hipStreamDestroy(s);
     FTAR_RETURN_IF(st);
     peers->assign(nranks, nullptr);
-    for (int q = 0; q < nranks; ++q) {
+    std::string why;
+    for (int q = 0; q < nranks && why.empty(); ++q) {
       if (q == rank) {
         (*peers)[q] = static_cast<char*>(mine);
         continue;
       }
       void* p = nullptr;
       hipError_t e = hipIpcOpenMemHandle(&p, all[q], hipIpcMemLazyEnablePeerAccess);
-      if (e != hipSuccess) {
-        unmap_peers(peers, rank);
-        set_error(std::string("hipIpcOpenMemHandle(rank ") + std::to_string(q) + "): " + hipGetErrorString(e),
-                  __FILE__, __LINE__);
-        return FTAR_ERR_HIP;
-      }
-      (*peers)[q] = static_cast<char*>(p);
+      if (e != hipSuccess)
+        why = std::string("hipIpcOpenMemHandle(rank ") + std::to_string(q) + "): " + hipGetErrorString(e);
+      else
+        (*peers)[q] = static_cast<char*>(p);
+    }
+    // every rank learns whether every rank mapped every peer: a rank that
+    // failed alone would otherwise leave the others waiting in the next barrier
+    int failed = 0;
+    FTAR_RETURN_IF(agree_failures(why.empty() ? 0 : 1, &failed));
+    if (failed) {
+      unmap_peers(peers, rank);
+      set_error(why.empty() ? std::to_string(failed) + " peer rank(s) could not map the exchange buffers" : why,
+                __FILE__, __LINE__);
+      return FTAR_ERR_HIP;
     }
     return FTAR_SUCCESS;
   }
@@ -142,6 +150,22 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  // sum of every rank's `mine` (host-blocking, on a private stream)
+  ftar_status_t agree_failures(int mine, int* total) {
+    int* word = reinterpret_cast<int*>(static_cast<char*>(scratch_) + 128);
+    hipStream_t s;
+    FTAR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    bool ok = hipMemcpyAsync(word, &mine, sizeof mine, hipMemcpyHostToDevice, s) == hipSuccess &&
+              ncclAllReduce(word, word, 1, ncclInt32, ncclSum, comm_, s) == ncclSuccess &&
+              hipMemcpyAsync(total, word, sizeof *total, hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipStreamSynchronize(s) == hipSuccess;
+    (void)hipStreamDestroy(s);
+    if (!ok) {
+      set_error("peer map: failure agreement failed", __FILE__, __LINE__);
+      return FTAR_ERR_RCCL;
+    }
+    return FTAR_SUCCESS;
+  }
   ftar_status_t ensure_scratch() {  // barrier word + FTAR_MAX_K IPC handles
     if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)FTAR_MAX_K * sizeof(hipIpcMemHandle_t)));
     return FTAR_SUCCESS;

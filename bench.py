@@ -195,6 +195,18 @@ def _factorizations(n):
 
 
 def bench_distributed(a):
+    """N > 1: one rank per GPU.  Order of work, safest first, so that a configuration that hangs on a node
+    cannot cost the run its result:
+      1. the default configuration (FT_TOPO/--topo, else the cost model; RCCL p2p, direct forms) timed for
+         exactly K steps after W warmup -- the headline unless the sweep finds a faster *validated* one;
+      2. the sweep (BASELINE configs[3]: topology x chunk x data-movement form), RCCL forms first, the
+         IPC peer-read form last, inside a time budget every rank agrees on;
+      3. the sweep's best, re-timed for exactly K steps after W warmup, if it beats the default;
+      4. RCCL's own ncclAllReduce on the same bucket (yardstick).
+    A watchdog (FTAR_BENCH_BUDGET_S, default 540 s) prints the best line measured so far and ends every
+    rank if anything hangs."""
+    import threading
+
     import torch
     import torch.distributed as dist
 
@@ -203,6 +215,34 @@ def bench_distributed(a):
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
+    t_start = time.time()
+    budget = float(os.environ.get("FTAR_BENCH_BUDGET_S", "540"))
+    sweep_budget = float(os.environ.get("FTAR_BENCH_SWEEP_S", "240"))
+    state = {"line": None, "printed": False, "done": False, "phase": "init"}
+    lock = threading.Lock()
+
+    def emit(res):
+        with lock:
+            if rank == 0 and not state["printed"]:
+                print(json.dumps(res), flush=True)
+            state["printed"] = True
+
+    def watchdog():
+        while time.time() - t_start < budget:
+            time.sleep(1.0)
+            if state["done"]:
+                return
+        sys.stderr.write(f"[bench rank {rank}] watchdog: {budget:.0f}s exceeded in phase {state['phase']}\n")
+        if state["line"] is not None:
+            res = dict(state["line"])
+            res["watchdog"] = f"run cut at {budget:.0f}s in phase '{state['phase']}'; headline = last complete measurement"
+            emit(res)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0 if state["line"] is not None else 3)
+
+    threading.Thread(target=watchdog, daemon=True).start()
+
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -252,118 +292,151 @@ def bench_distributed(a):
     eps = 2.0 ** -24 if a.dtype == "f32" else 2.0 ** -8
     tol = (world - 1) * eps * absum + 1e-30
 
-    def check_y():
+    def check_y(fn):
+        """y (from the timed calls) against the fp64 sample and across ranks; then one more call on the
+        negated inputs must give exactly -y everywhere (round-to-nearest-even is sign-symmetric), which
+        proves the call read this call's data (no stale copies) over the whole bucket."""
         torch.cuda.synchronize()
         mine = y[idx].float().cpu()
         ally = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(ally, mine)
         ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
+        y1 = y.clone()
+        x.neg_()
+        fn()
+        torch.cuda.synchronize()
+        ok = ok and bool(torch.equal(y, y1.neg_()))
+        x.neg_()
+        del y1
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return bool(flag.item())
 
-    # default: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model; default chunk
+    def bws(m):
+        alg = bucket / (m * 1e-3) / 1e9
+        return alg, (alg * 2 * (world - 1) / world if world > 1 else alg)
+
+    def make_result(ms, topo_, chunk, form, ok, steps, warmup, extra):
+        algbw, busbw = bws(ms)
+        # links one rank drives at once: every peer in the one-round (direct/collective/peer) forms; in the
+        # reference's rounds, one neighbour (ring) or the widest stage's group (tree)
+        if form != "stages":
+            links = min(XGMI_LINKS, world - 1)
+        elif topo_.ring:
+            links = 1
+        else:
+            links = min(XGMI_LINKS, max(topo_.widths) - 1)
+        links = max(1, links)
+        peak = links * XGMI_LINK_GBPS
+        res = {
+            "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
+            "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
+            "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
+            "config": {"workload": f"{world}xMI355X FlexTree AllReduce over xGMI, "
+                                   f"{'IPC-mapped peer reads' if form == 'peer' else 'RCCL p2p'} "
+                                   "(BASELINE configs[2-3])",
+                       "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo_),
+                       "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"},
+            "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
+            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
+                         "frac": round(busbw / peak, 4), "traffic": None,
+                         "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
+            "check": "ok" if ok else "MISMATCH",
+        }
+        res.update(extra)
+        return res
+
+    # 1. the default configuration: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model
+    state["phase"] = "default"
     if a.topo:
         default_topo = ftar.topo(a.topo, a.lonely, nranks=world)
     else:
         default_topo = ftar.topo_from_env(world, bucket)
     default_chunk = a.chunk_bytes or comm.chunk_bytes
+    fn_default = run_with(default_topo, default_chunk)
+    ms_default = timed(fn_default, a.steps, a.warmup)
+    ok_default = check_y(fn_default)
+    default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": "direct",
+                    "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
+                    "check": "ok" if ok_default else "MISMATCH"}
+    state["line"] = make_result(ms_default, default_topo, default_chunk, "direct", ok_default, a.steps, a.warmup,
+                                {"config_selection": "default (sweep not reached)", "default_config": default_info})
 
-    # BASELINE configs[3]: "chunk size swept" -- every factorization of P and the ring, x chunk sizes
+    # 2. the sweep: every factorization of P and the ring x chunk sizes x form; RCCL forms first, peer reads last
+    state["phase"] = "sweep"
     sweep = []
     cands = [str(default_topo)] + (["1"] if world > 1 else []) + [",".join(map(str, f)) for f in _factorizations(world)]
-    seen = set()
+    seen, plan = set(), []
     for tp in cands:
         t = ftar.topo("1" if tp == "ring" else tp, 0 if "+" not in tp else int(tp.split("+")[1]))
         key = str(t)
         if key in seen:
             continue
         seen.add(key)
-        # data-movement form: one direct round each way (default), the reference's rounds, or a collective all-gather
-        ags = ["direct", "stages"] + (["collective"] if (not t.ring and n % world == 0 and world > 1) else [])
-        if world > 1 and not a.no_peer and t.lonely == 0:
-            ags.append("peer")
-        for ag in ags:
+        forms = ["direct"] + (["collective"] if (not t.ring and n % world == 0) else []) + ["stages"]
+        for form in forms:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
-            if key == str(default_topo) and ag == "direct":  # 256 KiB ... 64 MiB
+            if key == str(default_topo) and form == "direct":  # SURVEY §8d C4: 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
-            if ag == "peer":
-                chunks = {default_chunk}  # no pieces: one fold and one gather kernel per call
-            for chunk in sorted(chunks):
-                if world > 1 and ag == "stages" and t.ring and chunk != default_chunk:
-                    continue  # the reference's ring rounds: one point is enough
-                try:
-                    ms_ = timed(run_with(t, chunk, ag), steps=min(5, a.steps), warmup=1)
-                    ok_ = check_y()   # every configuration's own output, before it may be chosen
-                except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
-                    sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "error": str(e)[:200]})
-                    continue
-                sweep.append({"topology": key, "chunk_bytes": chunk, "form": ag, "ms": round(ms_, 4),
-                              "busbw_GBps": round(bucket / (ms_ * 1e-3) / 1e9 * 2 * (world - 1) / max(1, world), 2),
-                              "check": "ok" if ok_ else "MISMATCH"})
+            if form == "stages" and t.ring:
+                chunks = {default_chunk}  # the reference's ring rounds: one point is enough
+            plan += [(t, chunk, form) for chunk in sorted(chunks)]
+        if not a.no_peer and t.lonely == 0:
+            plan.append((t, default_chunk, "peer"))  # no pieces: one fold and one gather kernel per call
+    plan.sort(key=lambda p: p[2] == "peer")  # stable: every RCCL configuration before any peer-read one
+    sweep_t0 = time.time()
+    for t, chunk, form in plan:
+        stop = torch.tensor([1 if time.time() - sweep_t0 > sweep_budget else 0], dtype=torch.int32)
+        dist.broadcast(stop, 0)  # every rank takes the same decision
+        if stop.item():
+            sweep.append({"skipped": f"sweep budget {sweep_budget:.0f}s reached ({len(plan) - len(sweep)} left)"})
+            break
+        key = str(t)
+        state["phase"] = f"sweep {key} {form} {chunk}"
+        try:
+            fn = run_with(t, chunk, form)
+            ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
+            ok_ = check_y(fn)   # every configuration's own output, before it may be chosen
+        except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
+            sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "error": str(e)[:200]})
+            continue
+        sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "ms": round(ms_, 4),
+                      "busbw_GBps": round(bws(ms_)[1], 2), "check": "ok" if ok_ else "MISMATCH"})
+    state["line"]["sweep"] = sweep
+
+    # 3. the sweep's best validated configuration, re-timed like the default, if it is faster
+    state["phase"] = "headline"
     ok_runs = [r for r in sweep if "ms" in r and r.get("check") == "ok"]
-    best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else {
-        "topology": str(default_topo), "chunk_bytes": default_chunk, "form": "direct"}
-    best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
+    best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else None
+    if best is not None and best["ms"] < ms_default:
+        best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
+        fn_best = run_with(best_topo, best["chunk_bytes"], best["form"])
+        ms = timed(fn_best, a.steps, a.warmup)
+        ok = check_y(fn_best)
+        if ok and ms < ms_default:
+            state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,
+                                        {"config_selection": "best validated configuration of the sweep",
+                                         "default_config": default_info, "sweep": sweep})
+        else:
+            state["line"]["config_selection"] = "default (sweep best not faster when re-timed)"
+    else:
+        state["line"]["config_selection"] = "default (fastest validated configuration)"
 
-    # headline: the swept-best configuration, K timed steps after W warmup
-    ms = timed(run_with(best_topo, best["chunk_bytes"], best["form"]), a.steps, a.warmup)
-    ms_default = timed(run_with(default_topo, default_chunk), min(a.steps, 10), 1)
-    run_with(best_topo, best["chunk_bytes"], best["form"])
-    comm.allreduce(x, y, n, a.dtype, "sum", topo_=best_topo, stream=stream)
-    torch.cuda.synchronize()
-
-    # RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
+    # 4. RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
+    state["phase"] = "rccl yardstick"
     try:
         y2 = torch.empty_like(x)
         ms_rccl = timed(lambda: comm.rccl_allreduce(x, y2, n, a.dtype, "sum", stream=stream), min(a.steps, 10), 2)
         del y2
+        state["line"]["rccl_native_allreduce"] = {"ms": round(ms_rccl, 4), "busbw_GBps": round(bws(ms_rccl)[1], 2)}
     except Exception as e:  # noqa: BLE001
-        ms_rccl = None
+        state["line"]["rccl_native_allreduce"] = None
         sys.stderr.write(f"rccl yardstick failed: {e}\n")
 
-    ok = check_y()   # the headline configuration's output (run just above)
-
-    def bws(m):
-        alg = bucket / (m * 1e-3) / 1e9
-        return alg, (alg * 2 * (world - 1) / world if world > 1 else alg)
-
-    algbw, busbw = bws(ms)
-    # links one rank drives at once: every peer in the one-round (direct/collective) forms; in the reference's
-    # rounds, one neighbour (ring) or the widest stage's group (tree)
-    if best["form"] != "stages":
-        links = min(XGMI_LINKS, world - 1)
-    elif best_topo.ring:
-        links = 1
-    else:
-        links = min(XGMI_LINKS, max(best_topo.widths) - 1)
-    links = max(1, links)
-    peak = links * XGMI_LINK_GBPS
-    if rank == 0:
-        res = {
-            "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
-            "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
-            "config": {"workload": f"{world}xMI355X FlexTree AllReduce over xGMI, "
-                                   f"{'IPC-mapped peer reads' if best['form'] == 'peer' else 'RCCL p2p'} "
-                                   "(BASELINE configs[2-3])",
-                       "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(best_topo),
-                       "chunk_bytes": best["chunk_bytes"], "form": best["form"],
-                       "selection": "best of sweep (FT_TOPO x chunk x data-movement form)",
-                       "parallelism": f"dp{world}"},
-            "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
-            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
-                         "frac": round(busbw / peak, 4), "traffic": None,
-                         "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
-            "default_config": {"topology": str(default_topo), "chunk_bytes": default_chunk, "ms": round(ms_default, 4),
-                               "busbw_GBps": round(bws(ms_default)[1], 2)},
-            "rccl_native_allreduce": None if ms_rccl is None else
-            {"ms": round(ms_rccl, 4), "busbw_GBps": round(bws(ms_rccl)[1], 2)},
-            "sweep": sweep,
-            "check": "ok" if ok else "MISMATCH",
-        }
-        print(json.dumps(res), flush=True)
+    state["line"]["wall_s"] = round(time.time() - t_start, 1)
+    emit(state["line"])
+    state["done"] = True
     comm.destroy()
     dist.destroy_process_group()
 
