@@ -37,7 +37,7 @@ struct ftar_comm {
   size_t staging_bytes = 0;
   size_t chunk_bytes = 0;
   size_t host_chunk_bytes = 0;
-  bool peer_direct = false;        // FTAR_PEER_DIRECT / ftar_comm_set_peer_direct
+  int peer_direct = 0;             // FTAR_PEER_DIRECT / ftar_comm_set_peer_direct: 0 off, 1 read, 2 write
   void* xbuf = nullptr;            // peer-direct exchange buffer (IPC-exported), grow-only
   size_t xbuf_bytes = 0;
   std::vector<char*> xpeers;       // every rank's exchange buffer, mapped here
@@ -78,7 +78,11 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
-  if (const char* pd = getenv("FTAR_PEER_DIRECT")) c->peer_direct = atoi(pd) != 0;
+  if (const char* pd = getenv("FTAR_PEER_DIRECT")) {
+    const std::string m(pd);
+    c->peer_direct = m == "write" ? FTAR_PEER_WRITE : m == "read" ? FTAR_PEER_READ
+                     : std::max(0, std::min(2, atoi(pd)));
+  }
   const char* hcb = getenv("FTAR_HOST_CHUNK_BYTES");
   c->host_chunk_bytes = hcb ? strtoull(hcb, nullptr, 0) : kDefaultHostChunkBytes;
   if (c->host_chunk_bytes && c->host_chunk_bytes < 256) c->host_chunk_bytes = 256;
@@ -115,85 +119,180 @@ void comm_teardown(ftar_comm* c) {
 }
 
 // ---------------------------------------------------------------------------
-// Peer-direct execution of a one-round plan (ring or tree, direct forms):
-// instead of RCCL moving blocks into scratch and a fold reading scratch, every
-// rank's fold reads the other ranks' copies straight out of their exchange
-// buffers over xGMI (IPC-mapped), and the all-gather pulls every final block
-// the same way.  The plan's own fold (operand order, nested shape, bf16
-// rounding) is executed unchanged, so the bits are the plan's.
-//   in -> X (local copy) | barrier | fold into X[own block] | barrier |
-//   gather every owner's block from X_q -> recvbuf | barrier
+// Peer-direct execution of a one-round plan (ring or tree, direct forms): no
+// RCCL data movement, no scratch pass.  Kernels move the blocks over xGMI
+// through IPC-mapped exchange buffers X (grow-only, comm-owned), and the
+// plan's own fold (operand order, nested shape, bf16 rounding) runs
+// unchanged, so the bits are the plan's.  Two forms:
+//
+//  READ (pull)   in -> X | barrier | fold my block reading every rank's copy
+//                from X_q, into X | barrier | gather every owner's block from
+//                X_q -> recvbuf | barrier (X stays intact until all have read)
+//  WRITE (push)  scatter: my copy of q's block -> X_q.slot[me], all peers in
+//                one launch | barrier | fold my block from in + X.slot[*]
+//                into recvbuf | push it -> X_q.final[my block] | barrier |
+//                X.final[other blocks] -> recvbuf
+//                Two barriers: call i's scatter lands after every rank passed
+//                call i-1's second barrier (its fold is done), and its pushes
+//                after every rank's call i-1 copy-out (first barrier of i).
+//
 // The barriers are stream-ordered (Transport::barrier), nothing spins on the
-// device; the last one keeps X intact until every peer has read it.
+// device.  Cross-GPU visibility rests on kernel-boundary release/acquire.
 // ---------------------------------------------------------------------------
 bool peer_eligible(const Plan& plan) {
   if (plan.stages.size() != 2 || plan.allgather != FTAR_AG_DIRECT || plan.nranks > FTAR_MAX_K) return false;
   const Stage& rs = plan.stages[0];
   const Stage& ag = plan.stages[1];
+  if (rs.reduces.size() > 1) return false;
+  std::vector<int> seen_s(plan.nranks, 0), seen_r(plan.nranks, 0), seen_a(plan.nranks, 0);
+  for (const Transfer& x : rs.sends)  // one block per peer each way (the write form's slot = sender)
+    if (x.buf != BUF_SRC || x.len > plan.split || seen_s[x.peer]++) return false;
   for (const Transfer& x : rs.recvs)
-    if (x.buf != BUF_SCRATCH) return false;
+    if (x.buf != BUF_SCRATCH || seen_r[x.peer]++) return false;
   for (const ReduceItem& r : rs.reduces)
     for (const Operand& o : r.srcs)
       if (o.buf == BUF_DST) return false;
   for (const Transfer& x : ag.recvs)
+    if (x.buf != BUF_DST || seen_a[x.peer]++) return false;
+  for (const Transfer& x : ag.sends)
     if (x.buf != BUF_DST) return false;
   return ag.reduces.empty();
 }
 
+namespace {
+// grow-only exchange buffer, exported and mapped by every rank (collective)
+ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
+  if (bytes <= c->xbuf_bytes && !c->xpeers.empty()) return FTAR_SUCCESS;
+  Transport* tp = c->tp.get();
+  FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still touches the old X
+  FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
+  const size_t want = std::max(bytes, c->xbuf_bytes);
+  tp->unmap_peers(&c->xpeers, c->rank);
+  if (c->xbuf) FTAR_CHECK_HIP(hipFree(c->xbuf));
+  c->xbuf = nullptr;
+  c->xbuf_bytes = 0;
+  FTAR_CHECK_HIP(hipMalloc(&c->xbuf, want));
+  c->xbuf_bytes = want;
+  return tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers);
+}
+
+// the plan's fold of my block with operand i read from where(i)
+template <class Where>
+ftar_status_t peer_fold(const ReduceItem& r, const Plan& plan, ftar_dtype_t dt, ftar_op_t op, void* dst,
+                        hipStream_t s, Where where) {
+  std::map<size_t, int> slot_peer;  // scratch slot -> the rank that would have sent it
+  for (const Transfer& x : plan.stages[0].recvs) slot_peer[x.off] = x.peer;
+  std::vector<const void*> srcs;
+  for (const Operand& o : r.srcs) {
+    if (o.buf == BUF_SRC) {
+      srcs.push_back(where(-1, o.off));
+    } else {
+      auto it = slot_peer.find(o.off);
+      if (it == slot_peer.end()) return FTAR_ERR_INTERNAL;
+      srcs.push_back(where(it->second, r.off));
+    }
+  }
+  return launch_reduce(srcs.data(), (int)srcs.size(), dst, r.len, dt, op, s, r.round_each, r.shape.data(),
+                       (int)r.shape.size());
+}
+}  // namespace
+
 ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                              const Plan& plan, ftar_comm* c, hipStream_t stream) {
   const size_t esz = dtype_size(dt), bytes = count * esz;
+  const bool write = c->peer_direct == FTAR_PEER_WRITE;
+  const size_t slot_bytes = plan.split * esz, final_at = (size_t)plan.nranks * slot_bytes;
+  FTAR_RETURN_IF(ensure_xbuf(c, write ? final_at + bytes : bytes));
   Transport* tp = c->tp.get();
-  if (bytes > c->xbuf_bytes) {  // collective: every rank sees the same counts, so all grow together
-    FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still reads the old X
-    FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-    tp->unmap_peers(&c->xpeers, c->rank);
-    if (c->xbuf) FTAR_CHECK_HIP(hipFree(c->xbuf));
-    c->xbuf = nullptr;
-    c->xbuf_bytes = 0;
-    FTAR_CHECK_HIP(hipMalloc(&c->xbuf, bytes));
-    c->xbuf_bytes = bytes;
-    FTAR_RETURN_IF(tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers));
-  }
   char* X = static_cast<char*>(c->xbuf);
+  char* out = static_cast<char*>(recvbuf);
+  const char* in = static_cast<const char*>(sendbuf ? sendbuf : recvbuf);
   const std::vector<char*>& Xq = c->xpeers;
+  const Stage& rs = plan.stages[0];
+  const Stage& ag = plan.stages[1];
   hipEvent_t* ev = c->events.data();
   FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
-  const void* in = sendbuf ? sendbuf : recvbuf;
-  FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
-  FTAR_RETURN_IF(tp->barrier(c->comm_s));
-  // reduce-scatter: scratch slot -> the rank that would have sent it
-  const Stage& rs = plan.stages[0];
-  std::map<size_t, int> slot_peer;
-  for (const Transfer& x : rs.recvs) slot_peer[x.off] = x.peer;
-  std::vector<const void*> srcs;
-  for (const ReduceItem& r : rs.reduces) {
-    srcs.clear();
-    for (const Operand& o : r.srcs) {
-      if (o.buf == BUF_SRC) {
-        srcs.push_back(X + o.off * esz);
-      } else {
-        auto it = slot_peer.find(o.off);
-        if (it == slot_peer.end()) return FTAR_ERR_INTERNAL;
-        srcs.push_back(Xq[it->second] + r.off * esz);  // that rank's copy of this block
-      }
-    }
-    FTAR_RETURN_IF(launch_reduce(srcs.data(), (int)srcs.size(), X + r.off * esz, r.len, dt, op, c->comm_s,
-                                 r.round_each, r.shape.data(), (int)r.shape.size()));
-  }
-  FTAR_RETURN_IF(tp->barrier(c->comm_s));
-  // all-gather: every owner's final block from its exchange buffer, one launch
   std::vector<Segment> segs;
-  for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, static_cast<char*>(recvbuf) + r.off * esz,
-                                                         r.len * esz});
-  for (const Transfer& x : plan.stages[1].recvs)
-    segs.push_back({Xq[x.peer] + x.off * esz, static_cast<char*>(recvbuf) + x.off * esz, x.len * esz});
-  FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
-  FTAR_RETURN_IF(tp->barrier(c->comm_s));
+  if (!write) {
+    FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    for (const ReduceItem& r : rs.reduces)
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, X + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+        return q < 0 ? X + off * esz : Xq[q] + off * esz;  // that rank's copy of this block
+      }));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    // all-gather: every owner's final block from its exchange buffer, one launch
+    for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, out + r.off * esz, r.len * esz});
+    for (const Transfer& x : ag.recvs) segs.push_back({Xq[x.peer] + x.off * esz, out + x.off * esz, x.len * esz});
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+  } else {
+    // scatter my copy of every peer's block into its slot for me, all links at once
+    for (const Transfer& x : rs.sends)
+      segs.push_back({in + x.off * esz, Xq[x.peer] + (size_t)c->rank * slot_bytes, x.len * esz});
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    for (const ReduceItem& r : rs.reduces)
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+        return q < 0 ? in + off * esz : X + (size_t)q * slot_bytes;  // rank q's copy, pushed into slot q
+      }));
+    segs.clear();  // my final block into every peer's final area
+    for (const Transfer& x : ag.sends) segs.push_back({out + x.off * esz, Xq[x.peer] + final_at + x.off * esz,
+                                                       x.len * esz});
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    segs.clear();
+    for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+  }
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
   return FTAR_SUCCESS;
+}
+
+// xGMI probe (diagnostic, collective): every rank runs the same copy pattern
+// at the same time between barriers, timed with events on the comm stream.
+ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int nout) {
+  const int P = c->nranks, me = c->rank;
+  FTAR_RETURN_IF(ensure_xbuf(c, 2 * (size_t)P * bytes));  // P send slots + P receive slots
+  Transport* tp = c->tp.get();
+  char* X = static_cast<char*>(c->xbuf);
+  const std::vector<char*>& Xq = c->xpeers;
+  auto send_slot = [&](char* base, int q) { return base + (size_t)q * bytes; };
+  auto recv_slot = [&](char* base, int q) { return base + (size_t)(P + q) * bytes; };
+  hipEvent_t e0, e1;
+  FTAR_CHECK_HIP(hipEventCreate(&e0));
+  FTAR_CHECK_HIP(hipEventCreate(&e1));
+  ftar_status_t st = FTAR_SUCCESS;
+  const int nxt = (me + 1) % P, prv = (me + P - 1) % P;
+  // 0 local copy | 1 read from one peer | 2 read from all | 3 write to one | 4 write to all
+  for (int mode = 0; mode < std::min(nout, 5) && st == FTAR_SUCCESS; ++mode) {
+    std::vector<Segment> segs;
+    if (mode == 0) segs.push_back({send_slot(X, 0), recv_slot(X, 0), bytes});
+    if (mode == 1 && P > 1) segs.push_back({send_slot(Xq[nxt], me), recv_slot(X, nxt), bytes});
+    if (mode == 3 && P > 1) segs.push_back({send_slot(X, prv), recv_slot(Xq[prv], me), bytes});
+    for (int q = 0; q < P; ++q) {
+      if (q == me) continue;
+      if (mode == 2) segs.push_back({send_slot(Xq[q], me), recv_slot(X, q), bytes});
+      if (mode == 4) segs.push_back({send_slot(X, q), recv_slot(Xq[q], me), bytes});
+    }
+    out[mode] = 0.0;
+    if (segs.empty()) continue;
+    if ((st = launch_gather(segs.data(), (int)segs.size(), c->comm_s)) != FTAR_SUCCESS) break;  // warm
+    if ((st = tp->barrier(c->comm_s)) != FTAR_SUCCESS) break;
+    if (hipEventRecord(e0, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
+    for (int i = 0; i < iters && st == FTAR_SUCCESS; ++i) st = launch_gather(segs.data(), (int)segs.size(), c->comm_s);
+    if (st == FTAR_SUCCESS && hipEventRecord(e1, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
+    if (st == FTAR_SUCCESS) st = tp->barrier(c->comm_s);
+    if (st == FTAR_SUCCESS && hipStreamSynchronize(c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
+    float ms = 0.f;
+    if (st == FTAR_SUCCESS && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) st = FTAR_ERR_HIP;
+    if (st == FTAR_SUCCESS && ms > 0.f) out[mode] = (double)segs.size() * bytes * iters / (ms * 1e-3) / 1e9;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return st;
 }
 
 // Host mode: sendbuf/recvbuf of the call are host memory (pinned for overlap).
@@ -644,17 +743,24 @@ ftar_status_t ftar_debug_peer_selftest(ftar_comm_t comm) {
   return st;
 }
 
-ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int enable) {
-  if (!comm) return FTAR_ERR_INVALID_ARG;
+ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode) {
+  if (!comm || mode < FTAR_PEER_OFF || mode > FTAR_PEER_WRITE) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
-  comm->peer_direct = enable != 0;
+  comm->peer_direct = mode;
   return FTAR_SUCCESS;
 }
 
-ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* enable) {
-  if (!comm || !enable) return FTAR_ERR_INVALID_ARG;
-  *enable = comm->peer_direct ? 1 : 0;
+ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode) {
+  if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  *mode = comm->peer_direct;
   return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters, double* gbps, int n) {
+  if (!comm || !gbps || n <= 0 || iters <= 0 || bytes_per_peer == 0) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n);
 }
 
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {

@@ -510,8 +510,11 @@ __global__ void __launch_bounds__(kThreads)
 
 // ---------------------------------------------------------------------------
 // multi-segment copy: the peer-direct all-gather pulls every rank's final block
-// (over xGMI) into the caller's buffer in ONE launch, grid.y = segment, so all
-// links stream at once.  16 B per lane per access when source and destination
+// (over xGMI) into the caller's buffer in ONE launch.  Workgroup w copies
+// piece w / m of segment w % m: consecutive workgroups -- the ones resident
+// at the same time -- pull from different ranks, so every link streams at
+// once (a grid.y = segment layout would dispatch segment 0's workgroups
+// first and drive one link at a time).  16 B per lane per access when source and destination
 // share their address mod 16 (always, in the all-gather: both sit at the same
 // block offset of 256-B aligned buffers); bytes otherwise.
 // ---------------------------------------------------------------------------
@@ -521,12 +524,13 @@ struct SegArgs {
   size_t bytes[FTAR_MAX_K];
 };
 
-__global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a) {
-  const int sgi = blockIdx.y;
+__global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
+  const int sgi = (int)(blockIdx.x % (unsigned)m);
+  const size_t bid = blockIdx.x / (unsigned)m, nb = gridDim.x / (unsigned)m;
   const char* src = a.src[sgi];
   char* dst = a.dst[sgi];
   const size_t n = a.bytes[sgi];
-  const size_t tid = (size_t)blockIdx.x * kThreads + threadIdx.x, nthr = (size_t)gridDim.x * kThreads;
+  const size_t tid = bid * kThreads + threadIdx.x, nthr = nb * kThreads;
   const uintptr_t ms = reinterpret_cast<uintptr_t>(src) & 15, md = reinterpret_cast<uintptr_t>(dst) & 15;
   if (ms != md) {
     for (size_t i = tid; i < n; i += nthr) dst[i] = src[i];
@@ -539,8 +543,8 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a) {
   if (tid < n - tail_at) dst[tail_at + tid] = src[tail_at + tid];
   const u32x4* s4 = reinterpret_cast<const u32x4*>(src + head);
   u32x4* d4 = reinterpret_cast<u32x4*>(dst + head);
-  size_t v = (size_t)blockIdx.x * (2 * kThreads) + threadIdx.x;
-  const size_t stride = (size_t)gridDim.x * (2 * kThreads);
+  size_t v = bid * (2 * kThreads) + threadIdx.x;
+  const size_t stride = nb * (2 * kThreads);
   for (; v + kThreads < nvec; v += stride) {
     const u32x4 x0 = s4[v], x1 = s4[v + kThreads];
     d4[v] = x0;
@@ -752,8 +756,8 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream) 
   }
   if (!m) return FTAR_SUCCESS;
   size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
-  bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)bx, (unsigned)m), dim3(kThreads), 0, stream, a);
+  bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
   FTAR_CHECK_HIP(hipGetLastError());
   return FTAR_SUCCESS;
 }

@@ -110,6 +110,16 @@ _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_
                                            ctypes.POINTER(Topo), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
+_lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
+PEER_MODE = {"off": 0, "read": 1, "write": 2}                # ftar_peer_mode_t
+
+
+def _peer_mode(mode):
+    if isinstance(mode, str):
+        return PEER_MODE[mode]
+    if mode is True or mode is False:
+        return int(mode)
+    return int(mode)
 _lib.ftar_comm_set_host_chunk_bytes.argtypes = [_vp, _sz]
 _lib.ftar_comm_get_host_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
@@ -329,14 +339,23 @@ class Comm:
 
     @property
     def peer_direct(self):
-        """Peer-direct data movement (IPC-mapped exchange buffers, no RCCL data path) for one-round plans."""
+        """Peer-direct data movement for one-round plans (IPC-mapped exchange buffers, no RCCL data path):
+        0 off, 1 read (folds and the all-gather pull from peers), 2 write (peers' blocks are pushed)."""
         v = _int()
         _check(_lib.ftar_comm_get_peer_direct(self.handle, ctypes.byref(v)), "peer_direct")
-        return bool(v.value)
+        return v.value
 
     @peer_direct.setter
-    def peer_direct(self, on):
-        _check(_lib.ftar_comm_set_peer_direct(self.handle, 1 if on else 0), "peer_direct")
+    def peer_direct(self, mode):
+        _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
+
+    def xgmi_probe(self, bytes_per_peer=64 << 20, iters=10):
+        """Collective xGMI calibration (ftar_xgmi_probe): GB/s of copy kernels through the exchange buffers,
+        every rank running the same pattern at once."""
+        out = (ctypes.c_double * 5)()
+        _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, 5), "ftar_xgmi_probe")
+        return dict(zip(("local_copy", "read_one_peer", "read_all_peers", "write_one_peer", "write_all_peers"),
+                        (round(v, 2) for v in out)))
 
     @property
     def host_chunk_bytes(self):

@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--chunk-bytes", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct form out of the sweep")
+    ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct forms out of the sweep")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     return ap.parse_args()
@@ -200,7 +200,7 @@ def bench_distributed(a):
       1. the default configuration (FT_TOPO/--topo, else the cost model; RCCL p2p, direct forms) timed for
          exactly K steps after W warmup -- the headline unless the sweep finds a faster *validated* one;
       2. the sweep (BASELINE configs[3]: topology x chunk x data-movement form), RCCL forms first, the
-         IPC peer-read form last, inside a time budget every rank agrees on;
+         IPC peer forms (read, write) last, inside a time budget every rank agrees on;
       3. the sweep's best, re-timed for exactly K steps after W warmup, if it beats the default;
       4. RCCL's own ncclAllReduce on the same bucket (yardstick).
     A watchdog (FTAR_BENCH_BUDGET_S, default 540 s) prints the best line measured so far and ends every
@@ -275,10 +275,11 @@ def bench_distributed(a):
 
     def run_with(topo, chunk, form="direct"):
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
-        rounds both ways), "collective" (ncclAllGather) or "peer" (one-round plan, IPC-mapped peer reads)."""
+        rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
+        kernel loads / stores through IPC-mapped exchange buffers)."""
         comm.chunk_bytes = chunk
-        comm.peer_direct = form == "peer"
-        comm.allgather = "direct" if form == "peer" else form
+        comm.peer_direct = form[len("peer-"):] if form.startswith("peer-") else 0
+        comm.allgather = "direct" if form.startswith("peer-") else form
         comm.reduce_scatter = "stages" if form == "stages" else "direct"
         return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
 
@@ -334,7 +335,7 @@ def bench_distributed(a):
             "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (torch.rand uniform [-1,1), HBM-resident)",
             "config": {"workload": f"{world}xMI355X FlexTree AllReduce over xGMI, "
-                                   f"{'IPC-mapped peer reads' if form == 'peer' else 'RCCL p2p'} "
+                                   f"{'IPC-mapped ' + form if form.startswith('peer-') else 'RCCL p2p'} "
                                    "(BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo_),
                        "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"},
@@ -382,11 +383,29 @@ def bench_distributed(a):
             if form == "stages" and t.ring:
                 chunks = {default_chunk}  # the reference's ring rounds: one point is enough
             plan += [(t, chunk, form) for chunk in sorted(chunks)]
-        if not a.no_peer and t.lonely == 0:
-            plan.append((t, default_chunk, "peer"))  # no pieces: one fold and one gather kernel per call
-    plan.sort(key=lambda p: p[2] == "peer")  # stable: every RCCL configuration before any peer-read one
+        if not a.no_peer and t.lonely == 0:  # no pieces: whole-block kernels
+            plan += [(t, default_chunk, "peer-read"), (t, default_chunk, "peer-write")]
+    plan.sort(key=lambda p: p[2].startswith("peer-"))  # stable: every RCCL configuration before any peer one
     sweep_t0 = time.time()
+    probed = False
     for t, chunk, form in plan:
+        if form.startswith("peer-") and not probed and world > 1:
+            # xGMI calibration before the first peer configuration: link rates by copy kernels (read/write,
+            # one peer / all peers), every rank at once; min/max over ranks
+            probed = True
+            state["phase"] = "xgmi probe"
+            try:
+                pr = comm.xgmi_probe(64 << 20, iters=10)
+                vals = torch.tensor(list(pr.values()), dtype=torch.float64)
+                lo, hi = vals.clone(), vals.clone()
+                dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+                dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+                state["line"]["xgmi_probe_GBps"] = {k: [round(lo[i].item(), 1), round(hi[i].item(), 1)]
+                                                    for i, k in enumerate(pr)}
+                state["line"]["xgmi_probe_GBps"]["note"] = ("[min, max] over ranks; 64 MiB per peer per copy, "
+                                                            "10 launches, all ranks at once")
+            except Exception as e:  # noqa: BLE001
+                state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
         stop = torch.tensor([1 if time.time() - sweep_t0 > sweep_budget else 0], dtype=torch.int32)
         dist.broadcast(stop, 0)  # every rank takes the same decision
         if stop.item():
@@ -415,9 +434,10 @@ def bench_distributed(a):
         ms = timed(fn_best, a.steps, a.warmup)
         ok = check_y(fn_best)
         if ok and ms < ms_default:
+            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps",) if k in state["line"]}
             state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,
                                         {"config_selection": "best validated configuration of the sweep",
-                                         "default_config": default_info, "sweep": sweep})
+                                         "default_config": default_info, "sweep": sweep, **carry})
         else:
             state["line"]["config_selection"] = "default (sweep best not faster when re-timed)"
     else:

@@ -176,15 +176,21 @@ typedef enum { FTAR_RS_STAGES = 0, FTAR_RS_DIRECT = 1 } ftar_reduce_scatter_t;
 ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t mode);
 ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode);
 
-/* Peer-direct data movement (extension; default off, FTAR_PEER_DIRECT=1 at
- * init).  For one-round plans (the ring, and trees without lonely ranks, under
- * FTAR_RS_DIRECT-or-single-stage + FTAR_AG_DIRECT), each rank's fold reads the
- * other ranks' copies of its block straight from their IPC-mapped exchange
- * buffers over xGMI, and the all-gather pulls every final block the same way:
- * no RCCL data movement, no scratch pass, three stream-ordered barriers.  The
- * plan's fold is executed unchanged: same bits.  Other plans keep RCCL p2p. */
-ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int enable);
-ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* enable);
+/* Peer-direct data movement (extension; default off, FTAR_PEER_DIRECT=1|read
+ * or 2|write at init).  For one-round plans (the ring, and trees without
+ * lonely ranks, under FTAR_RS_DIRECT-or-single-stage + FTAR_AG_DIRECT), the
+ * blocks move by kernel loads/stores through IPC-mapped, comm-owned exchange
+ * buffers over xGMI instead of RCCL p2p into scratch:
+ *   FTAR_PEER_READ   each rank's fold reads the other ranks' copies of its
+ *                    block from their exchange buffers, and the all-gather
+ *                    pulls every final block (three stream-ordered barriers);
+ *   FTAR_PEER_WRITE  each rank pushes its copy of every peer's block into that
+ *                    peer's buffer, folds locally, and pushes its final block
+ *                    to every peer (two barriers).
+ * The plan's fold is executed unchanged: same bits.  Other plans keep RCCL p2p. */
+typedef enum { FTAR_PEER_OFF = 0, FTAR_PEER_READ = 1, FTAR_PEER_WRITE = 2 } ftar_peer_mode_t;
+ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode);
+ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode);
 
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
@@ -224,6 +230,13 @@ ftar_status_t ftar_comm_get_host_chunk_bytes(ftar_comm_t comm, size_t* bytes);
  * to ftar at N > 1.  FTAR_ERR_UNSUPPORTED on local (in-process) groups. */
 ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
                                   ftar_comm_t comm, void* stream);
+/* xGMI calibration (collective; every rank calls it): GB/s seen by this rank
+ * for copy kernels through the peer-direct exchange buffers, all ranks running
+ * the same pattern at once -- gbps[0] local HBM copy, [1] read from one peer
+ * (ring neighbour), [2] read from all peers at once (aggregate), [3] write to
+ * one peer, [4] write to all peers at once (aggregate).  bytes_per_peer per
+ * copy, `iters` timed launches; grows the exchange buffer to 2*P*bytes. */
+ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters, double* gbps, int n);
 
 /* ---- introspection (tests) -------------------------------------------------
  * FMA-level schedule of `rank` (same JSON shape as the reference dump in

@@ -1,5 +1,7 @@
-"""Peer-direct data movement (ftar_comm_set_peer_direct): the plan's fold reads the other ranks'
-exchange buffers directly, the all-gather pulls every final block; barriers are stream-ordered.
+"""Peer-direct data movement (ftar_comm_set_peer_direct), both forms: "read" (the plan's fold reads the
+other ranks' exchange buffers directly, the all-gather pulls every final block) and "write" (every rank
+pushes its copies into the owners' buffers, folds locally, pushes its final block); barriers are
+stream-ordered.
 
 * in-process groups on cuda:0 (local transport: the peers' buffers are plain pointers): every golden
   case, the one-round ring and trees, ragged and larger buckets, all bit-exact vs the oracle; plans
@@ -30,9 +32,9 @@ def group(P):
     return _groups[P]
 
 
-def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", rs="direct", repeat=1):
+def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", rs="direct", repeat=1, mode="read"):
     g = group(len(ins))
-    g.set_peer_direct(True)
+    g.set_peer_direct(mode)
     g.set_allgather(ag)
     g.set_reduce_scatter(rs)
     try:
@@ -49,22 +51,27 @@ def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", 
         g.set_peer_direct(False)
 
 
+MODES = ["read", "write"]
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("case", gc.allreduce_cases(max_n=70000), ids=lambda c: c["id"])
-def test_peer_direct_matches_reference_golden(case):
+def test_peer_direct_matches_reference_golden(case, mode):
     ins = gc.case_inputs(case)
     outs = run_peer(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
-                    repeat=case["repeat"])
+                    repeat=case["repeat"], mode=mode)
     for r in range(case["P"]):
         gc.check_output(case, r, outs[r])
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("dt", ["f32", "bf16", "f64", "i16"])
 @pytest.mark.parametrize("P,topo", [(2, "1"), (8, "1"), (5, "1"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3"),
                                     (16, "4,4"), (16, "2,2,2,2")])
-def test_peer_direct_one_round_plans(P, topo, dt):
+def test_peer_direct_one_round_plans(P, topo, dt, mode):
     n = 40_009 * P + 3       # ragged blocks, unaligned block offsets
     ins = [fi.fill(dt, 9, r, n) for r in range(P)]
-    outs = run_peer(ins, topo, dtype=fi.BY_NAME[dt])
+    outs = run_peer(ins, topo, dtype=fi.BY_NAME[dt], mode=mode)
     ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
     for r in range(P):
         assert outs[r].tobytes() == ref[r].tobytes(), r
@@ -72,10 +79,11 @@ def test_peer_direct_one_round_plans(P, topo, dt):
 
 @pytest.mark.parametrize("P,topo,lonely,form", [(5, "2,2", 1, "direct"), (8, "2,4", 0, "stages"),
                                                 (8, "1", 0, "stages")])
-def test_peer_direct_falls_back_for_multi_round_plans(P, topo, lonely, form):
+@pytest.mark.parametrize("mode", MODES)
+def test_peer_direct_falls_back_for_multi_round_plans(P, topo, lonely, form, mode):
     n = 30_001
     ins = [fi.fill("f32", 10, r, n) for r in range(P)]
-    outs = run_peer(ins, topo, lonely, ag=form, rs=form)
+    outs = run_peer(ins, topo, lonely, ag=form, rs=form, mode=mode)
     ref = oracle_lib.allreduce(ins, topo, lonely)
     for r in range(P):
         assert outs[r].tobytes() == ref[r].tobytes(), r
@@ -86,11 +94,12 @@ def test_peer_direct_growing_buckets_and_mode_switches():
     import ftar
     P = 4
     g = group(P)
-    for n in (1000, 200_003, 7, 600_001):
+    for i, n in enumerate((1000, 200_003, 7, 600_001, 90_001)):
         ins = [fi.fill("f32", 11, r, n) for r in range(P)]
         ref = oracle_lib.allreduce(ins, "2,2")
-        outs = run_peer(ins, "2,2")
-        assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P)), n
+        for mode in (MODES if i % 2 else MODES[::-1]):   # the two forms share (and regrow) the buffers
+            outs = run_peer(ins, "2,2", mode=mode)
+            assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P)), (n, mode)
         g.set_chunk_bytes(4096)
         bufs = [to_dev(x) for x in ins]
         g.allreduce(None, [p for _, p in bufs], n, "f32", topo_="2,2")
@@ -176,6 +185,42 @@ def test_rccl_peer_plumbing_single_rank():
         lib.ftar_debug_peer_selftest.argtypes = [ctypes.c_void_p]
         assert lib.ftar_debug_peer_selftest(comm.handle) == 0, lib.ftar_last_error()
         comm.peer_direct = True
-        assert comm.peer_direct
+        assert comm.peer_direct == 1
+        comm.peer_direct = "write"
+        assert comm.peer_direct == 2
+        probe = comm.xgmi_probe(1 << 20, iters=2)   # 1 rank: only the local copy has a partner
+        assert probe["local_copy"] > 0 and probe["read_all_peers"] == 0, probe
     finally:
         comm.destroy()
+
+
+@pytest.mark.parametrize("P", [2, 8])
+def test_xgmi_probe_local_group(P):
+    """The calibration probe on an in-process group (every 'peer' is this GPU): every pattern runs, all
+    ranks at once, and reports a rate."""
+    import threading
+    g = group(P)
+    res = [None] * P
+
+    def run(r):
+        res[r] = g[r].xgmi_probe(1 << 20, iters=3)
+    th = [threading.Thread(target=run, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    for r in range(P):
+        assert res[r] is not None and all(v > 0 for v in res[r].values()), (r, res[r])
+
+
+def test_peer_write_in_place_and_out_of_place_repeats():
+    """Write form: repeated calls reuse the slots and final areas with two barriers per call."""
+    P, n = 8, 123_457
+    ins = [fi.fill("f32", 13, r, n) for r in range(P)]
+    for oop in (False, True):
+        outs = run_peer(ins, "2,4", outofplace=oop, repeat=3, mode="write")
+        exp = ins
+        for _ in range(3):
+            exp = oracle_lib.allreduce(exp, "2,4")
+        for r in range(P):
+            assert outs[r].tobytes() == exp[r].tobytes(), (oop, r)
