@@ -203,7 +203,7 @@ def bench_distributed(a):
          IPC peer forms (read, write) last, inside a time budget every rank agrees on;
       3. the sweep's best, re-timed for exactly K steps after W warmup, if it beats the default;
       4. RCCL's own ncclAllReduce on the same bucket (yardstick).
-    A watchdog (FTAR_BENCH_BUDGET_S, default 540 s) prints the best line measured so far and ends every
+    A watchdog (FTAR_BENCH_BUDGET_S, default 300 s) prints the best line measured so far and ends every
     rank if anything hangs."""
     import threading
 
@@ -216,8 +216,8 @@ def bench_distributed(a):
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     t_start = time.time()
-    budget = float(os.environ.get("FTAR_BENCH_BUDGET_S", "540"))
-    sweep_budget = float(os.environ.get("FTAR_BENCH_SWEEP_S", "240"))
+    budget = float(os.environ.get("FTAR_BENCH_BUDGET_S", "300"))
+    sweep_budget = float(os.environ.get("FTAR_BENCH_SWEEP_S", "150"))
     state = {"line": None, "printed": False, "done": False, "phase": "init"}
     lock = threading.Lock()
 
