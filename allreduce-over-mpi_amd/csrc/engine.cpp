@@ -19,6 +19,8 @@
 // is stream-ordered like any other HIP operation.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <cstdio>
 #include <initializer_list>
 #include <map>
 #include <mutex>
@@ -47,6 +49,12 @@ struct ftar_comm {
   ftar::Topology topo;
   std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
   std::vector<hipEvent_t> events;
+  // phase timing (diagnostic, ftar_comm_set_phase_timing): timing events
+  // recorded at the phase boundaries of the last call, in issue order
+  bool phase_timing = false;
+  std::vector<hipEvent_t> tev;
+  std::vector<std::string> tnames;
+  size_t nmarks = 0;
   std::mutex mu;
 };
 
@@ -61,6 +69,20 @@ constexpr size_t kDefaultChunkBytes = 16u << 20;
 // (profiles/r01/host/): 8 pieces per block at P = 8 x 1 GiB.
 constexpr size_t kDefaultHostChunkBytes = 0;
 size_t auto_host_chunk(size_t split_bytes) { return std::max<size_t>(16u << 20, split_bytes / 64); }
+
+// phase timing: one timing event per boundary, on the stream that reaches it
+ftar_status_t mark(ftar_comm* c, const std::string& name, hipStream_t s) {
+  if (!c->phase_timing) return FTAR_SUCCESS;
+  if (c->nmarks == c->tev.size()) {
+    hipEvent_t e;
+    FTAR_CHECK_HIP(hipEventCreate(&e));
+    c->tev.push_back(e);
+    c->tnames.emplace_back();
+  }
+  c->tnames[c->nmarks] = name;
+  FTAR_CHECK_HIP(hipEventRecord(c->tev[c->nmarks++], s));
+  return FTAR_SUCCESS;
+}
 
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
   while (c->events.size() < n) {
@@ -112,6 +134,7 @@ void comm_teardown(ftar_comm* c) {
   if (c->xbuf) (void)hipFree(c->xbuf);
   c->tp.reset();
   for (auto e : c->events) (void)hipEventDestroy(e);
+  for (auto e : c->tev) (void)hipEventDestroy(e);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->staging) (void)hipFree(c->staging);
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
@@ -213,38 +236,52 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
   hipEvent_t* ev = c->events.data();
   FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
+  c->nmarks = 0;
+  FTAR_RETURN_IF(mark(c, "start", c->comm_s));
   std::vector<Segment> segs;
   if (!write) {
     FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
+    FTAR_RETURN_IF(mark(c, "copy-in", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const ReduceItem& r : rs.reduces)
       FTAR_RETURN_IF(peer_fold(r, plan, dt, op, X + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
         return q < 0 ? X + off * esz : Xq[q] + off * esz;  // that rank's copy of this block
       }));
+    FTAR_RETURN_IF(mark(c, "fold (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     // all-gather: every owner's final block from its exchange buffer, one launch
     for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, out + r.off * esz, r.len * esz});
     for (const Transfer& x : ag.recvs) segs.push_back({Xq[x.peer] + x.off * esz, out + x.off * esz, x.len * esz});
     FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   } else {
     // scatter my copy of every peer's block into its slot for me, all links at once
     for (const Transfer& x : rs.sends)
       segs.push_back({in + x.off * esz, Xq[x.peer] + (size_t)c->rank * slot_bytes, x.len * esz});
     FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(mark(c, "scatter (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const ReduceItem& r : rs.reduces)
       FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
         return q < 0 ? in + off * esz : X + (size_t)q * slot_bytes;  // rank q's copy, pushed into slot q
       }));
+    FTAR_RETURN_IF(mark(c, "fold (local)", c->comm_s));
     segs.clear();  // my final block into every peer's final area
     for (const Transfer& x : ag.sends) segs.push_back({out + x.off * esz, Xq[x.peer] + final_at + x.off * esz,
                                                        x.len * esz});
     FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(mark(c, "push (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     segs.clear();
     for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
     FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
   }
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
@@ -494,6 +531,8 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[0], 0));
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev[0], 0));
+  c->nmarks = 0;
+  FTAR_RETURN_IF(mark(c, "start", c->comm_s));
   if (host) {  // all pieces in, in order, on their own stream (the DMA engines run ahead)
     FTAR_CHECK_HIP(hipStreamWaitEvent(c->h2d_s, ev[0], 0));
     FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev[0], 0));
@@ -553,6 +592,10 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
       }
       FTAR_CHECK_HIP(hipEventRecord(ev_r(s, k), c->red_s));
     }
+    if (c->phase_timing && !skew && k == nchunks - 1) {  // stage-major: the stage's last piece
+      if (moves[s]) FTAR_RETURN_IF(mark(c, "stage " + std::to_string(s) + " moved", c->comm_s));
+      if (reduces[s]) FTAR_RETURN_IF(mark(c, "stage " + std::to_string(s) + " reduced", c->red_s));
+    }
     if (host && s == nst - 1) {  // piece k is final everywhere: out over PCIe while later pieces come in
       FTAR_CHECK_HIP(hipEventRecord(ev_d(k), reduces[s] ? c->red_s : c->comm_s));
       if (reduces[s]) FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_x(s, k), 0));
@@ -572,6 +615,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(tp->allgather(bufs[BUF_DST] + (size_t)c->rank * plan.split * esz, bufs[BUF_DST], plan.split * esz,
                                  c->rank, c->nranks, c->comm_s));
   }
+  if (plan.allgather == FTAR_AG_COLLECTIVE) FTAR_RETURN_IF(mark(c, "collective all-gather", c->comm_s));
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipEventRecord(ev[2], c->red_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
@@ -754,6 +798,39 @@ ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode) {
   if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
   *mode = comm->peer_direct;
   return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_set_phase_timing(ftar_comm_t comm, int enable) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->phase_timing = enable != 0;
+  comm->nmarks = 0;
+  return FTAR_SUCCESS;
+}
+
+long ftar_comm_phase_json(ftar_comm_t comm, char* buf, size_t buflen) {
+  if (!comm) return -FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  std::string j = "[";
+  if (comm->nmarks) {
+    if (hipSetDevice(comm->device) != hipSuccess) return -FTAR_ERR_HIP;
+    for (size_t i = 0; i < comm->nmarks; ++i)
+      if (hipEventSynchronize(comm->tev[i]) != hipSuccess) return -FTAR_ERR_HIP;
+    for (size_t i = 0; i < comm->nmarks; ++i) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, comm->tev[0], comm->tev[i]) != hipSuccess) return -FTAR_ERR_HIP;
+      char item[160];
+      snprintf(item, sizeof item, "%s[\"%s\", %.4f]", i ? ", " : "", comm->tnames[i].c_str(), (double)ms);
+      j += item;
+    }
+  }
+  j += "]";
+  if (buf && buflen) {
+    const size_t m = std::min(buflen - 1, j.size());
+    memcpy(buf, j.data(), m);
+    buf[m] = 0;
+  }
+  return (long)j.size();
 }
 
 ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters, double* gbps, int n) {

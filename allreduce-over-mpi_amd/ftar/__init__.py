@@ -111,6 +111,9 @@ _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_
 _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
+_lib.ftar_comm_set_phase_timing.argtypes = [_vp, _int]
+_lib.ftar_comm_phase_json.argtypes = [_vp, ctypes.c_char_p, _sz]
+_lib.ftar_comm_phase_json.restype = ctypes.c_long
 PEER_MODE = {"off": 0, "read": 1, "write": 2}                # ftar_peer_mode_t
 
 
@@ -348,6 +351,19 @@ class Comm:
     @peer_direct.setter
     def peer_direct(self, mode):
         _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
+
+    def phase_timing(self, on=True):
+        """Record timing events at the phase boundaries of every following call (diagnostic)."""
+        _check(_lib.ftar_comm_set_phase_timing(self.handle, 1 if on else 0), "phase_timing")
+
+    def last_phases(self):
+        """[(phase, ms since the call's start), ...] of the last call made with phase timing on (waits for it)."""
+        n = _lib.ftar_comm_phase_json(self.handle, None, 0)
+        if n < 0:
+            raise FtarError(-n, "ftar_comm_phase_json")
+        buf = ctypes.create_string_buffer(n + 1)
+        _lib.ftar_comm_phase_json(self.handle, buf, n + 1)
+        return [tuple(p) for p in json.loads(buf.value.decode())]
 
     def xgmi_probe(self, bytes_per_peer=64 << 20, iters=10):
         """Collective xGMI calibration (ftar_xgmi_probe): GB/s of copy kernels through the exchange buffers,

@@ -443,6 +443,29 @@ def bench_distributed(a):
     else:
         state["line"]["config_selection"] = "default (fastest validated configuration)"
 
+    # phase timelines (rank 0's view) of the default and of the fastest validated configuration of each form:
+    # where a call's time goes (transfer rounds vs folds vs barriers), for the next round's tuning
+    state["phase"] = "phase timing"
+    try:
+        fam_best = {}
+        for r in ok_runs:
+            if r["form"] not in fam_best or r["ms"] < fam_best[r["form"]]["ms"]:
+                fam_best[r["form"]] = r
+        configs = [("default", default_topo, default_chunk, "direct")] + [
+            (f"best {fam}", ftar.topo("1" if r["topology"] == "ring" else r["topology"]), r["chunk_bytes"], fam)
+            for fam, r in sorted(fam_best.items())]
+        phases = {}
+        comm.phase_timing(True)
+        for label, t, ch, form in configs:
+            fn = run_with(t, ch, form)
+            fn()
+            torch.cuda.synchronize()
+            phases[label] = {"topology": str(t), "chunk_bytes": ch, "form": form, "phases_ms": comm.last_phases()}
+        comm.phase_timing(False)
+        state["line"]["phases_rank0"] = phases
+    except Exception as e:  # noqa: BLE001
+        state["line"]["phases_rank0"] = {"error": str(e)[:200]}
+
     # 4. RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
     state["phase"] = "rccl yardstick"
     try:

@@ -237,6 +237,14 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
  * one peer, [4] write to all peers at once (aggregate).  bytes_per_peer per
  * copy, `iters` timed launches; grows the exchange buffer to 2*P*bytes. */
 ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters, double* gbps, int n);
+/* Phase timing of the last call on this communicator (diagnostic; off by
+ * default): timing events at the phase boundaries -- per stage "moved" (comm
+ * stream) and "reduced" (reduce stream) for the p2p executor in device mode,
+ * every copy/fold/barrier for the peer forms.  ftar_comm_phase_json waits for
+ * them and writes [["start", 0.0], [name, ms since start], ...]; returns the
+ * needed length or < 0 on error. */
+ftar_status_t ftar_comm_set_phase_timing(ftar_comm_t comm, int enable);
+long ftar_comm_phase_json(ftar_comm_t comm, char* buf, size_t buflen);
 
 /* ---- introspection (tests) -------------------------------------------------
  * FMA-level schedule of `rank` (same JSON shape as the reference dump in

@@ -224,3 +224,35 @@ def test_peer_write_in_place_and_out_of_place_repeats():
             exp = oracle_lib.allreduce(exp, "2,4")
         for r in range(P):
             assert outs[r].tobytes() == exp[r].tobytes(), (oop, r)
+
+
+@pytest.mark.parametrize("mode,topo,names", [
+    (0, "2,2", ["start", "stage 0 moved", "stage 0 reduced", "stage 1 moved"]),
+    ("read", "2,2", ["start", "copy-in", "barrier", "fold (remote reads)", "barrier", "gather (remote reads)",
+                     "barrier"]),
+    ("write", "4", ["start", "scatter (remote writes)", "barrier", "fold (local)", "push (remote writes)",
+                    "barrier", "copy-out"])])
+def test_phase_timing(mode, topo, names):
+    """ftar_comm_set_phase_timing / ftar_comm_phase_json: the phases of the last call, in issue order."""
+    import threading
+    P, n = 4, 1 << 20
+    g = group(P)
+    ins = [fi.fill("f32", 14, r, n) for r in range(P)]
+    ref = oracle_lib.allreduce(ins, topo)
+    for c in g.comms:
+        c.phase_timing(True)
+    try:
+        outs = run_peer(ins, topo, mode=mode)
+        got = [None] * P
+        th = [threading.Thread(target=lambda r=r: got.__setitem__(r, g[r].last_phases())) for r in range(P)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=60)
+    finally:
+        for c in g.comms:
+            c.phase_timing(False)
+    assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P))
+    for r in range(P):
+        assert [p[0] for p in got[r]] == names, got[r]
+        assert got[r][0][1] == 0.0 and all(ms >= 0 for _, ms in got[r]), got[r]
