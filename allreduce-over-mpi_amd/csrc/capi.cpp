@@ -10,6 +10,7 @@
 #include <mutex>
 #include <sstream>
 
+#include <map>
 #include "ftar_internal.h"
 
 namespace ftar {
@@ -318,25 +319,45 @@ long ftar_plan_json(const ftar_topo_t* topo, int nranks, int rank, size_t count,
 // same device and reduces through the mapping, as RcclTransport::map_peers does
 // across devices.
 // ---------------------------------------------------------------------------
-extern "C" ftar_status_t ftar_debug_ipc_handle(const void* base, void* handle64) {
-  if (!base || !handle64) return FTAR_ERR_INVALID_ARG;
-  hipIpcMemHandle_t h;
-  FTAR_CHECK_HIP(hipIpcGetMemHandle(&h, const_cast<void*>(base)));
-  static_assert(sizeof h == 64, "IPC handle size");
-  memcpy(handle64, &h, sizeof h);
+// The reference is ftar::IpcRef (128 bytes): allocation handle + offset, so a
+// pointer anywhere inside an allocation (a registered tensor) maps correctly.
+namespace {
+std::mutex g_dbg_mu;
+std::map<void*, void*> g_dbg_bases;  // pointer handed out -> mapped allocation
+}  // namespace
+
+extern "C" ftar_status_t ftar_debug_ipc_handle(const void* ptr, void* ref128) {
+  if (!ptr || !ref128) return FTAR_ERR_INVALID_ARG;
+  ftar::IpcRef r;
+  FTAR_RETURN_IF(ftar::ipc_export(ptr, &r));
+  memcpy(ref128, &r, sizeof r);
   return FTAR_SUCCESS;
 }
 
-extern "C" ftar_status_t ftar_debug_ipc_open(const void* handle64, void** ptr) {
-  if (!handle64 || !ptr) return FTAR_ERR_INVALID_ARG;
-  hipIpcMemHandle_t h;
-  memcpy(&h, handle64, sizeof h);
-  FTAR_CHECK_HIP(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+extern "C" ftar_status_t ftar_debug_ipc_open(const void* ref128, void** ptr) {
+  if (!ref128 || !ptr) return FTAR_ERR_INVALID_ARG;
+  ftar::IpcRef r;
+  memcpy(&r, ref128, sizeof r);
+  void* base = nullptr;
+  char* p = nullptr;
+  FTAR_RETURN_IF(ftar::ipc_import(r, &base, &p));
+  std::lock_guard<std::mutex> g(g_dbg_mu);
+  g_dbg_bases[p] = base;
+  *ptr = p;
   return FTAR_SUCCESS;
 }
 
 extern "C" ftar_status_t ftar_debug_ipc_close(void* ptr) {
   if (!ptr) return FTAR_ERR_INVALID_ARG;
-  FTAR_CHECK_HIP(hipIpcCloseMemHandle(ptr));
+  void* base = ptr;
+  {
+    std::lock_guard<std::mutex> g(g_dbg_mu);
+    auto it = g_dbg_bases.find(ptr);
+    if (it != g_dbg_bases.end()) {
+      base = it->second;
+      g_dbg_bases.erase(it);
+    }
+  }
+  FTAR_CHECK_HIP(hipIpcCloseMemHandle(base));
   return FTAR_SUCCESS;
 }

@@ -43,6 +43,15 @@ struct ftar_comm {
   void* xbuf = nullptr;            // peer-direct exchange buffer (IPC-exported), grow-only
   size_t xbuf_bytes = 0;
   std::vector<char*> xpeers;       // every rank's exchange buffer, mapped here
+  // registered user buffers (ftar_comm_register): id -> my range + every rank's
+  // matching pointer, mapped here; the peer forms read/write them in place
+  struct Reg {
+    char* ptr;
+    size_t bytes;
+    std::vector<char*> peers;
+  };
+  std::map<int, Reg> regs;
+  int next_reg = 1;
   bool auto_topo = true;
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
@@ -130,7 +139,11 @@ void comm_teardown(ftar_comm* c) {
   (void)hipSetDevice(c->device);
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) (void)hipStreamSynchronize(st);
-  if (c->tp) c->tp->unmap_peers(&c->xpeers, c->rank);
+  if (c->tp) {
+    c->tp->unmap_peers(&c->xpeers, c->rank);
+    for (auto& r : c->regs) c->tp->unmap_peers(&r.second.peers, c->rank);
+  }
+  c->regs.clear();
   if (c->xbuf) (void)hipFree(c->xbuf);
   c->tp.reset();
   for (auto e : c->events) (void)hipEventDestroy(e);
@@ -220,16 +233,36 @@ ftar_status_t peer_fold(const ReduceItem& r, const Plan& plan, ftar_dtype_t dt, 
 }
 }  // namespace
 
+namespace {
+// the registration holding [p, p+bytes), or null
+const ftar_comm::Reg* find_reg(const ftar_comm* c, const void* p, size_t bytes) {
+  const char* q = static_cast<const char*>(p);
+  for (const auto& r : c->regs)
+    if (q >= r.second.ptr && q + bytes <= r.second.ptr + r.second.bytes) return &r.second;
+  return nullptr;
+}
+// rank `peer`'s buffer at the same offset into its registration as p into mine
+char* reg_peer(const ftar_comm::Reg* r, const void* p, int peer) {
+  return r->peers[peer] + (static_cast<const char*>(p) - r->ptr);
+}
+}  // namespace
+
 ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                              const Plan& plan, ftar_comm* c, hipStream_t stream) {
   const size_t esz = dtype_size(dt), bytes = count * esz;
   const bool write = c->peer_direct == FTAR_PEER_WRITE;
   const size_t slot_bytes = plan.split * esz, final_at = (size_t)plan.nranks * slot_bytes;
-  FTAR_RETURN_IF(ensure_xbuf(c, write ? final_at + bytes : bytes));
-  Transport* tp = c->tp.get();
-  char* X = static_cast<char*>(c->xbuf);
   char* out = static_cast<char*>(recvbuf);
   const char* in = static_cast<const char*>(sendbuf ? sendbuf : recvbuf);
+  // registered buffers (every rank's, at the same offsets): no local pass --
+  // read: peers' inputs and outputs are read in place; write: final blocks are
+  // pushed straight into the peers' outputs
+  const ftar_comm::Reg* rin = find_reg(c, in, bytes);
+  const ftar_comm::Reg* rout = find_reg(c, out, bytes);
+  const bool zc = write ? rout != nullptr : (rin != nullptr && rout != nullptr);
+  FTAR_RETURN_IF(ensure_xbuf(c, write ? final_at + (zc ? 0 : bytes) : (zc ? 256 : bytes)));
+  Transport* tp = c->tp.get();
+  char* X = static_cast<char*>(c->xbuf);
   const std::vector<char*>& Xq = c->xpeers;
   const Stage& rs = plan.stages[0];
   const Stage& ag = plan.stages[1];
@@ -239,7 +272,23 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
   c->nmarks = 0;
   FTAR_RETURN_IF(mark(c, "start", c->comm_s));
   std::vector<Segment> segs;
-  if (!write) {
+  if (!write && zc) {
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));  // every rank's input is ready
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
+    for (const ReduceItem& r : rs.reduces)
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+        return q < 0 ? in + off * esz : reg_peer(rin, in, q) + off * esz;  // that rank's input, in place
+      }));
+    FTAR_RETURN_IF(mark(c, "fold (remote reads)", c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
+    for (const Transfer& x : ag.recvs)
+      segs.push_back({reg_peer(rout, out, x.peer) + x.off * esz, out + x.off * esz, x.len * esz});
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my buffers after the call
+    FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
+  } else if (!write) {
     FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
     FTAR_RETURN_IF(mark(c, "copy-in", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
@@ -271,17 +320,20 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
         return q < 0 ? in + off * esz : X + (size_t)q * slot_bytes;  // rank q's copy, pushed into slot q
       }));
     FTAR_RETURN_IF(mark(c, "fold (local)", c->comm_s));
-    segs.clear();  // my final block into every peer's final area
-    for (const Transfer& x : ag.sends) segs.push_back({out + x.off * esz, Xq[x.peer] + final_at + x.off * esz,
-                                                       x.len * esz});
+    segs.clear();  // my final block into every peer's final area, or straight into its registered output
+    for (const Transfer& x : ag.sends)
+      segs.push_back({out + x.off * esz, (zc ? reg_peer(rout, out, x.peer) : Xq[x.peer] + final_at) + x.off * esz,
+                      x.len * esz});
     FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
     FTAR_RETURN_IF(mark(c, "push (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
-    segs.clear();
-    for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
-    FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
+    if (!zc) {
+      segs.clear();
+      for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
+      FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+      FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
+    }
   }
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
@@ -797,6 +849,30 @@ ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode) {
 ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode) {
   if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
   *mode = comm->peer_direct;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_register(ftar_comm_t comm, void* buf, size_t bytes, int* reg) {
+  if (!comm || !buf || !bytes || !reg) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  ftar_comm::Reg r{static_cast<char*>(buf), bytes, {}};
+  FTAR_RETURN_IF(comm->tp->map_peers(buf, comm->rank, comm->nranks, &r.peers));
+  *reg = comm->next_reg++;
+  comm->regs.emplace(*reg, std::move(r));
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  auto it = comm->regs.find(reg);
+  if (it == comm->regs.end()) return FTAR_ERR_INVALID_ARG;
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  FTAR_CHECK_HIP(hipStreamSynchronize(comm->comm_s));  // its last call ended in a barrier: no peer touches it
+  FTAR_CHECK_HIP(hipStreamSynchronize(comm->red_s));
+  comm->tp->unmap_peers(&it->second.peers, comm->rank);
+  comm->regs.erase(it);
   return FTAR_SUCCESS;
 }
 

@@ -143,9 +143,10 @@ class Transport {
   }
   // Peer-direct mode (engine.cpp peer_allreduce).  barrier: stream-ordered,
   // work after it on `s` starts once every rank's stream reached it.
-  // map_peers: collective and host-blocking; every rank passes the base of a
-  // hipMalloc allocation and gets every rank's base as a pointer usable by
-  // kernels on its own device (peers[rank] == mine).  unmap_peers undoes it.
+  // map_peers: collective and host-blocking; every rank passes a pointer into
+  // device memory (any offset into a hipMalloc allocation) and gets every
+  // rank's pointer as an address usable by kernels on its own device
+  // (peers[rank] == mine).  unmap_peers undoes it.
   virtual ftar_status_t barrier(hipStream_t s) = 0;
   virtual ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) = 0;
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
@@ -156,6 +157,18 @@ class Transport {
     return FTAR_ERR_UNSUPPORTED;
   }
 };
+
+// IPC reference to any device pointer: the handle of its allocation plus the
+// pointer's offset in it (dmabuf IPC exports whole allocations).
+struct IpcRef {
+  hipIpcMemHandle_t handle;
+  uint64_t offset;
+  uint64_t pad[7];
+};
+static_assert(sizeof(IpcRef) == 128, "IpcRef layout");
+ftar_status_t ipc_export(const void* p, IpcRef* out);
+// opens ref; *base = the mapped allocation (for hipIpcCloseMemHandle), *p = base + offset
+ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p);
 
 std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_t& id, int rank,
                                                ftar_status_t* st);

@@ -29,6 +29,22 @@
 
 namespace ftar {
 
+ftar_status_t ipc_export(const void* p, IpcRef* out) {
+  memset(out, 0, sizeof *out);
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  FTAR_CHECK_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)));
+  out->offset = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<const char*>(base));
+  FTAR_CHECK_HIP(hipIpcGetMemHandle(&out->handle, base));
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p) {
+  FTAR_CHECK_HIP(hipIpcOpenMemHandle(base, ref.handle, hipIpcMemLazyEnablePeerAccess));
+  *p = static_cast<char*>(*base) + ref.offset;
+  return FTAR_SUCCESS;
+}
+
 // ---------------------------------------------------------------------------
 // RCCL
 // ---------------------------------------------------------------------------
@@ -57,20 +73,21 @@ class RcclTransport final : public Transport {
     FTAR_CHECK_NCCL(ncclAllReduce(scratch_, scratch_, 1, ncclInt32, ncclSum, comm_, s));
     return FTAR_SUCCESS;
   }
-  // IPC handles of every rank's allocation, all-gathered over RCCL, opened here
-  // (dmabuf IPC; peer access enabled lazily by the runtime)
+  // IPC references (allocation handle + offset) of every rank's pointer,
+  // all-gathered over RCCL, opened here (dmabuf IPC; peer access enabled
+  // lazily by the runtime)
   ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
     FTAR_RETURN_IF(ensure_scratch());
-    hipIpcMemHandle_t h;
-    FTAR_CHECK_HIP(hipIpcGetMemHandle(&h, mine));
-    std::vector<hipIpcMemHandle_t> all(nranks);
-    char* dev = static_cast<char*>(scratch_) + 256;  // nranks handles after the barrier word
+    IpcRef ref;
+    FTAR_RETURN_IF(ipc_export(mine, &ref));
+    std::vector<IpcRef> all(nranks);
+    char* dev = static_cast<char*>(scratch_) + 256;  // nranks refs after the barrier and agreement words
     hipStream_t s;
     FTAR_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     ftar_status_t st = FTAR_SUCCESS;
-    if (hipMemcpyAsync(dev + (size_t)rank * sizeof h, &h, sizeof h, hipMemcpyHostToDevice, s) != hipSuccess ||
-        ncclAllGather(dev + (size_t)rank * sizeof h, dev, sizeof h, ncclUint8, comm_, s) != ncclSuccess ||
-        hipMemcpyAsync(all.data(), dev, (size_t)nranks * sizeof h, hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemcpyAsync(dev + (size_t)rank * sizeof ref, &ref, sizeof ref, hipMemcpyHostToDevice, s) != hipSuccess ||
+        ncclAllGather(dev + (size_t)rank * sizeof ref, dev, sizeof ref, ncclUint8, comm_, s) != ncclSuccess ||
+        hipMemcpyAsync(all.data(), dev, (size_t)nranks * sizeof ref, hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
       set_error("peer map: handle exchange failed", __FILE__, __LINE__);
       st = FTAR_ERR_RCCL;
@@ -84,12 +101,22 @@ class RcclTransport final : public Transport {
         (*peers)[q] = static_cast<char*>(mine);
         continue;
       }
-      void* p = nullptr;
-      hipError_t e = hipIpcOpenMemHandle(&p, all[q], hipIpcMemLazyEnablePeerAccess);
-      if (e != hipSuccess)
-        why = std::string("hipIpcOpenMemHandle(rank ") + std::to_string(q) + "): " + hipGetErrorString(e);
-      else
-        (*peers)[q] = static_cast<char*>(p);
+      // one mapping per peer allocation (two registered buffers may share one),
+      // reference-counted by the pointers handed out
+      const std::string key(reinterpret_cast<const char*>(&all[q].handle), sizeof all[q].handle);
+      auto it = imports_.find(key);
+      if (it == imports_.end()) {
+        void* base = nullptr;
+        char* p = nullptr;
+        if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
+          why = std::string("rank ") + std::to_string(q) + ": " + last_error();
+          break;
+        }
+        it = imports_.emplace(key, Import{base, 0}).first;
+      }
+      ++it->second.refs;
+      (*peers)[q] = static_cast<char*>(it->second.base) + all[q].offset;
+      handed_.emplace((*peers)[q], key);
     }
     // every rank learns whether every rank mapped every peer: a rank that
     // failed alone would otherwise leave the others waiting in the next barrier
@@ -104,8 +131,17 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   void unmap_peers(std::vector<char*>* peers, int rank) override {
-    for (int q = 0; q < (int)peers->size(); ++q)
-      if (q != rank && (*peers)[q]) (void)hipIpcCloseMemHandle((*peers)[q]);
+    for (int q = 0; q < (int)peers->size(); ++q) {
+      if (q == rank || !(*peers)[q]) continue;
+      auto h = handed_.find((*peers)[q]);
+      if (h == handed_.end()) continue;
+      auto it = imports_.find(h->second);
+      handed_.erase(h);
+      if (it != imports_.end() && --it->second.refs == 0) {
+        (void)hipIpcCloseMemHandle(it->second.base);
+        imports_.erase(it);
+      }
+    }
     peers->clear();
   }
   ftar_status_t group_start() override {
@@ -166,12 +202,18 @@ class RcclTransport final : public Transport {
     }
     return FTAR_SUCCESS;
   }
-  ftar_status_t ensure_scratch() {  // barrier word + FTAR_MAX_K IPC handles
-    if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)FTAR_MAX_K * sizeof(hipIpcMemHandle_t)));
+  ftar_status_t ensure_scratch() {  // barrier word, agreement word, FTAR_MAX_K IPC references
+    if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)FTAR_MAX_K * sizeof(IpcRef)));
     return FTAR_SUCCESS;
   }
   ncclComm_t comm_;
   void* scratch_ = nullptr;
+  struct Import {
+    void* base;
+    int refs;
+  };
+  std::map<std::string, Import> imports_;         // peer allocation (IPC handle bytes) -> its mapping here
+  std::multimap<char*, std::string> handed_;      // peer pointer handed out -> its allocation
 };
 
 }  // namespace

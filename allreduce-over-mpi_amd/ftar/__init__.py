@@ -112,6 +112,8 @@ _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_comm_set_phase_timing.argtypes = [_vp, _int]
+_lib.ftar_comm_register.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_int)]
+_lib.ftar_comm_deregister.argtypes = [_vp, _int]
 _lib.ftar_comm_phase_json.argtypes = [_vp, ctypes.c_char_p, _sz]
 _lib.ftar_comm_phase_json.restype = ctypes.c_long
 PEER_MODE = {"off": 0, "read": 1, "write": 2}                # ftar_peer_mode_t
@@ -352,6 +354,16 @@ class Comm:
     def peer_direct(self, mode):
         _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
 
+    def register(self, buf, nbytes):
+        """Collective: register this rank's buffer (device pointer or tensor) for the peer forms' in-place
+        paths (ftar_comm_register); returns the registration id (the same on every rank)."""
+        r = _int()
+        _check(_lib.ftar_comm_register(self.handle, _ptr(buf), nbytes, ctypes.byref(r)), "ftar_comm_register")
+        return r.value
+
+    def deregister(self, reg):
+        _check(_lib.ftar_comm_deregister(self.handle, reg), "ftar_comm_deregister")
+
     def phase_timing(self, on=True):
         """Record timing events at the phase boundaries of every following call (diagnostic)."""
         _check(_lib.ftar_comm_set_phase_timing(self.handle, 1 if on else 0), "phase_timing")
@@ -465,6 +477,29 @@ class LocalGroup:
     def set_reduce_scatter(self, mode):
         for c in self.comms:
             c.reduce_scatter = mode
+
+    def register(self, bufs, nbytes):
+        """Register one buffer per rank (collective: one host thread per rank); returns the ids."""
+        import threading
+        ids, errs = [None] * len(self.comms), []
+
+        def run(r):
+            try:
+                ids[r] = self.comms[r].register(bufs[r], nbytes)
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        th = [threading.Thread(target=run, args=(r,)) for r in range(len(self.comms))]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return ids
+
+    def deregister(self, ids):
+        for c, i in zip(self.comms, ids):
+            c.deregister(i)
 
     def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None,
                   host=False):

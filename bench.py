@@ -276,12 +276,30 @@ def bench_distributed(a):
     def run_with(topo, chunk, form="direct"):
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
         rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
-        kernel loads / stores through IPC-mapped exchange buffers)."""
+        kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
+        no local pass)."""
         comm.chunk_bytes = chunk
-        comm.peer_direct = form[len("peer-"):] if form.startswith("peer-") else 0
-        comm.allgather = "direct" if form.startswith("peer-") else form
+        peer = form.startswith("peer-")
+        comm.peer_direct = form.split("-")[1] if peer else 0
+        comm.allgather = "direct" if peer else form
         comm.reduce_scatter = "stages" if form == "stages" else "direct"
-        return lambda: comm.allreduce(x, y, n, a.dtype, "sum", topo_=topo, stream=stream)
+        xin, yout = (reg_bufs() if form.endswith("-reg") else (x, y))
+
+        def fn():
+            comm.allreduce(xin, yout, n, a.dtype, "sum", topo_=topo, stream=stream)
+        fn.xin, fn.yout = xin, yout
+        return fn
+
+    reg = {}
+
+    def reg_bufs():
+        """x and y copies registered with the communicator (ftar_comm_register, collective, once): the peer
+        forms then read / write the peers' buffers in place, with no local pass."""
+        if not reg:
+            reg["x"], reg["y"] = x.clone(), torch.empty_like(y)
+            torch.cuda.synchronize()
+            reg["ids"] = [comm.register(reg["x"], bucket), comm.register(reg["y"], bucket)]
+        return reg["x"], reg["y"]
 
     # correctness of y: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
     idx = torch.linspace(0, n - 1, 4096, device=dev).long()
@@ -297,6 +315,7 @@ def bench_distributed(a):
         """y (from the timed calls) against the fp64 sample and across ranks; then one more call on the
         negated inputs must give exactly -y everywhere (round-to-nearest-even is sign-symmetric), which
         proves the call read this call's data (no stale copies) over the whole bucket."""
+        x, y = fn.xin, fn.yout
         torch.cuda.synchronize()
         mine = y[idx].float().cpu()
         ally = [torch.empty_like(mine) for _ in range(world)]
@@ -384,7 +403,7 @@ def bench_distributed(a):
                 chunks = {default_chunk}  # the reference's ring rounds: one point is enough
             plan += [(t, chunk, form) for chunk in sorted(chunks)]
         if not a.no_peer and t.lonely == 0:  # no pieces: whole-block kernels
-            plan += [(t, default_chunk, "peer-read"), (t, default_chunk, "peer-write")]
+            plan += [(t, default_chunk, f) for f in ("peer-read", "peer-write", "peer-read-reg", "peer-write-reg")]
     plan.sort(key=lambda p: p[2].startswith("peer-"))  # stable: every RCCL configuration before any peer one
     sweep_t0 = time.time()
     probed = False
@@ -480,6 +499,8 @@ def bench_distributed(a):
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
     state["done"] = True
+    for i in reg.get("ids", []):
+        comm.deregister(i)
     comm.destroy()
     dist.destroy_process_group()
 

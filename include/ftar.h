@@ -191,6 +191,18 @@ ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter
 typedef enum { FTAR_PEER_OFF = 0, FTAR_PEER_READ = 1, FTAR_PEER_WRITE = 2 } ftar_peer_mode_t;
 ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode);
 ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode);
+/* Registered (symmetric) buffers for the peer forms, like RCCL's user-buffer
+ * registration.  Collective: every rank registers its own buffer of the same
+ * role in the same call order; *reg is the same id on every rank.  A call
+ * whose buffers lie in registrations -- on EVERY rank, at the SAME offsets
+ * -- skips the peer forms' local pass: READ (sendbuf and recvbuf registered)
+ * reads the peers' inputs and final blocks in place, three barriers, no
+ * copy; WRITE (recvbuf registered) pushes final blocks straight into the
+ * peers' outputs, two barriers, no copy.  Mixing registered and unregistered
+ * buffers across ranks in one call is undefined.  deregister is local; the
+ * buffer must not be freed before it (or before the calls using it ended). */
+ftar_status_t ftar_comm_register(ftar_comm_t comm, void* buf, size_t bytes, int* reg);
+ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg);
 
 /* ---- AllReduce (device resident) -------------------------------------------
  * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the

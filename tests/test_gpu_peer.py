@@ -32,15 +32,22 @@ def group(P):
     return _groups[P]
 
 
-def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", rs="direct", repeat=1, mode="read"):
+def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", rs="direct", repeat=1, mode="read",
+             registered=False):
     g = group(len(ins))
     g.set_peer_direct(mode)
     g.set_allgather(ag)
     g.set_reduce_scatter(rs)
+    regs = []
     try:
         n = ins[0].size
         send = [to_dev(x) for x in ins]
         recv = [filled_dev(x.nbytes) for x in ins] if outofplace else send
+        if registered:   # every rank's send and recv buffers: the in-place (no local pass) paths
+            nb = max(1, ins[0].nbytes)
+            regs.append(g.register([p for _, p in send], nb))
+            if outofplace:
+                regs.append(g.register([p for _, p in recv], nb))
         for it in range(repeat):
             sb = [p for _, p in send] if outofplace else None
             g.allreduce(sb, [p for _, p in recv], n, dtype, op, topo_=topo, lonely=lonely)
@@ -48,6 +55,8 @@ def run_peer(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, ag="direct", 
                 send, recv = recv, send
         return [from_dev(t, ins[0].dtype, n) for t, _ in recv]
     finally:
+        for ids in regs:
+            g.deregister(ids)
         g.set_peer_direct(False)
 
 
@@ -118,12 +127,14 @@ def _ipc_owner(n, q_handle, q_done):
     lib = ftar.lib()
     p = ctypes.c_void_p()
     assert hip.hipSetDevice(0) == 0
-    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n * 4)) == 0
+    inner = 4112   # export a pointer INSIDE the allocation (a registered tensor): handle + offset
+    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(n * 4 + inner)) == 0
     x = fi.fill("f32", 12, 0, n)
-    assert hip.hipMemcpy(p, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n * 4), 1) == 0   # H2D
-    h = ctypes.create_string_buffer(64)
+    px = ctypes.c_void_p(p.value + inner)
+    assert hip.hipMemcpy(px, x.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(n * 4), 1) == 0   # H2D
+    h = ctypes.create_string_buffer(128)
     lib.ftar_debug_ipc_handle.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    assert lib.ftar_debug_ipc_handle(p, h) == 0
+    assert lib.ftar_debug_ipc_handle(px, h) == 0
     q_handle.put(h.raw)
     ok = q_done.get(timeout=240)
     assert hip.hipFree(p) == 0
@@ -142,7 +153,7 @@ def _ipc_user(n, q_handle, q_done, q_res):
         lib = ftar.lib()
         lib.ftar_debug_ipc_open.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]
         lib.ftar_debug_ipc_close.argtypes = [ctypes.c_void_p]
-        h = ctypes.create_string_buffer(raw, 64)
+        h = ctypes.create_string_buffer(raw, 128)
         mapped = ctypes.c_void_p()
         assert lib.ftar_debug_ipc_open(h, ctypes.byref(mapped)) == 0
         mine = fi.fill("f32", 12, 1, n)
@@ -256,3 +267,50 @@ def test_phase_timing(mode, topo, names):
     for r in range(P):
         assert [p[0] for p in got[r]] == names, got[r]
         assert got[r][0][1] == 0.0 and all(ms >= 0 for _, ms in got[r]), got[r]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("case", [c for c in gc.allreduce_cases(max_n=70000) if c["n"] > 0][::3],
+                         ids=lambda c: c["id"])
+def test_peer_registered_matches_reference_golden(case, mode):
+    """Registered buffers: the peer forms read the peers' inputs / write the peers' outputs in place."""
+    ins = gc.case_inputs(case)
+    outs = run_peer(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                    repeat=case["repeat"], mode=mode, registered=True)
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("P,topo,dt", [(8, "1", "f32"), (8, "2,4", "bf16"), (8, "8", "f32"), (5, "1", "f64"),
+                                       (16, "4,4", "f32")])
+@pytest.mark.parametrize("oop", [False, True])
+def test_peer_registered_one_round_plans(P, topo, dt, mode, oop):
+    n = 50_021 * P + 5
+    ins = [fi.fill(dt, 15, r, n) for r in range(P)]
+    outs = run_peer(ins, topo, dtype=fi.BY_NAME[dt], mode=mode, registered=True, outofplace=oop, repeat=2)
+    ref = oracle_lib.allreduce(oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt]), topo, dtype=fi.BY_NAME[dt])
+    for r in range(P):
+        assert outs[r].tobytes() == ref[r].tobytes(), r
+
+
+def test_peer_registered_phases_skip_the_local_pass():
+    """With registered buffers the phase list has no copy-in / copy-out."""
+    import ftar  # noqa: F401
+    P, n = 4, 1 << 18
+    g = group(P)
+    ins = [fi.fill("f32", 16, r, n) for r in range(P)]
+    for c in g.comms:
+        c.phase_timing(True)
+    try:
+        names = {}
+        for mode in MODES:
+            run_peer(ins, "4", mode=mode, registered=True)
+            names[mode] = [p[0] for p in g[0].last_phases()]
+    finally:
+        for c in g.comms:
+            c.phase_timing(False)
+    assert names["read"] == ["start", "barrier", "fold (remote reads)", "barrier", "gather (remote reads)",
+                             "barrier"], names
+    assert names["write"] == ["start", "scatter (remote writes)", "barrier", "fold (local)",
+                              "push (remote writes)", "barrier"], names
