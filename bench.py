@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct forms out of the sweep")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
+    ap.add_argument("--no-c5", action="store_true", help="N>1: skip the bf16 configs[4] line item")
+    ap.add_argument("--elements-c5", dest="n_c5", type=int, default=0, help="N>1: bf16 elements (default 2^29)")
     return ap.parse_args()
 
 
@@ -179,6 +181,16 @@ def bench_single(a):
     print(json.dumps(res), flush=True)
 
 
+def sample_index(n, dev, m=4096):
+    """m element indices spread over [0, n), computed in int64.  (A float32 linspace rounds n - 1 up to n
+    once n > 2^24 -- at 2^28 elements it indexes one past the end of the bucket.)"""
+    import torch
+    m = max(1, min(m, n))
+    idx = torch.arange(m, dtype=torch.int64, device=dev) * (n - 1) // max(1, m - 1)
+    assert int(idx[-1]) <= n - 1 and int(idx[0]) >= 0
+    return idx
+
+
 def _factorizations(n):
     out = []
 
@@ -302,7 +314,7 @@ def bench_distributed(a):
         return reg["x"], reg["y"]
 
     # correctness of y: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
-    idx = torch.linspace(0, n - 1, 4096, device=dev).long()
+    idx = sample_index(n, dev)
     xs = x[idx].float().cpu()
     allx = [torch.empty_like(xs) for _ in range(world)]
     dist.all_gather(allx, xs)
@@ -331,6 +343,40 @@ def bench_distributed(a):
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return bool(flag.item())
+
+    def measure_c5():
+        nb = a.n_c5 or (1 << 29)
+        xb = (torch.rand(nb, generator=gen, device=dev, dtype=torch.float32) * 2 - 1).to(torch.bfloat16)
+        yb = torch.empty_like(xb)
+        t5 = ftar.topo(a.topo, a.lonely, nranks=world) if a.topo else ftar.topo_from_env(world, nb * 2)
+        comm.chunk_bytes = default_chunk
+        comm.peer_direct = 0
+        comm.allgather = "direct"
+        comm.reduce_scatter = "direct"
+
+        def fn5():
+            comm.allreduce(xb, yb, nb, "bf16", "sum", topo_=t5, stream=stream)
+        ms5 = timed(fn5, min(a.steps, 10), 2)
+        # validation: every rank identical; within one bf16 rounding per fold level (at most P) of the fp64 sum
+        ix = sample_index(nb, dev)
+        xs5 = xb[ix].double().cpu()
+        ax = [torch.empty_like(xs5) for _ in range(world)]
+        dist.all_gather(ax, xs5)
+        r64, ab = sum(ax), sum(t.abs() for t in ax)
+        mine = yb[ix].double().cpu()
+        ay = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(ay, mine)
+        ok5 = all(torch.equal(ay[0], t) for t in ay) and bool(((mine - r64).abs() <= world * 2.0 ** -8 * ab + 1e-30).all())
+        flag = torch.tensor([1 if ok5 else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        alg5 = nb * 2 / (ms5 * 1e-3) / 1e9
+        del xb, yb
+        return {"workload": f"{world}xMI355X FlexTree AllReduce, bf16 2^{nb.bit_length() - 1} elements per rank "
+                            "(BASELINE configs[4])", "topology": str(t5), "form": "direct",
+                "chunk_bytes": default_chunk, "ms": round(ms5, 4), "value_GBps": round(world * alg5, 2),
+                "algbw_GBps_per_rank": round(alg5, 2),
+                "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
+                "check": "ok" if bool(flag.item()) else "MISMATCH"}
 
     def bws(m):
         alg = bucket / (m * 1e-3) / 1e9
@@ -495,6 +541,15 @@ def bench_distributed(a):
     except Exception as e:  # noqa: BLE001
         state["line"]["rccl_native_allreduce"] = None
         sys.stderr.write(f"rccl yardstick failed: {e}\n")
+
+    # 5. BASELINE configs[4] (C5): bf16 bucket of 2^29 elements (1 GiB) with the cost model's topology, the
+    # default data movement; one more line item, validated like the rest
+    state["phase"] = "C5 bf16"
+    if a.dtype == "f32" and not a.no_c5:
+        try:
+            state["line"]["c5_bf16"] = measure_c5()
+        except Exception as e:  # noqa: BLE001
+            state["line"]["c5_bf16"] = {"error": str(e)[:200]}
 
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])

@@ -31,7 +31,7 @@ for s in "${steps[@]}"; do
     ktree) run kbench_tree 600 python tools/kbench.py --rounds 8 --dtypes f32,bf16 --shapes "8;2,4;4,2;2,2,2;4;2,2;16;4,4;2,2,2,2" ;;
     host) run hostpath 600 python tools/hostpath.py ;;
     hosttrace) run hosttrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/htrace -o run -- python3 tools/engine_trace.py --host --ranks 2 --topo 2 --elements 268435456 --host-chunk-bytes 4194304 --iters 2 ;;
-    dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 --elements 16777216 ;;
+    dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
   esac
 done
