@@ -707,6 +707,23 @@ ftar_status_t ftar_comm_init_rank(ftar_comm_t* comm, int nranks, ftar_unique_id_
   return FTAR_SUCCESS;
 }
 
+ftar_status_t ftar_comm_init_host(ftar_comm_t* comm, int nranks, int rank, int device, ftar_host_allgather_fn allgather,
+                                  void* user) {
+  if (!comm || !allgather || nranks <= 0 || rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
+  std::unique_ptr<ftar_comm> c(new ftar_comm);
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  c->tp = ftar::make_host_transport(nranks, rank, allgather, user);
+  ftar_status_t st = ftar::comm_setup(c.get());
+  if (st != FTAR_SUCCESS) {
+    ftar::comm_teardown(c.get());
+    return st;
+  }
+  *comm = c.release();
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* devices) {
   if (!comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
   // ranks on different GPUs of this process copy straight over xGMI

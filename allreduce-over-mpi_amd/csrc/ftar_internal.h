@@ -175,5 +175,6 @@ std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_
 struct LocalHub;
 std::shared_ptr<LocalHub> make_local_hub(int nranks);
 std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, int rank);
+std::unique_ptr<Transport> make_host_transport(int nranks, int rank, ftar_host_allgather_fn fn, void* user);
 
 }  // namespace ftar

@@ -437,4 +437,90 @@ std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, i
   return std::unique_ptr<Transport>(new LocalTransport(std::move(hub), rank));
 }
 
+// ---------------------------------------------------------------------------
+// caller-bootstrapped processes (ftar_comm_init_host): peer-direct only
+// ---------------------------------------------------------------------------
+namespace {
+class HostTransport final : public Transport {
+ public:
+  HostTransport(int nranks, int rank, ftar_host_allgather_fn fn, void* user)
+      : nranks_(nranks), rank_(rank), fn_(fn), user_(user) {}
+  ftar_status_t group_start() override { return FTAR_SUCCESS; }
+  ftar_status_t send(const void*, size_t, int, hipStream_t) override { return unsupported(); }
+  ftar_status_t recv(void*, size_t, int, hipStream_t) override { return unsupported(); }
+  ftar_status_t group_end() override { return FTAR_SUCCESS; }
+  ftar_status_t allgather(const void*, void*, size_t, int, int, hipStream_t) override { return unsupported(); }
+  const char* name() const override { return "host"; }
+  // everything before it on s, on every rank, is complete when it returns
+  ftar_status_t barrier(hipStream_t s) override {
+    FTAR_CHECK_HIP(hipStreamSynchronize(s));
+    char mine = 1;
+    std::vector<char> all(nranks_);
+    return gather(&mine, all.data(), 1);
+  }
+  ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    IpcRef ref;
+    const bool exported = ipc_export(mine, &ref) == FTAR_SUCCESS;
+    std::vector<IpcRef> all(nranks);
+    FTAR_RETURN_IF(gather(&ref, all.data(), sizeof ref));
+    peers->assign(nranks, nullptr);
+    int failed = exported ? 0 : 1;
+    for (int q = 0; q < nranks && !failed; ++q) {
+      if (q == rank) {
+        (*peers)[q] = static_cast<char*>(mine);
+        continue;
+      }
+      void* base = nullptr;
+      char* p = nullptr;
+      if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
+        failed = 1;
+        break;
+      }
+      (*peers)[q] = p;
+      bases_[p] = base;
+    }
+    std::vector<int> flags(nranks);  // agreed: all map or none
+    FTAR_RETURN_IF(gather(&failed, flags.data(), sizeof failed));
+    for (int f : flags)
+      if (f) {
+        unmap_peers(peers, rank);
+        set_error("host transport: a rank could not map the peers' buffers", __FILE__, __LINE__);
+        return FTAR_ERR_HIP;
+      }
+    return FTAR_SUCCESS;
+  }
+  void unmap_peers(std::vector<char*>* peers, int rank) override {
+    for (int q = 0; q < (int)peers->size(); ++q) {
+      auto it = q == rank ? bases_.end() : bases_.find((*peers)[q]);
+      if (it == bases_.end()) continue;
+      (void)hipIpcCloseMemHandle(it->second);
+      bases_.erase(it);
+    }
+    peers->clear();
+  }
+
+ private:
+  static ftar_status_t unsupported() {
+    set_error("host transport: point-to-point transfers are not available (peer-direct forms only)", __FILE__,
+              __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
+  ftar_status_t gather(const void* mine, void* all, size_t bytes) {
+    if (fn_(mine, all, bytes, user_) != 0) {
+      set_error("host transport: the caller's allgather failed", __FILE__, __LINE__);
+      return FTAR_ERR_INTERNAL;
+    }
+    return FTAR_SUCCESS;
+  }
+  int nranks_, rank_;
+  ftar_host_allgather_fn fn_;
+  void* user_;
+  std::map<char*, void*> bases_;
+};
+}  // namespace
+
+std::unique_ptr<Transport> make_host_transport(int nranks, int rank, ftar_host_allgather_fn fn, void* user) {
+  return std::unique_ptr<Transport>(new HostTransport(nranks, rank, fn, user));
+}
+
 }  // namespace ftar

@@ -113,6 +113,8 @@ _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_comm_set_phase_timing.argtypes = [_vp, _int]
 _lib.ftar_comm_register.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_int)]
+_HOST_ALLGATHER = ctypes.CFUNCTYPE(_int, _vp, _vp, _sz, _vp)
+_lib.ftar_comm_init_host.argtypes = [ctypes.POINTER(_vp), _int, _int, _int, _HOST_ALLGATHER, _vp]
 _lib.ftar_comm_deregister.argtypes = [_vp, _int]
 _lib.ftar_comm_phase_json.argtypes = [_vp, ctypes.c_char_p, _sz]
 _lib.ftar_comm_phase_json.restype = ctypes.c_long
@@ -307,6 +309,25 @@ class Comm:
         h = _vp()
         _check(_lib.ftar_comm_init_rank(ctypes.byref(h), nranks, u, rank, device), "ftar_comm_init_rank")
         return cls(h.value, rank, nranks, device)
+
+    @classmethod
+    def init_host(cls, nranks, rank, device, allgather):
+        """One process per rank, bootstrapped by the caller's host collective (ftar_comm_init_host):
+        allgather(mine: bytes) -> list of every rank's bytes.  Peer-direct forms only."""
+        def cb(mine, all_, nbytes, user):
+            try:
+                parts = allgather(ctypes.string_at(mine, nbytes))
+                for r, b in enumerate(parts):
+                    ctypes.memmove(all_ + r * nbytes, b, nbytes)
+                return 0
+            except Exception:  # noqa: BLE001  reported to the library as a failed collective
+                return 1
+        fn = _HOST_ALLGATHER(cb)
+        h = _vp()
+        _check(_lib.ftar_comm_init_host(ctypes.byref(h), nranks, rank, device, fn, None), "ftar_comm_init_host")
+        c = cls(h.value, rank, nranks, device)
+        c._host_cb = fn   # the library calls it for as long as the communicator lives
+        return c
 
     @classmethod
     def init_local(cls, nranks, devices=None):

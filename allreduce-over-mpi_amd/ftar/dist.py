@@ -25,3 +25,20 @@ def init_comm(device=None, group=None):
         device = int(os.environ.get("LOCAL_RANK", dist.get_rank(group)))
     uid = exchange_unique_id(group)
     return ftar.Comm.init_rank(dist.get_world_size(group), uid, dist.get_rank(group), device)
+
+
+def init_host_comm(device=None, group=None):
+    """ftar.Comm bootstrapped over the torch.distributed group itself (no RCCL; ftar_comm_init_host):
+    the peer-direct forms only.  Ranks may share a device."""
+    import torch
+    import torch.distributed as dist
+    if device is None:
+        device = int(os.environ.get("LOCAL_RANK", dist.get_rank(group)))
+    world = dist.get_world_size(group)
+
+    def allgather(mine):
+        t = torch.frombuffer(bytearray(mine), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(outs, t, group=group)
+        return [o.numpy().tobytes() for o in outs]
+    return ftar.Comm.init_host(world, dist.get_rank(group), device, allgather)

@@ -138,6 +138,16 @@ ftar_status_t ftar_comm_init_rank(ftar_comm_t* comm, int nranks, ftar_unique_id_
  * Each ftar_allreduce on them must be issued from its own host thread, or via
  * ftar_allreduce_group. */
 ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* devices);
+/* One process per rank, bootstrapped by the caller's own host collective (MPI,
+ * gloo, ...): `allgather` copies `bytes` from `mine` into slot `rank` of `all`
+ * on every rank and returns 0 on success.  Data moves only by the peer-direct
+ * forms (IPC-mapped exchange or registered buffers; set FTAR_PEER_READ or
+ * FTAR_PEER_WRITE): p2p transfers are FTAR_ERR_UNSUPPORTED, so staged and
+ * lonely plans cannot run on it.  Barriers synchronize the stream and then
+ * the host collective (blocking).  Ranks may share a device. */
+typedef int (*ftar_host_allgather_fn)(const void* mine, void* all, size_t bytes, void* user);
+ftar_status_t ftar_comm_init_host(ftar_comm_t* comm, int nranks, int rank, int device, ftar_host_allgather_fn allgather,
+                                  void* user);
 ftar_status_t ftar_comm_destroy(ftar_comm_t comm);
 ftar_status_t ftar_comm_rank(ftar_comm_t comm, int* rank);
 ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size);
