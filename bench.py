@@ -542,6 +542,26 @@ def bench_distributed(a):
         state["line"]["rccl_native_allreduce"] = None
         sys.stderr.write(f"rccl yardstick failed: {e}\n")
 
+    # BASELINE configs[2] quotes 2 GPUs on a 256 MiB bucket: the headline configuration on the first 2^26
+    # elements of the same buffers, as a line item (the headline keeps the 1 GiB bucket at every N: weak scaling)
+    state["phase"] = "256 MiB"
+    try:
+        n2 = min(n, 1 << 26)
+        if n2 < n:
+            hb = state["line"]["config"]
+            t2 = ftar.topo("1" if hb["topology"] == "ring" else hb["topology"])
+            f2 = run_with(t2, hb["chunk_bytes"], hb["form"])
+            xin2, yout2 = f2.xin[:n2], f2.yout[:n2]
+            ms2 = timed(lambda: comm.allreduce(xin2, yout2, n2, a.dtype, "sum", topo_=t2, stream=stream),
+                        min(a.steps, 10), 2)
+            alg2 = n2 * esz / (ms2 * 1e-3) / 1e9
+            state["line"]["bucket_256MiB"] = {
+                "topology": str(t2), "form": hb["form"], "chunk_bytes": hb["chunk_bytes"], "ms": round(ms2, 4),
+                "value_GBps": round(world * alg2, 2), "algbw_GBps_per_rank": round(alg2, 2),
+                "busbw_GBps_per_rank": round(alg2 * 2 * (world - 1) / world if world > 1 else alg2, 2)}
+    except Exception as e:  # noqa: BLE001
+        state["line"]["bucket_256MiB"] = {"error": str(e)[:200]}
+
     # 5. BASELINE configs[4] (C5): bf16 bucket of 2^29 elements (1 GiB) with the cost model's topology, the
     # default data movement; one more line item, validated like the rest
     state["phase"] = "C5 bf16"
