@@ -255,6 +255,13 @@ def bench_distributed(a):
 
     threading.Thread(target=watchdog, daemon=True).start()
 
+    def phase(name):
+        """progress on stderr (rank 0): a long N>1 run never looks idle"""
+        state["phase"] = name
+        if rank == 0:
+            sys.stderr.write(f"[bench {time.time() - t_start:7.1f}s] {name}\n")
+            sys.stderr.flush()
+
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -414,7 +421,7 @@ def bench_distributed(a):
         return res
 
     # 1. the default configuration: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model
-    state["phase"] = "default"
+    phase("default")
     if a.topo:
         default_topo = ftar.topo(a.topo, a.lonely, nranks=world)
     else:
@@ -430,7 +437,7 @@ def bench_distributed(a):
                                 {"config_selection": "default (sweep not reached)", "default_config": default_info})
 
     # 2. the sweep: every factorization of P and the ring x chunk sizes x form; RCCL forms first, peer reads last
-    state["phase"] = "sweep"
+    phase("sweep")
     sweep = []
     cands = [str(default_topo)] + (["1"] if world > 1 else []) + [",".join(map(str, f)) for f in _factorizations(world)]
     seen, plan = set(), []
@@ -458,7 +465,7 @@ def bench_distributed(a):
             # xGMI calibration before the first peer configuration: link rates by copy kernels (read/write,
             # one peer / all peers), every rank at once; min/max over ranks
             probed = True
-            state["phase"] = "xgmi probe"
+            phase("xgmi probe")
             try:
                 pr = comm.xgmi_probe(64 << 20, iters=10)
                 vals = torch.tensor(list(pr.values()), dtype=torch.float64)
@@ -477,7 +484,7 @@ def bench_distributed(a):
             sweep.append({"skipped": f"sweep budget {sweep_budget:.0f}s reached ({len(plan) - len(sweep)} left)"})
             break
         key = str(t)
-        state["phase"] = f"sweep {key} {form} {chunk}"
+        phase(f"sweep {key} {form} {chunk}")
         try:
             fn = run_with(t, chunk, form)
             ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
@@ -490,7 +497,7 @@ def bench_distributed(a):
     state["line"]["sweep"] = sweep
 
     # 3. the sweep's best validated configuration, re-timed like the default, if it is faster
-    state["phase"] = "headline"
+    phase("headline")
     ok_runs = [r for r in sweep if "ms" in r and r.get("check") == "ok"]
     best = min(ok_runs, key=lambda r: r["ms"]) if ok_runs else None
     if best is not None and best["ms"] < ms_default:
@@ -510,7 +517,7 @@ def bench_distributed(a):
 
     # phase timelines (rank 0's view) of the default and of the fastest validated configuration of each form:
     # where a call's time goes (transfer rounds vs folds vs barriers), for the next round's tuning
-    state["phase"] = "phase timing"
+    phase("phase timing")
     try:
         fam_best = {}
         for r in ok_runs:
@@ -532,7 +539,7 @@ def bench_distributed(a):
         state["line"]["phases_rank0"] = {"error": str(e)[:200]}
 
     # 4. RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
-    state["phase"] = "rccl yardstick"
+    phase("rccl yardstick")
     try:
         y2 = torch.empty_like(x)
         ms_rccl = timed(lambda: comm.rccl_allreduce(x, y2, n, a.dtype, "sum", stream=stream), min(a.steps, 10), 2)
@@ -544,7 +551,7 @@ def bench_distributed(a):
 
     # BASELINE configs[2] quotes 2 GPUs on a 256 MiB bucket: the headline configuration on the first 2^26
     # elements of the same buffers, as a line item (the headline keeps the 1 GiB bucket at every N: weak scaling)
-    state["phase"] = "256 MiB"
+    phase("256 MiB")
     try:
         n2 = min(n, 1 << 26)
         if n2 < n:
@@ -564,7 +571,7 @@ def bench_distributed(a):
 
     # 5. BASELINE configs[4] (C5): bf16 bucket of 2^29 elements (1 GiB) with the cost model's topology, the
     # default data movement; one more line item, validated like the rest
-    state["phase"] = "C5 bf16"
+    phase("C5 bf16")
     if a.dtype == "f32" and not a.no_c5:
         try:
             state["line"]["c5_bf16"] = measure_c5()
