@@ -288,3 +288,30 @@ def test_host_allreduce_growing_buckets():
         outs = run_group_host(ins, "2,2", host_chunk=65536, ag="stages", rs="stages")
         ref = oracle_lib.allreduce(ins, "2,2")
         assert all(outs[r].tobytes() == ref[r].tobytes() for r in range(P)), n
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_soak_all_forms(seed):
+    """Seeded random cases (topologies incl. lonely, dtypes, ops, ragged sizes, pieces) through every
+    data-movement form: reduce-scatter stages|direct x all-gather stages|direct|collective x peer
+    off|read|write (peer forms fall back to p2p where the plan is not one-round).  Bit-exact vs the oracle.
+    FTAR_SOAK scales the case count (default 40 per seed)."""
+    import os
+    import random
+    import random_cases
+    per = int(os.environ.get("FTAR_SOAK", "40"))
+    rng = random.Random(1000 + seed)
+    for c in random_cases.cases(seed=500 + seed, count=per, max_p=12):
+        rs = rng.choice(["stages", "direct"])
+        ag = rng.choice(["stages", "direct", "collective"])
+        peer = rng.choice([0, 0, "read", "write"])
+        g = group(c["P"])
+        g.set_peer_direct(peer)
+        try:
+            outs = run_group(c["ins"], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1,
+                             c["oop"], chunk_bytes=c["chunk"], ag=ag, rs=rs)
+        finally:
+            g.set_peer_direct(0)
+        for r in range(c["P"]):
+            assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"],
+                                                                rs, ag, peer, r)
