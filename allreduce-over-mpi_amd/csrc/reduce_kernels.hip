@@ -34,12 +34,22 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kTreeLevels = kMaxFoldLevels;
-// Measured on MI355X (tools/kbench.py, interleaved, 2^26 fp32):
-// nontemporal loads + plain stores, 2 vectors per lane, 256-thread workgroups
-// is the best of the variants at k = 2 (6.96 TB/s) and among the best at k = 8;
-// nontemporal STORES cost 6-8 % (they also evict what the next ring step sends).
+// Measured on MI355X with COLD data (tools/kbench_cold.py: launches rotate over
+// 4 disjoint buffer sets, so nothing is left in the 256 MB Infinity Cache from
+// the previous launch -- the AllReduce's situation, where every piece is new
+// data; DESIGN.md §3, profiles/r01/kbench_cold*.log): nontemporal loads AND
+// nontemporal stores (f32 k = 2: 6.55 TB/s vs 6.09 with plain stores), with
+//   4 vectors per lane, 256-thread workgroups for k <= 4 and for 16-bit types,
+//   2 vectors per lane, 512-thread workgroups otherwise (f32 k = 8: 5.94 vs
+//   5.70 TB/s with 4 x 256, whose 8 x 4 outstanding loads per lane cost waves).
+// Rewriting the same destination back to back (the reference harness's loop)
+// favours plain stores instead: the MALL absorbs part of the writes; that
+// regime is not the hot path's.
 constexpr int kUnroll = 2;
-constexpr bool kNtLoads = true, kNtStores = false;
+constexpr int kVecThreads = 512;
+constexpr bool kNtLoads = true, kNtStores = true;
+template <class Tr, int K>
+constexpr bool kWideLanes = K >= 2 && (K <= 4 || sizeof(typename Tr::S) <= 2);
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -484,7 +494,7 @@ __global__ void __launch_bounds__(kThreads)
       }
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) d[v0 + u * kThreads] = Tr::v_fin(v[u]);
+    for (int u = 0; u < U; ++u) st16<kNtStores>(d + v0 + u * kThreads, Tr::v_fin(v[u]));
   }
 #pragma unroll
   for (int u = 0; u < U; ++u) {  // the one partial tile (if any)
@@ -575,7 +585,10 @@ hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, in
 
 template <class Tr, int K>
 hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
-  return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kThreads>(srcs, k, dst, nvec, head, tail, s, 0);
+  if constexpr (kWideLanes<Tr, K>)
+    return launch_cfg<Tr, K, 4, kNtLoads, kNtStores, 256>(srcs, k, dst, nvec, head, tail, s, 0);
+  else
+    return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kVecThreads>(srcs, k, dst, nvec, head, tail, s, 0);
 }
 
 // Leaf codes of a nested fold with bottom-up widths shape[0..nlevels) over k
@@ -705,6 +718,22 @@ hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nv
     case 9: return launch_cfg<Tr, K, 2, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
     case 10: return launch_cfg<Tr, K, 1, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 11: return launch_cfg<Tr, K, 4, true, false, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 12: return launch_cfg<Tr, K, 2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);   // nt stores
+    case 13: return launch_cfg<Tr, K, 1, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 14: return launch_cfg<Tr, K, 4, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 15: return launch_cfg<Tr, K, 2, false, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 16: return launch_cfg<Tr, K, 2, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 17: return launch_cfg<Tr, K, 4, true, false, 256>(srcs, k, dst, nvec, 0, 0, s, 4096);
+    case 18: return launch_cfg<Tr, K, 2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 8192);
+    case 19: return launch_cfg<Tr, K, 4, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 23: return launch_cfg<Tr, K, 4, true, true, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 24: return launch_cfg<Tr, K, 8, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 25: return launch_cfg<Tr, K, 2, true, true, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 26: return launch_cfg<Tr, K, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 27: return launch_cfg<Tr, 0, 2, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);  // runtime-k loop
+    case 28: return launch_cfg<Tr, 0, 4, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 29: return launch_cfg<Tr, 0, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 30: return launch_cfg<Tr, 0, 2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 20: return launch_lds<Tr, K, 2, 2>(srcs, dst, nvec, s);  // LDS-DMA, nt
     case 21: return launch_lds<Tr, K, 4, 2>(srcs, dst, nvec, s);
     case 22: return launch_lds<Tr, K, 2, 0>(srcs, dst, nvec, s);  // LDS-DMA, default policy

@@ -23,10 +23,13 @@ ap.add_argument("--source", default="")
 a = ap.parse_args()
 
 
-def values(path, counter):
+def rows(path, counter):
     with open(path) as f:
-        return [float(r["Counter_Value"]) for r in csv.DictReader(f)
-                if r["Counter_Name"] == counter and "reduce_vec_kernel" in r["Kernel_Name"]]
+        return [r for r in csv.DictReader(f) if r["Counter_Name"] == counter and "reduce_vec_kernel" in r["Kernel_Name"]]
+
+
+def values(path, counter):
+    return [float(r["Counter_Value"]) for r in rows(path, counter)]
 
 
 fetch = statistics.median(values(a.fetch_csv, "FETCH_SIZE"))
@@ -34,7 +37,8 @@ write = statistics.median(values(a.write_csv, "WRITE_SIZE"))
 rd, wr = 2 * fetch * 1024, write * 1024
 key = f"reduce_k{a.k}_f32_n{a.elements}"
 res = {key: {
-    "kernel": f"reduce_vec_kernel<F32Sum, {a.k}, 2, NTL=true, NTS=false, 256>",
+    "kernel": rows(a.fetch_csv, "FETCH_SIZE")[0]["Kernel_Name"].replace("ftar::(anonymous namespace)::", "")
+                                                                 .replace("void ", "").split("(")[0],
     "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write,
     "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
     "algorithmic_bytes_per_launch": (a.k + 1) * a.elements * 4,
