@@ -289,7 +289,8 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my buffers after the call
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   } else if (!write) {
-    FTAR_CHECK_HIP(hipMemcpyAsync(X, in, bytes, hipMemcpyDeviceToDevice, c->comm_s));
+    const Segment whole{in, X, bytes};
+    FTAR_RETURN_IF(launch_gather(&whole, 1, c->comm_s));
     FTAR_RETURN_IF(mark(c, "copy-in", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -510,9 +511,12 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   if (sendbuf == recvbuf) sendbuf = nullptr;
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
-    if (sendbuf && count)
-      FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, host ? hipMemcpyHostToHost : hipMemcpyDeviceToDevice,
-                                    stream));
+    if (sendbuf && count && host)
+      FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, hipMemcpyHostToHost, stream));
+    if (sendbuf && count && !host) {
+      const Segment whole{sendbuf, recvbuf, count * esz};
+      return launch_gather(&whole, 1, stream);
+    }
     return FTAR_SUCCESS;
   }
   if (count == 0) return FTAR_SUCCESS;

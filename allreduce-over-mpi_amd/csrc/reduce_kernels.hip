@@ -555,12 +555,12 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   u32x4* d4 = reinterpret_cast<u32x4*>(dst + head);
   size_t v = bid * (2 * kThreads) + threadIdx.x;
   const size_t stride = nb * (2 * kThreads);
-  for (; v + kThreads < nvec; v += stride) {
-    const u32x4 x0 = s4[v], x1 = s4[v + kThreads];
-    d4[v] = x0;
-    d4[v + kThreads] = x1;
+  for (; v + kThreads < nvec; v += stride) {  // streaming both ways (cold copy: 6.3 vs 5.5 TB/s for the DMA blit)
+    const u32x4 x0 = ld16<true>(s4 + v), x1 = ld16<true>(s4 + v + kThreads);
+    st16<true>(d4 + v, x0);
+    st16<true>(d4 + v + kThreads, x1);
   }
-  if (v < nvec) d4[v] = s4[v];
+  if (v < nvec) st16<true>(d4 + v, ld16<true>(s4 + v));
 }
 
 // ---------------------------------------------------------------------------
@@ -798,9 +798,10 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   if (count == 0) return FTAR_SUCCESS;
   for (int j = 0; j < k; ++j)
     if (!srcs[j]) return FTAR_ERR_INVALID_ARG;
-  if (k == 1) {  // vector_add/reduce_sum.h:36-47: a copy
-    if (srcs[0] != dst) FTAR_CHECK_HIP(hipMemcpyAsync(dst, srcs[0], count * dtype_size(dt), hipMemcpyDeviceToDevice, s));
-    return FTAR_SUCCESS;
+  if (k == 1) {  // vector_add/reduce_sum.h:36-47: a copy (streaming copy kernel, not the DMA blit)
+    if (srcs[0] == dst) return FTAR_SUCCESS;
+    const Segment seg{srcs[0], dst, count * dtype_size(dt)};
+    return launch_gather(&seg, 1, s);
   }
   hipError_t e = hipErrorInvalidValue;
   if (nlevels > 1 && op == FTAR_SUM && (dt == FTAR_FLOAT32 || dt == FTAR_FLOAT64 || dt == FTAR_BFLOAT16)) {

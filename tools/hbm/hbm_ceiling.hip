@@ -54,6 +54,20 @@ __global__ void __launch_bounds__(kT) add2(const u32x4* a, const u32x4* b, u32x4
     if (v + u * kT < nvec) d[v + u * kT] = x[u] + y[u];
 }
 
+template <int U>
+__global__ void __launch_bounds__(kT) copy_nt(const u32x4* a, u32x4* d, size_t nvec) {
+  size_t v = (size_t)blockIdx.x * (U * kT) + threadIdx.x;
+  u32x4 x[U];
+  for (int u = 0; u < U; ++u) x[u] = v + u * kT < nvec ? __builtin_nontemporal_load(a + v + u * kT) : u32x4{0, 0, 0, 0};
+  for (int u = 0; u < U; ++u)
+    if (v + u * kT < nvec) __builtin_nontemporal_store(x[u], d + v + u * kT);
+}
+__global__ void __launch_bounds__(kT) write_nt(u32x4* d, size_t nvec) {
+  size_t v = (size_t)blockIdx.x * (kU * kT) + threadIdx.x;
+  for (int u = 0; u < kU; ++u, v += kT)
+    if (v < nvec) __builtin_nontemporal_store(u32x4{(unsigned)v, 1u, 2u, 3u}, d + v);
+}
+
 int main(int argc, char** argv) {
   const size_t n = argc > 1 ? strtoull(argv[1], nullptr, 0) : (size_t)1 << 26;  // fp32 elements per stream
   const int reps = argc > 2 ? atoi(argv[2]) : 20, rounds = argc > 3 ? atoi(argv[3]) : 5;
@@ -73,10 +87,13 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  const char* names[4] = {"read 2 streams", "write 1 stream", "copy 1R:1W", "add 2R:1W (k=2 reduce mix)"};
-  const double traffic[4] = {2.0 * bytes, 1.0 * bytes, 2.0 * bytes, 3.0 * bytes};
+  const char* names[8] = {"read 2 streams", "write 1 stream", "copy 1R:1W", "add 2R:1W (k=2 reduce mix)",
+                          "write 1 stream, nt stores", "copy 1R:1W, nt stores, 2/lane", "copy 1R:1W, nt stores, 4/lane",
+                          "hipMemcpyAsync D2D"};
+  const double traffic[8] = {2.0 * bytes, 1.0 * bytes, 2.0 * bytes, 3.0 * bytes, 1.0 * bytes, 2.0 * bytes, 2.0 * bytes,
+                             2.0 * bytes};
   for (int r = 0; r < rounds; ++r)
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < 8; ++t) {
       auto launch = [&] {
         const int i = cur++ % sets;
         u32x4 *a = A[i], *b = B[i], *d = D[i];
@@ -84,6 +101,10 @@ int main(int argc, char** argv) {
         if (t == 1) hipLaunchKernelGGL(write1, dim3(blocks), dim3(kT), 0, 0, d, nvec);
         if (t == 2) hipLaunchKernelGGL(copy1, dim3(blocks), dim3(kT), 0, 0, a, d, nvec);
         if (t == 3) hipLaunchKernelGGL(add2, dim3(blocks), dim3(kT), 0, 0, a, b, d, nvec);
+        if (t == 4) hipLaunchKernelGGL(write_nt, dim3(blocks), dim3(kT), 0, 0, d, nvec);
+        if (t == 5) hipLaunchKernelGGL(copy_nt<2>, dim3(blocks), dim3(kT), 0, 0, a, d, nvec);
+        if (t == 6) hipLaunchKernelGGL(copy_nt<4>, dim3((blocks + 1) / 2), dim3(kT), 0, 0, a, d, nvec);
+        if (t == 7) (void)hipMemcpyAsync(d, a, bytes, hipMemcpyDeviceToDevice, 0);
       };
       for (int i = 0; i < 3; ++i) launch();
       CHECK(hipEventRecord(e0, 0));
