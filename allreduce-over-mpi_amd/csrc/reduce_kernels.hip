@@ -37,19 +37,22 @@ constexpr int kTreeLevels = kMaxFoldLevels;
 // Measured on MI355X with COLD data (tools/kbench_cold.py: launches rotate over
 // 4 disjoint buffer sets, so nothing is left in the 256 MB Infinity Cache from
 // the previous launch -- the AllReduce's situation, where every piece is new
-// data; DESIGN.md §3, profiles/r01/kbench_cold*.log): nontemporal loads AND
-// nontemporal stores (f32 k = 2: 6.55 TB/s vs 6.09 with plain stores), with
-//   4 vectors per lane, 256-thread workgroups for k <= 4 and for 16-bit types,
-//   2 vectors per lane, 512-thread workgroups otherwise (f32 k = 8: 5.94 vs
-//   5.70 TB/s with 4 x 256, whose 8 x 4 outstanding loads per lane cost waves).
-// Rewriting the same destination back to back (the reference harness's loop)
-// favours plain stores instead: the MALL absorbs part of the writes; that
-// regime is not the hot path's.
+// data; DESIGN.md §3, profiles/r01/kbench_cold*.log):
+//  * nontemporal loads AND stores (f32 k = 2: 6.55 TB/s vs 6.09 with plain
+//    stores; rewriting the same destination back to back -- the reference
+//    harness's loop -- favours plain stores instead, because the MALL absorbs
+//    part of the writes, a regime the hot path never sees);
+//  * k = 2..8: staged through LDS (LDS-DMA): every wave streams U tiles of 1 KiB
+//    per source into LDS with global_load_lds_dwordx4 (no VGPR landing zone),
+//    waits on its own vmcnt and folds from LDS -- f32 +1 % at k = 2 and +3-5 %
+//    at k = 4..8 over the best register variant with U = 4; 16-bit sums (more
+//    ALU per byte) keep occupancy with fewer tiles as k grows;
+//  * k > 8 (runtime k): registers, 2 vectors per lane, 512-thread workgroups.
 constexpr int kUnroll = 2;
 constexpr int kVecThreads = 512;
 constexpr bool kNtLoads = true, kNtStores = true;
 template <class Tr, int K>
-constexpr bool kWideLanes = K >= 2 && (K <= 4 || sizeof(typename Tr::S) <= 2);
+constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? 4 : (K <= 4 ? 4 : (K <= 6 ? 3 : 2));
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -296,25 +299,37 @@ __global__ void __launch_bounds__(BS)
   }
 }
 
-// LDS-staged variant (A/B only, tools/kbench.py variants 20-22): each wave
-// streams its sources into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB
-// per wave instruction, no VGPR destination), waits on its own vmcnt, then
-// every lane reads back its own 16 B with ds_read_b128 and folds.  On an
-// element-wise reduce nothing is shared between lanes, so LDS only replaces
-// VGPRs as the landing zone of the loads; measured against the register path
-// in DESIGN.md §3.
+// LDS-staged reduce: the production kernel for k = 2..8 (launch_k; A/B
+// variants 20/21/31-33 in tools/kbench_cold.py).  Each wave streams U tiles of
+// every source into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction, nontemporal, no VGPR destination), waits on its own vmcnt, then
+// every lane reads back its own 16 B with ds_read_b128 and folds.  Nothing is
+// shared between lanes in an element-wise sum, so LDS serves as the landing
+// zone of the loads: more bytes in flight per wave than VGPRs allow (K x U KiB
+// per wave).  Workgroup 0 also does the `head` leading and `tail` trailing
+// elements element-wise, as reduce_vec_kernel does.
 template <class Tr, int K, int U, int AUX>
-__global__ void __launch_bounds__(256) reduce_lds_kernel(Srcs<K> src, void* __restrict__ dst, size_t nvec) {
+__global__ void __launch_bounds__(256)
+    reduce_lds_kernel(Srcs<K> src, void* __restrict__ dst, size_t nvec, int head, int tail) {
+  using S = typename Tr::S;
+  constexpr int VE = 16 / sizeof(S);
   __shared__ u32x4 lds[4][K][U][64];
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {  // unaligned head / short tail
+    const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
+    typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
+    for (int j = 1; j < K; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
+    static_cast<S*>(dst)[e] = Tr::s_fin(a);
+  }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t base = ((size_t)blockIdx.x * 4 + wave) * (U * 64);
-  u32x4* d = static_cast<u32x4*>(dst);
+  u32x4* d = reinterpret_cast<u32x4*>(static_cast<S*>(dst) + head);
+  auto sp = [&](int j) { return reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head); };
   if (base + U * 64 <= nvec) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const u32x4* g = static_cast<const u32x4*>(src.p[j]) + base + u * 64 + lane;
+        const u32x4* g = sp(j) + base + u * 64 + lane;
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
                                          (__attribute__((address_space(3))) void*)&lds[wave][j][u][0], 16, 0, AUX);
       }
@@ -324,27 +339,27 @@ __global__ void __launch_bounds__(256) reduce_lds_kernel(Srcs<K> src, void* __re
       typename Tr::VA a = Tr::v_init(lds[wave][0][u][lane]);
 #pragma unroll
       for (int j = 1; j < K; ++j) a = Tr::v_comb(a, lds[wave][j][u][lane]);
-      d[base + u * 64 + lane] = Tr::v_fin(a);
+      st16<kNtStores>(d + base + u * 64 + lane, Tr::v_fin(a));
     }
   } else {
     for (int u = 0; u < U; ++u) {
       const size_t v = base + u * 64 + lane;
       if (v >= nvec) break;
-      typename Tr::VA a = Tr::v_init(static_cast<const u32x4*>(src.p[0])[v]);
-      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, static_cast<const u32x4*>(src.p[j])[v]);
-      d[v] = Tr::v_fin(a);
+      typename Tr::VA a = Tr::v_init(ld16<kNtLoads>(sp(0) + v));
+      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, ld16<kNtLoads>(sp(j) + v));
+      st16<kNtStores>(d + v, Tr::v_fin(a));
     }
   }
 }
 
 template <class Tr, int K, int U, int AUX>
-hipError_t launch_lds(const void* const* srcs, void* dst, size_t nvec, hipStream_t s) {
+hipError_t launch_lds(const void* const* srcs, void* dst, size_t nvec, hipStream_t s, int head = 0, int tail = 0) {
   Srcs<K> a{};
   for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
   const size_t per_block = (size_t)4 * U * 64;
   const size_t blocks = (nvec + per_block - 1) / per_block;
   hipLaunchKernelGGL((reduce_lds_kernel<Tr, K, U, AUX>), dim3((unsigned)(blocks ? blocks : 1)), dim3(256), 0, s, a,
-                     dst, nvec);
+                     dst, nvec, head, tail);
   return hipGetLastError();
 }
 
@@ -585,8 +600,8 @@ hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, in
 
 template <class Tr, int K>
 hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
-  if constexpr (kWideLanes<Tr, K>)
-    return launch_cfg<Tr, K, 4, kNtLoads, kNtStores, 256>(srcs, k, dst, nvec, head, tail, s, 0);
+  if constexpr (K >= 2)
+    return launch_lds<Tr, K, kLdsTiles<Tr, K>, 2>(srcs, dst, nvec, s, head, tail);
   else
     return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kVecThreads>(srcs, k, dst, nvec, head, tail, s, 0);
 }
@@ -730,6 +745,9 @@ hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nv
     case 24: return launch_cfg<Tr, K, 8, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 25: return launch_cfg<Tr, K, 2, true, true, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 26: return launch_cfg<Tr, K, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
+    case 31: return launch_lds<Tr, K, (K <= 4 ? 4 : 2), 2>(srcs, dst, nvec, s);
+    case 32: return launch_lds<Tr, K, (K <= 4 ? 4 : (K <= 6 ? 3 : 2)), 2>(srcs, dst, nvec, s);
+    case 33: return launch_lds<Tr, K, 1, 2>(srcs, dst, nvec, s);
     case 27: return launch_cfg<Tr, 0, 2, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);  // runtime-k loop
     case 28: return launch_cfg<Tr, 0, 4, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 29: return launch_cfg<Tr, 0, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
@@ -744,7 +762,9 @@ template <class Tr>
 hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
   switch (k) {
     case 2: return variant_k<Tr, 2>(v, srcs, k, dst, nvec, s);
+    case 3: return variant_k<Tr, 3>(v, srcs, k, dst, nvec, s);
     case 4: return variant_k<Tr, 4>(v, srcs, k, dst, nvec, s);
+    case 6: return variant_k<Tr, 6>(v, srcs, k, dst, nvec, s);
     case 8: return variant_k<Tr, 8>(v, srcs, k, dst, nvec, s);
   }
   return hipErrorInvalidValue;

@@ -25,7 +25,7 @@ a = ap.parse_args()
 
 def rows(path, counter):
     with open(path) as f:
-        return [r for r in csv.DictReader(f) if r["Counter_Name"] == counter and "reduce_vec_kernel" in r["Kernel_Name"]]
+        return [r for r in csv.DictReader(f) if r["Counter_Name"] == counter and ("reduce_lds_kernel" in r["Kernel_Name"] or "reduce_vec_kernel" in r["Kernel_Name"])]
 
 
 def values(path, counter):
