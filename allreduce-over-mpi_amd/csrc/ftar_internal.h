@@ -117,7 +117,9 @@ struct Segment {
   void* dst;
   size_t bytes;
 };
-ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream);
+// nt: nontemporal loads and stores (the default: cold copies, data not
+// re-read soon); false keeps both in the caches.
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true);
 size_t dtype_size(ftar_dtype_t dt);
 
 // ---------------------------------------------------------------------------

@@ -549,6 +549,7 @@ struct SegArgs {
   size_t bytes[FTAR_MAX_K];
 };
 
+template <bool NT>
 __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   const int sgi = (int)(blockIdx.x % (unsigned)m);
   const size_t bid = blockIdx.x / (unsigned)m, nb = gridDim.x / (unsigned)m;
@@ -571,11 +572,11 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   size_t v = bid * (2 * kThreads) + threadIdx.x;
   const size_t stride = nb * (2 * kThreads);
   for (; v + kThreads < nvec; v += stride) {  // streaming both ways (cold copy: 6.3 vs 5.5 TB/s for the DMA blit)
-    const u32x4 x0 = ld16<true>(s4 + v), x1 = ld16<true>(s4 + v + kThreads);
-    st16<true>(d4 + v, x0);
-    st16<true>(d4 + v + kThreads, x1);
+    const u32x4 x0 = ld16<NT>(s4 + v), x1 = ld16<NT>(s4 + v + kThreads);
+    st16<NT>(d4 + v, x0);
+    st16<NT>(d4 + v + kThreads, x1);
   }
-  if (v < nvec) st16<true>(d4 + v, ld16<true>(s4 + v));
+  if (v < nvec) st16<NT>(d4 + v, ld16<NT>(s4 + v));
 }
 
 // ---------------------------------------------------------------------------
@@ -790,7 +791,7 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
   return false;
 }
 
-ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream) {
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt) {
   if (nsegs < 0 || nsegs > FTAR_MAX_K) return FTAR_ERR_INVALID_ARG;
   SegArgs a{};
   int m = 0;
@@ -806,7 +807,10 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream) 
   if (!m) return FTAR_SUCCESS;
   size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
   bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+  if (nt)
+    hipLaunchKernelGGL(gather_kernel<true>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+  else
+    hipLaunchKernelGGL(gather_kernel<false>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
   FTAR_CHECK_HIP(hipGetLastError());
   return FTAR_SUCCESS;
 }
