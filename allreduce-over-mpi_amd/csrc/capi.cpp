@@ -3,7 +3,10 @@
 // AllReduce entry points live in engine.cpp.
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -24,6 +27,18 @@ void set_error(const std::string& msg, const char* file, int line) {
   if (getenv("FTAR_DEBUG")) fprintf(stderr, "[ftar] %s\n", g_last_error.c_str());
 }
 const char* last_error() { return g_last_error.c_str(); }
+
+void trace(const char* fmt, ...) {
+  static const bool on = getenv("FTAR_TRACE") && *getenv("FTAR_TRACE") && *getenv("FTAR_TRACE") != '0';
+  if (!on) return;
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "[ftar pid %d] %s\n", (int)getpid(), buf);
+  fflush(stderr);
+}
 
 namespace {
 

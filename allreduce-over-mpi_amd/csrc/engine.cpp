@@ -197,19 +197,46 @@ bool peer_eligible(const Plan& plan) {
 
 namespace {
 // grow-only exchange buffer, exported and mapped by every rank (collective)
+//
+// The new buffer is allocated while the old one and the old peer mappings are
+// still alive, and it must pass an export check before it is used: a fresh
+// allocation whose address range was recently an IPC mapping (closed) can
+// fail hipIpcGetMemHandle with "invalid argument" (seen on ROCm 7.2 with
+// dmabuf IPC, tools/peer_rehearsal.py), so such an allocation is set aside
+// and another one taken.  Nothing here returns before map_peers: every rank
+// must reach the exchange, a failed rank publishes an invalid reference and
+// all ranks fail together.
 ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   if (bytes <= c->xbuf_bytes && !c->xpeers.empty()) return FTAR_SUCCESS;
   Transport* tp = c->tp.get();
   FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still touches the old X
   FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-  const size_t want = std::max(bytes, c->xbuf_bytes);
+  const size_t want = tp->uses_ipc() ? ipc_safe_size(std::max(bytes, c->xbuf_bytes)) : std::max(bytes, c->xbuf_bytes);
+  trace("rank %d: exchange buffer %zu -> %zu bytes", c->rank, c->xbuf_bytes, want);
+  void* fresh = nullptr;
+  std::vector<void*> set_aside;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    if (hipMalloc(&fresh, want) != hipSuccess) {
+      fresh = nullptr;
+      set_error("exchange buffer: hipMalloc of " + std::to_string(want) + " bytes failed", __FILE__, __LINE__);
+      break;
+    }
+    IpcRef probe;
+    if (!tp->uses_ipc() || ipc_export(fresh, &probe) == FTAR_SUCCESS) break;
+    trace("rank %d: %p not exportable, allocating another", c->rank, fresh);
+    set_aside.push_back(fresh);
+    fresh = nullptr;
+  }
+  for (void* p : set_aside) (void)hipFree(p);
   tp->unmap_peers(&c->xpeers, c->rank);
-  if (c->xbuf) FTAR_CHECK_HIP(hipFree(c->xbuf));
-  c->xbuf = nullptr;
-  c->xbuf_bytes = 0;
-  FTAR_CHECK_HIP(hipMalloc(&c->xbuf, want));
-  c->xbuf_bytes = want;
-  return tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers);
+  if (c->xbuf) (void)hipFree(c->xbuf);  // (no early return: the peers are on their way to the exchange)
+  c->xbuf = fresh;
+  c->xbuf_bytes = fresh ? want : 0;
+  trace("rank %d: exchange buffer at %p, map peers", c->rank, fresh);
+  const ftar_status_t st = tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers);
+  trace("rank %d: map peers -> %d", c->rank, (int)st);
+  if (st != FTAR_SUCCESS) c->xpeers.clear();
+  return st;
 }
 
 // the plan's fold of my block with operand i read from where(i)

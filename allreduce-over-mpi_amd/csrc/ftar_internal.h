@@ -29,6 +29,9 @@ namespace ftar {
   } while (0)
 
 void set_error(const std::string& msg, const char* file, int line);
+// FTAR_TRACE=1: one stderr line per step of the collective bring-up paths
+// (exchange-buffer growth, IPC export/import/close), so a stall names its call
+void trace(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 const char* last_error();
 
 // ---------------------------------------------------------------------------
@@ -152,6 +155,8 @@ class Transport {
   virtual ftar_status_t barrier(hipStream_t s) = 0;
   virtual ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) = 0;
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
+  // map_peers exports and opens IPC handles (false: one address space)
+  virtual bool uses_ipc() const { return false; }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {
@@ -165,10 +170,23 @@ class Transport {
 struct IpcRef {
   hipIpcMemHandle_t handle;
   uint64_t offset;
-  uint64_t pad[7];
+  uint64_t valid;  // 1 when the export succeeded: peers never open a failed rank's handle
+  uint64_t pad[6];
 };
 static_assert(sizeof(IpcRef) == 128, "IpcRef layout");
+// On failure *out is still a well-formed reference with valid = 0, so the
+// caller publishes it like any other and every rank learns of the failure in
+// the same exchange (an unpublished or garbage handle would leave the peers
+// blocked in hipIpcOpenMemHandle or in the exchange itself).
 ftar_status_t ipc_export(const void* p, IpcRef* out);
+// HIP runtimes before 7.2 (torch 2.10 bundles 7.0) block forever in
+// hipIpcOpenMemHandle when the exported allocation's size has bit 31 set
+// (2-4 GiB, 6-8 GiB, ...; measured: tools/ipc_order_probe.py --torch).  When
+// the loaded runtime is affected (or FTAR_IPC_SIZE_GUARD=1; =0 turns it off)
+// ipc_export refuses such allocations and the exchange buffers are sized
+// around them (ipc_safe_size).
+bool ipc_size_guard();
+size_t ipc_safe_size(size_t bytes);
 // opens ref; *base = the mapped allocation (for hipIpcCloseMemHandle), *p = base + offset
 ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p);
 

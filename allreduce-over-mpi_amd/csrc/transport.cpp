@@ -20,6 +20,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -29,19 +30,54 @@
 
 namespace ftar {
 
+bool ipc_size_guard() {
+  static const bool on = [] {
+    if (const char* e = getenv("FTAR_IPC_SIZE_GUARD")) return *e != '0';
+    int v = 0;
+    return hipRuntimeGetVersion(&v) != hipSuccess || v < 70200000;  // major*1e7 + minor*1e5 + patch
+  }();
+  return on;
+}
+
+size_t ipc_safe_size(size_t bytes) {
+  const size_t bit31 = size_t(1) << 31, mask4g = (size_t(1) << 32) - 1;
+  return (ipc_size_guard() && (bytes & bit31)) ? (bytes | mask4g) + 1 : bytes;  // up to the next 4 GiB
+}
+
 ftar_status_t ipc_export(const void* p, IpcRef* out) {
   memset(out, 0, sizeof *out);
   hipDeviceptr_t base = nullptr;
   size_t size = 0;
   FTAR_CHECK_HIP(hipMemGetAddressRange(&base, &size, const_cast<void*>(p)));
+  trace("ipc_export %p: allocation %p + %zu bytes", p, (void*)base, size);
+  if (ipc_size_guard() && (size & (size_t(1) << 31))) {
+    set_error("IPC export of a " + std::to_string(size) +
+                  "-byte allocation refused: this HIP runtime blocks in hipIpcOpenMemHandle for sizes with bit 31 "
+                  "set (FTAR_IPC_SIZE_GUARD)",
+              __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
   out->offset = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<const char*>(base));
-  FTAR_CHECK_HIP(hipIpcGetMemHandle(&out->handle, base));
+  const hipError_t e = hipIpcGetMemHandle(&out->handle, base);
+  if (e != hipSuccess) {
+    memset(&out->handle, 0, sizeof out->handle);
+    set_error(std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e), __FILE__, __LINE__);
+    trace("ipc_export %p failed: %s", p, hipGetErrorString(e));
+    return FTAR_ERR_HIP;
+  }
+  out->valid = 1;
   return FTAR_SUCCESS;
 }
 
 ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p) {
+  if (ref.valid != 1) {
+    set_error("ipc_import: the peer's export failed", __FILE__, __LINE__);
+    return FTAR_ERR_HIP;
+  }
+  trace("ipc_import: open (offset %llu)", (unsigned long long)ref.offset);
   FTAR_CHECK_HIP(hipIpcOpenMemHandle(base, ref.handle, hipIpcMemLazyEnablePeerAccess));
   *p = static_cast<char*>(*base) + ref.offset;
+  trace("ipc_import: mapped at %p", *base);
   return FTAR_SUCCESS;
 }
 
@@ -79,7 +115,8 @@ class RcclTransport final : public Transport {
   ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
     FTAR_RETURN_IF(ensure_scratch());
     IpcRef ref;
-    FTAR_RETURN_IF(ipc_export(mine, &ref));
+    std::string why;
+    if (ipc_export(mine, &ref) != FTAR_SUCCESS) why = std::string("rank ") + std::to_string(rank) + ": " + last_error();
     std::vector<IpcRef> all(nranks);
     char* dev = static_cast<char*>(scratch_) + 256;  // nranks refs after the barrier and agreement words
     hipStream_t s;
@@ -95,33 +132,43 @@ class RcclTransport final : public Transport {
     (void)hipStreamDestroy(s);
     FTAR_RETURN_IF(st);
     peers->assign(nranks, nullptr);
-    std::string why;
-    for (int q = 0; q < nranks && why.empty(); ++q) {
-      if (q == rank) {
-        (*peers)[q] = static_cast<char*>(mine);
-        continue;
-      }
-      // one mapping per peer allocation (two registered buffers may share one),
-      // reference-counted by the pointers handed out
-      const std::string key(reinterpret_cast<const char*>(&all[q].handle), sizeof all[q].handle);
-      auto it = imports_.find(key);
-      if (it == imports_.end()) {
-        void* base = nullptr;
-        char* p = nullptr;
-        if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
-          why = std::string("rank ") + std::to_string(q) + ": " + last_error();
-          break;
-        }
-        it = imports_.emplace(key, Import{base, 0}).first;
-      }
-      ++it->second.refs;
-      (*peers)[q] = static_cast<char*>(it->second.base) + all[q].offset;
-      handed_.emplace((*peers)[q], key);
-    }
-    // every rank learns whether every rank mapped every peer: a rank that
-    // failed alone would otherwise leave the others waiting in the next barrier
+    for (int q = 0; q < nranks && why.empty(); ++q)  // a failed export anywhere: nobody opens anything
+      if (all[q].valid != 1) why = std::string("rank ") + std::to_string(q) + " could not export its buffer";
+    // The ranks open the peers' handles one rank at a time: two processes
+    // opening each other's handles at the same moment can block each other
+    // for good inside hipIpcOpenMemHandle (seen with 2 GiB buffers on ROCm 7.2
+    // dmabuf IPC, tools/peer_rehearsal.py).  Each turn ends with a host-side
+    // agreement on the failures so far, so every rank also learns whether
+    // every rank mapped every peer (a rank that failed alone would otherwise
+    // leave the others waiting in the next barrier).
     int failed = 0;
-    FTAR_RETURN_IF(agree_failures(why.empty() ? 0 : 1, &failed));
+    for (int turn = 0; turn < nranks; ++turn) {
+      if (turn == rank && why.empty()) {
+        for (int q = 0; q < nranks; ++q) {
+          if (q == rank) {
+            (*peers)[q] = static_cast<char*>(mine);
+            continue;
+          }
+          // one mapping per peer allocation (two registered buffers may share one),
+          // reference-counted by the pointers handed out
+          const std::string key(reinterpret_cast<const char*>(&all[q].handle), sizeof all[q].handle);
+          auto it = imports_.find(key);
+          if (it == imports_.end()) {
+            void* base = nullptr;
+            char* p = nullptr;
+            if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
+              why = std::string("rank ") + std::to_string(q) + ": " + last_error();
+              break;
+            }
+            it = imports_.emplace(key, Import{base, 0}).first;
+          }
+          ++it->second.refs;
+          (*peers)[q] = static_cast<char*>(it->second.base) + all[q].offset;
+          handed_.emplace((*peers)[q], key);
+        }
+      }
+      FTAR_RETURN_IF(agree_failures(why.empty() ? 0 : 1, &failed));
+    }
     if (failed) {
       unmap_peers(peers, rank);
       set_error(why.empty() ? std::to_string(failed) + " peer rank(s) could not map the exchange buffers" : why,
@@ -138,6 +185,7 @@ class RcclTransport final : public Transport {
       auto it = imports_.find(h->second);
       handed_.erase(h);
       if (it != imports_.end() && --it->second.refs == 0) {
+        trace("ipc close %p", it->second.base);
         (void)hipIpcCloseMemHandle(it->second.base);
         imports_.erase(it);
       }
@@ -161,6 +209,7 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "rccl"; }
+  bool uses_ipc() const override { return true; }
   ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) override {
     (void)rank;
     (void)nranks;
@@ -451,6 +500,7 @@ class HostTransport final : public Transport {
   ftar_status_t group_end() override { return FTAR_SUCCESS; }
   ftar_status_t allgather(const void*, void*, size_t, int, int, hipStream_t) override { return unsupported(); }
   const char* name() const override { return "host"; }
+  bool uses_ipc() const override { return true; }
   // everything before it on s, on every rank, is complete when it returns
   ftar_status_t barrier(hipStream_t s) override {
     FTAR_CHECK_HIP(hipStreamSynchronize(s));
@@ -465,34 +515,41 @@ class HostTransport final : public Transport {
     FTAR_RETURN_IF(gather(&ref, all.data(), sizeof ref));
     peers->assign(nranks, nullptr);
     int failed = exported ? 0 : 1;
-    for (int q = 0; q < nranks && !failed; ++q) {
-      if (q == rank) {
-        (*peers)[q] = static_cast<char*>(mine);
-        continue;
+    for (int q = 0; q < nranks; ++q)  // a failed export anywhere: nobody opens anything
+      if (all[q].valid != 1) failed = 1;
+    // one rank at a time opens the peers' handles (see RcclTransport::map_peers);
+    // every turn ends with an agreement on the failures so far: all map or none
+    std::vector<int> flags(nranks);
+    for (int turn = 0; turn < nranks; ++turn) {
+      for (int q = 0; q < nranks && turn == rank && !failed; ++q) {
+        if (q == rank) {
+          (*peers)[q] = static_cast<char*>(mine);
+          continue;
+        }
+        void* base = nullptr;
+        char* p = nullptr;
+        if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
+          failed = 1;
+          break;
+        }
+        (*peers)[q] = p;
+        bases_[p] = base;
       }
-      void* base = nullptr;
-      char* p = nullptr;
-      if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
-        failed = 1;
-        break;
-      }
-      (*peers)[q] = p;
-      bases_[p] = base;
+      FTAR_RETURN_IF(gather(&failed, flags.data(), sizeof failed));
+      for (int f : flags) failed |= f;
     }
-    std::vector<int> flags(nranks);  // agreed: all map or none
-    FTAR_RETURN_IF(gather(&failed, flags.data(), sizeof failed));
-    for (int f : flags)
-      if (f) {
-        unmap_peers(peers, rank);
-        set_error("host transport: a rank could not map the peers' buffers", __FILE__, __LINE__);
-        return FTAR_ERR_HIP;
-      }
+    if (failed) {
+      unmap_peers(peers, rank);
+      set_error("host transport: a rank could not map the peers' buffers", __FILE__, __LINE__);
+      return FTAR_ERR_HIP;
+    }
     return FTAR_SUCCESS;
   }
   void unmap_peers(std::vector<char*>* peers, int rank) override {
     for (int q = 0; q < (int)peers->size(); ++q) {
       auto it = q == rank ? bases_.end() : bases_.find((*peers)[q]);
       if (it == bases_.end()) continue;
+      trace("ipc close %p", it->second);
       (void)hipIpcCloseMemHandle(it->second);
       bases_.erase(it);
     }
@@ -506,6 +563,7 @@ class HostTransport final : public Transport {
     return FTAR_ERR_UNSUPPORTED;
   }
   ftar_status_t gather(const void* mine, void* all, size_t bytes) {
+    trace("host gather %zu bytes", bytes);
     if (fn_(mine, all, bytes, user_) != 0) {
       set_error("host transport: the caller's allgather failed", __FILE__, __LINE__);
       return FTAR_ERR_INTERNAL;

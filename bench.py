@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     ap.add_argument("--no-c5", action="store_true", help="N>1: skip the bf16 configs[4] line item")
     ap.add_argument("--elements-c5", dest="n_c5", type=int, default=0, help="N>1: bf16 elements (default 2^29)")
+    ap.add_argument("--host-comm", action="store_true",
+                    help="N>1 rehearsal on fewer GPUs than ranks: communicator bootstrapped over gloo "
+                         "(ftar_comm_init_host, no RCCL), ranks may share a GPU, peer-direct forms only")
     return ap.parse_args()
 
 
@@ -274,6 +277,8 @@ def bench_distributed(a):
             if state["done"]:
                 return
         sys.stderr.write(f"[bench rank {rank}] watchdog: {budget:.0f}s exceeded in phase {state['phase']}\n")
+        import faulthandler
+        faulthandler.dump_traceback(file=sys.stderr, all_threads=True)   # where every thread of this rank is
         if state["line"] is not None:
             res = dict(state["line"])
             res["watchdog"] = f"run cut at {budget:.0f}s in phase '{state['phase']}'; headline = last complete measurement"
@@ -292,9 +297,17 @@ def bench_distributed(a):
             sys.stderr.flush()
 
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
+    if a.host_comm:
+        # rehearsal: ranks share the visible GPUs, IPC peer forms over a gloo-bootstrapped communicator;
+        # exercises this whole function at P > 1 on a 1-GPU box (timings are not xGMI numbers)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
+    if a.host_comm:
+        comm = ftar.dist.init_host_comm(device=local)
+    else:
+        comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
+    base_form = "peer-read" if a.host_comm else "direct"   # the default configuration's data movement
     n = a.n or (1 << 28)
     esz = ftar.dtype_size(a.dtype)
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
@@ -386,7 +399,7 @@ def bench_distributed(a):
         yb = torch.empty_like(xb)
         t5 = ftar.topo(a.topo, a.lonely, nranks=world) if a.topo else ftar.topo_from_env(world, nb * 2)
         comm.chunk_bytes = default_chunk
-        comm.peer_direct = 0
+        comm.peer_direct = "read" if a.host_comm else 0
         comm.allgather = "direct"
         comm.reduce_scatter = "direct"
 
@@ -408,7 +421,7 @@ def bench_distributed(a):
         alg5 = nb * 2 / (ms5 * 1e-3) / 1e9
         del xb, yb
         return {"workload": f"{world}xMI355X FlexTree AllReduce, bf16 2^{nb.bit_length() - 1} elements per rank "
-                            "(BASELINE configs[4])", "topology": str(t5), "form": "direct",
+                            "(BASELINE configs[4])", "topology": str(t5), "form": base_form,
                 "chunk_bytes": default_chunk, "ms": round(ms5, 4), "value_GBps": round(world * alg5, 2),
                 "algbw_GBps_per_rank": round(alg5, 2),
                 "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
@@ -439,7 +452,9 @@ def bench_distributed(a):
                                    f"{'IPC-mapped ' + form if form.startswith('peer-') else 'RCCL p2p'} "
                                    "(BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo_),
-                       "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"},
+                       "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"
+                       + (f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), host-bootstrapped "
+                          "communicator; not an xGMI measurement)" if a.host_comm else "")},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
                          "frac": round(busbw / peak, 4), "traffic": None,
@@ -456,13 +471,13 @@ def bench_distributed(a):
     else:
         default_topo = ftar.topo_from_env(world, bucket)
     default_chunk = a.chunk_bytes or comm.chunk_bytes
-    fn_default = run_with(default_topo, default_chunk)
+    fn_default = run_with(default_topo, default_chunk, base_form)
     ms_default = timed(fn_default, a.steps, a.warmup)
     ok_default = check_y(fn_default)
-    default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": "direct",
+    default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": base_form,
                     "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
                     "check": "ok" if ok_default else "MISMATCH"}
-    state["line"] = make_result(ms_default, default_topo, default_chunk, "direct", ok_default, a.steps, a.warmup,
+    state["line"] = make_result(ms_default, default_topo, default_chunk, base_form, ok_default, a.steps, a.warmup,
                                 {"config_selection": "default (sweep not reached)", "default_config": default_info})
 
     # 2. the sweep: every factorization of P and the ring x chunk sizes x form; RCCL forms first, peer reads last
@@ -477,6 +492,8 @@ def bench_distributed(a):
             continue
         seen.add(key)
         forms = ["direct"] + (["collective"] if (not t.ring and n % world == 0) else []) + ["stages"]
+        if a.host_comm:
+            forms = []   # no point-to-point transport: the peer forms only
         for form in forms:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
@@ -552,7 +569,7 @@ def bench_distributed(a):
         for r in ok_runs:
             if r["form"] not in fam_best or r["ms"] < fam_best[r["form"]]["ms"]:
                 fam_best[r["form"]] = r
-        configs = [("default", default_topo, default_chunk, "direct")] + [
+        configs = [("default", default_topo, default_chunk, base_form)] + [
             (f"best {fam}", ftar.topo("1" if r["topology"] == "ring" else r["topology"]), r["chunk_bytes"], fam)
             for fam, r in sorted(fam_best.items())]
         phases = {}

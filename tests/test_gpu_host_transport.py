@@ -93,3 +93,65 @@ def test_peer_forms_across_processes(world):
             for r in range(world):
                 assert res[r][key] == ref[r].tobytes(), (world, key, r)
     assert all(res[r]["p2p"] == 2 for r in range(world)), [res[r]["p2p"] for r in range(world)]
+
+
+def _big_worker(rank, world, port, n, q):
+    """Exchange-buffer growth across the 2 GiB line (tools/peer_rehearsal.py): the write form at n = 2^28 fp32
+    needs a 2 GiB exchange buffer, and torch's HIP 7.0 runtime blocks forever in hipIpcOpenMemHandle for
+    allocations whose size has bit 31 set; the buffer is sized around that (ipc_safe_size)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ftar
+    import ftar.dist
+    out = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        comm = ftar.dist.init_host_comm(device=0)
+        x = torch.full((n,), float(rank + 1), device="cuda")
+        y = torch.empty_like(x)
+        for mode in ("read", "write"):
+            comm.peer_direct = mode
+            comm.allreduce(x, y, n, "f32", "sum", topo_="1")
+            torch.cuda.synchronize()
+            out[mode] = bool((y == float(world * (world + 1) // 2)).all())
+            y.zero_()
+        # a 2 GiB registration is refused on every rank alike (no hang) where the runtime is affected
+        big = torch.empty(1 << 29, dtype=torch.float32, device="cuda")
+        try:
+            r = comm.register(big, big.numel() * 4)
+            comm.deregister(r)
+            out["reg2g"] = "registered"
+        except ftar.FtarError as e:
+            out["reg2g"] = e.status
+        comm.destroy()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        out["error"] = repr(e)
+    q.put((rank, out))
+
+
+def test_exchange_buffer_past_2gib():
+    import torch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    ps = [ctx.Process(target=_big_worker, args=(r, world, port, 1 << 28, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["read"] and res[r]["write"], res[r]
+    # agreed across ranks: both registered, or both refused with FTAR_ERR_HIP (the guard's agreed failure)
+    assert res[0]["reg2g"] == res[1]["reg2g"], res
+    affected = int(torch.version.hip.split(".")[0]) * 100 + int(torch.version.hip.split(".")[1]) < 702
+    if affected and os.environ.get("FTAR_IPC_SIZE_GUARD", "") != "0":
+        assert res[0]["reg2g"] != "registered", res
