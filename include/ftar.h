@@ -210,7 +210,10 @@ ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode);
  * copy; WRITE (recvbuf registered) pushes final blocks straight into the
  * peers' outputs, two barriers, no copy.  Mixing registered and unregistered
  * buffers across ranks in one call is undefined.  deregister is local; the
- * buffer must not be freed before it (or before the calls using it ended). */
+ * buffer must not be freed before it (or before the calls using it ended).
+ * Under HIP runtimes older than 7.2 an allocation whose size has bit 31 set
+ * cannot be registered (FTAR_ERR_HIP on every rank): those runtimes block in
+ * hipIpcOpenMemHandle for such sizes.  FTAR_IPC_SIZE_GUARD=0|1 overrides. */
 ftar_status_t ftar_comm_register(ftar_comm_t comm, void* buf, size_t bytes, int* reg);
 ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg);
 
