@@ -13,7 +13,7 @@
 //     (streamed once), stores do not (the next ring step sends that block);
 //     one-shot grid of ceil(nvec / 512) workgroups of 256 (>> 256 CUs);
 //   * source pointers travel in the kernarg segment (no device-side pointer
-//     table, no extra dependent load); K is a template parameter for 2..8;
+//     table, no extra dependent load); K is a template parameter for 2..16;
 //   * unaligned heads/tails (block offsets need not be 16-B aligned) are done
 //     element-wise by workgroup 0 in the same launch; sources whose alignment
 //     differs from dst's take a dword-granular kernel instead;
@@ -42,17 +42,20 @@ constexpr int kTreeLevels = kMaxFoldLevels;
 //    stores; rewriting the same destination back to back -- the reference
 //    harness's loop -- favours plain stores instead, because the MALL absorbs
 //    part of the writes, a regime the hot path never sees);
-//  * k = 2..8: staged through LDS (LDS-DMA): every wave streams U tiles of 1 KiB
+//  * k = 2..16 (fp32/bf16; 2..8 for the other types): staged through LDS (LDS-DMA): every wave streams U tiles of 1 KiB
 //    per source into LDS with global_load_lds_dwordx4 (no VGPR landing zone),
 //    waits on its own vmcnt and folds from LDS -- f32 +1 % at k = 2 and +3-5 %
 //    at k = 4..8 over the best register variant with U = 4; 16-bit sums (more
-//    ALU per byte) keep occupancy with fewer tiles as k grows;
-//  * k > 8 (runtime k): registers, 2 vectors per lane, 512-thread workgroups.
+//    ALU per byte) keep occupancy with fewer tiles as k grows, and so does
+//    every type past k = 9 (LDS holds 4 waves x k x U KiB <= 160 KiB);
+//  * larger k (runtime k): registers, 2 vectors per lane, 512-thread workgroups.
 constexpr int kUnroll = 2;
 constexpr int kVecThreads = 512;
 constexpr bool kNtLoads = true, kNtStores = true;
 template <class Tr, int K>
-constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? 4 : (K <= 4 ? 4 : (K <= 6 ? 3 : 2));
+constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? (K <= 8 ? 4 : 2)
+                                                     : (K <= 4 ? 4 : (K <= 6 ? 3 : 2));
+// LDS per workgroup = 4 waves x K x U x 1 KiB (<= 160 KiB): k = 16 at U = 2 stages 128 KiB
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -299,7 +302,7 @@ __global__ void __launch_bounds__(BS)
   }
 }
 
-// LDS-staged reduce: the production kernel for k = 2..8 (launch_k; A/B
+// LDS-staged reduce: the production kernel for k = 2..16 (launch_k; A/B
 // variants 20/21/31-33 in tools/kbench_cold.py).  Each wave streams U tiles of
 // every source into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
 // instruction, nontemporal, no VGPR destination), waits on its own vmcnt, then
@@ -704,6 +707,14 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
       case 6: return launch_k<Tr, 6>(srcs, k, dst, nvec, (int)head, (int)tail, s);
       case 7: return launch_k<Tr, 7>(srcs, k, dst, nvec, (int)head, (int)tail, s);
       case 8: return launch_k<Tr, 8>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 9: return launch_k<Tr, 9>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 10: return launch_k<Tr, 10>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 11: return launch_k<Tr, 11>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 12: return launch_k<Tr, 12>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 13: return launch_k<Tr, 13>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 14: return launch_k<Tr, 14>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 15: return launch_k<Tr, 15>(srcs, k, dst, nvec, (int)head, (int)tail, s);
+      case 16: return launch_k<Tr, 16>(srcs, k, dst, nvec, (int)head, (int)tail, s);
       default: break;
     }
   } else if (k == 2) {
