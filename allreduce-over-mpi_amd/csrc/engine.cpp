@@ -40,6 +40,9 @@ struct ftar_comm {
   size_t chunk_bytes = 0;
   size_t host_chunk_bytes = 0;
   int peer_direct = 0;             // FTAR_PEER_DIRECT / ftar_comm_set_peer_direct: 0 off, 1 read, 2 write
+  // peer-form tuning (ftar_debug_set_peer_tuning; bench.py sweeps both on a
+  // real node): nontemporal copies, LDS-staged fold (false: register kernel)
+  bool peer_nt = true, peer_lds = true;
   void* xbuf = nullptr;            // peer-direct exchange buffer (IPC-exported), grow-only
   size_t xbuf_bytes = 0;
   std::vector<char*> xpeers;       // every rank's exchange buffer, mapped here
@@ -242,7 +245,7 @@ ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
 // the plan's fold of my block with operand i read from where(i)
 template <class Where>
 ftar_status_t peer_fold(const ReduceItem& r, const Plan& plan, ftar_dtype_t dt, ftar_op_t op, void* dst,
-                        hipStream_t s, Where where) {
+                        hipStream_t s, bool lds, Where where) {
   std::map<size_t, int> slot_peer;  // scratch slot -> the rank that would have sent it
   for (const Transfer& x : plan.stages[0].recvs) slot_peer[x.off] = x.peer;
   std::vector<const void*> srcs;
@@ -256,7 +259,7 @@ ftar_status_t peer_fold(const ReduceItem& r, const Plan& plan, ftar_dtype_t dt, 
     }
   }
   return launch_reduce(srcs.data(), (int)srcs.size(), dst, r.len, dt, op, s, r.round_each, r.shape.data(),
-                       (int)r.shape.size());
+                       (int)r.shape.size(), lds);
 }
 }  // namespace
 
@@ -303,7 +306,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     FTAR_RETURN_IF(tp->barrier(c->comm_s));  // every rank's input is ready
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const ReduceItem& r : rs.reduces)
-      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, c->peer_lds, [&](int q, size_t off) -> const void* {
         return q < 0 ? in + off * esz : reg_peer(rin, in, q) + off * esz;  // that rank's input, in place
       }));
     FTAR_RETURN_IF(mark(c, "fold (remote reads)", c->comm_s));
@@ -311,18 +314,18 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const Transfer& x : ag.recvs)
       segs.push_back({reg_peer(rout, out, x.peer) + x.off * esz, out + x.off * esz, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
     FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my buffers after the call
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   } else if (!write) {
     const Segment whole{in, X, bytes};
-    FTAR_RETURN_IF(launch_gather(&whole, 1, c->comm_s));
+    FTAR_RETURN_IF(launch_gather(&whole, 1, c->comm_s, c->peer_nt));
     FTAR_RETURN_IF(mark(c, "copy-in", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const ReduceItem& r : rs.reduces)
-      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, X + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, X + r.off * esz, c->comm_s, c->peer_lds, [&](int q, size_t off) -> const void* {
         return q < 0 ? X + off * esz : Xq[q] + off * esz;  // that rank's copy of this block
       }));
     FTAR_RETURN_IF(mark(c, "fold (remote reads)", c->comm_s));
@@ -331,7 +334,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     // all-gather: every owner's final block from its exchange buffer, one launch
     for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, out + r.off * esz, r.len * esz});
     for (const Transfer& x : ag.recvs) segs.push_back({Xq[x.peer] + x.off * esz, out + x.off * esz, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
     FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -339,12 +342,12 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     // scatter my copy of every peer's block into its slot for me, all links at once
     for (const Transfer& x : rs.sends)
       segs.push_back({in + x.off * esz, Xq[x.peer] + (size_t)c->rank * slot_bytes, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
     FTAR_RETURN_IF(mark(c, "scatter (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const ReduceItem& r : rs.reduces)
-      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, [&](int q, size_t off) -> const void* {
+      FTAR_RETURN_IF(peer_fold(r, plan, dt, op, out + r.off * esz, c->comm_s, c->peer_lds, [&](int q, size_t off) -> const void* {
         return q < 0 ? in + off * esz : X + (size_t)q * slot_bytes;  // rank q's copy, pushed into slot q
       }));
     FTAR_RETURN_IF(mark(c, "fold (local)", c->comm_s));
@@ -352,14 +355,14 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     for (const Transfer& x : ag.sends)
       segs.push_back({out + x.off * esz, (zc ? reg_peer(rout, out, x.peer) : Xq[x.peer] + final_at) + x.off * esz,
                       x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
     FTAR_RETURN_IF(mark(c, "push (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     if (!zc) {
       segs.clear();
       for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
-      FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s));
+      FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
       FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
     }
   }
@@ -891,6 +894,16 @@ ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode) {
   if (!comm || mode < FTAR_PEER_OFF || mode > FTAR_PEER_WRITE) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   comm->peer_direct = mode;
+  return FTAR_SUCCESS;
+}
+
+// Test/tuning hook (not in ftar.h): peer-form copies nontemporal (nt) or not,
+// fold through the LDS-staged kernel (lds) or the register kernel.
+ftar_status_t ftar_debug_set_peer_tuning(ftar_comm_t comm, int nt, int lds) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->peer_nt = nt != 0;
+  comm->peer_lds = lds != 0;
   return FTAR_SUCCESS;
 }
 

@@ -111,7 +111,7 @@ ftar_status_t check_world(const Topology& t, int nranks, size_t count, Form form
 constexpr int kMaxFoldLevels = 4;
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
                             hipStream_t stream, bool round_each = false, const int* shape = nullptr,
-                            int nlevels = 0);
+                            int nlevels = 0, bool lds = true);
 bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op);
 // dst_i[0..bytes_i) = src_i[0..bytes_i) for up to FTAR_MAX_K segments in one
 // launch (the peer-direct all-gather: each segment pulls one rank's block).

@@ -827,7 +827,7 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, 
 }
 
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                            hipStream_t s, bool round_each, const int* shape, int nlevels) {
+                            hipStream_t s, bool round_each, const int* shape, int nlevels, bool lds) {
   if (k < 1 || k > FTAR_MAX_K || !srcs || !dst) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
   if (count == 0) return FTAR_SUCCESS;
@@ -852,10 +852,10 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   }
   if (op == FTAR_SUM) {
     switch (dt) {
-      case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, true); break;
+      case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, lds); break;
       case FTAR_BFLOAT16:
-        e = round_each && k > 2 ? launch_tr<BF16SumHop>(srcs, k, dst, count, s, true)
-                                : launch_tr<BF16Sum>(srcs, k, dst, count, s, true);
+        e = round_each && k > 2 ? launch_tr<BF16SumHop>(srcs, k, dst, count, s, lds)
+                                : launch_tr<BF16Sum>(srcs, k, dst, count, s, lds);
         break;
       case FTAR_FLOAT64: e = launch_tr<F64Sum>(srcs, k, dst, count, s, false); break;
       case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum>(srcs, k, dst, count, s, false); break;

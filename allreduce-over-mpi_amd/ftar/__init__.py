@@ -109,6 +109,7 @@ _lib.ftar_allreduce_host.argtypes = [_vp, _vp, _sz, _int, _int, ctypes.POINTER(T
 _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_vp), _sz, _int, _int,
                                            ctypes.POINTER(Topo), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
+_lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_comm_set_phase_timing.argtypes = [_vp, _int]
@@ -374,6 +375,11 @@ class Comm:
     @peer_direct.setter
     def peer_direct(self, mode):
         _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
+
+    def peer_tuning(self, nt=True, lds=True):
+        """Peer forms: nontemporal copies (nt) and the LDS-staged fold (lds; False = register kernel).
+        Tuning hook for bench.py's sweep (ftar_debug_set_peer_tuning); results are identical either way."""
+        _check(_lib.ftar_debug_set_peer_tuning(self.handle, 1 if nt else 0, 1 if lds else 0), "peer_tuning")
 
     def register(self, buf, nbytes):
         """Collective: register this rank's buffer (device pointer or tensor) for the peer forms' in-place
