@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     ap.add_argument("--no-c5", action="store_true", help="N>1: skip the bf16 configs[4] line item")
     ap.add_argument("--elements-c5", dest="n_c5", type=int, default=0, help="N>1: bf16 elements (default 2^29)")
+    ap.add_argument("--no-host", action="store_true", help="N>1: skip the host-memory end-to-end line item")
     ap.add_argument("--host-comm", action="store_true",
                     help="N>1 rehearsal on fewer GPUs than ranks: communicator bootstrapped over gloo "
                          "(ftar_comm_init_host, no RCCL), ranks may share a GPU, peer-direct forms only")
@@ -430,6 +431,34 @@ def bench_distributed(a):
                 "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
                 "check": "ok" if bool(flag.item()) else "MISMATCH"}
 
+    def measure_host():
+        """The reference's setting: the bucket lives in host memory (MPI send/recv buffers,
+        benchmark.cpp:125-131).  Pinned host buckets through ftar_allreduce_host -- H2D, the exchange and D2H
+        pipelined per piece -- with the default topology; the same plan gives the device path's bits."""
+        hx = x.cpu().pin_memory()
+        hy = torch.empty_like(hx).pin_memory()
+        comm.chunk_bytes = default_chunk
+        comm.peer_direct = 0
+        comm.allgather = "direct"
+        comm.reduce_scatter = "direct"
+        comm.peer_tuning()
+
+        def fnh():
+            comm.allreduce_host(hx, hy, n, a.dtype, "sum", topo_=default_topo, stream=stream)
+        msh = timed(fnh, min(a.steps, 5), 1)
+        fn_default()   # the device path on the same inputs: y
+        torch.cuda.synchronize()
+        ic = idx.cpu()
+        same = torch.tensor([1 if torch.equal(hy[ic], y[idx].cpu()) else 0], dtype=torch.int32)
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        alg = bucket / (msh * 1e-3) / 1e9
+        del hx, hy
+        return {"workload": f"{world}xMI355X host-memory AllReduce (pinned buckets, H2D + exchange + D2H "
+                            "pipelined; ftar_allreduce_host, the MPI_Allreduce_FT path)",
+                "topology": str(default_topo), "ms": round(msh, 4), "value_GBps": round(world * alg, 2),
+                "algbw_GBps_per_rank": round(alg, 2),
+                "check": "bit-identical to the device path" if same.item() else "MISMATCH"}
+
     def bws(m):
         alg = bucket / (m * 1e-3) / 1e9
         return alg, (alg * 2 * (world - 1) / world if world > 1 else alg)
@@ -629,6 +658,14 @@ def bench_distributed(a):
             state["line"]["c5_bf16"] = measure_c5()
         except Exception as e:  # noqa: BLE001
             state["line"]["c5_bf16"] = {"error": str(e)[:200]}
+
+    # 6. the host-memory end-to-end rate: PCIe in and out included, never the headline
+    phase("host e2e")
+    if not a.no_host:
+        try:
+            state["line"]["host_e2e"] = measure_host()
+        except Exception as e:  # noqa: BLE001
+            state["line"]["host_e2e"] = {"error": str(e)[:200]}
 
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
