@@ -298,16 +298,32 @@ def bench_distributed(a):
             sys.stderr.flush()
 
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
-    if a.host_comm:
+    if a.host_comm or world > torch.cuda.device_count():
         # rehearsal: ranks share the visible GPUs, IPC peer forms over a gloo-bootstrapped communicator;
-        # exercises this whole function at P > 1 on a 1-GPU box (timings are not xGMI numbers)
+        # exercises this whole function at P > 1 on a 1-GPU box (timings are not xGMI numbers).  Without
+        # --host-comm RCCL refuses the shared GPU and the run takes the fallback below.
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if a.host_comm:
+    comm, rccl_error = None, None
+    if not a.host_comm:
+        try:
+            comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
+        except Exception as e:  # noqa: BLE001
+            rccl_error = str(e)[:200]
+        ok = torch.tensor([0 if rccl_error else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank takes the same path
+        if not ok.item():
+            # RCCL could not come up on some rank: the peer forms over a gloo-bootstrapped communicator still
+            # move the data over xGMI (IPC), so the run keeps a measured line
+            if comm is not None:
+                comm.destroy()
+                comm = None
+            sys.stderr.write(f"[bench rank {rank}] RCCL communicator failed ({rccl_error or 'on another rank'}); "
+                             "falling back to the host-bootstrapped peer forms\n")
+            a.host_comm = True
+    if comm is None:
         comm = ftar.dist.init_host_comm(device=local)
-    else:
-        comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
     base_form = "peer-read" if a.host_comm else "direct"   # the default configuration's data movement
     n = a.n or (1 << 28)
     esz = ftar.dtype_size(a.dtype)
@@ -486,13 +502,16 @@ def bench_distributed(a):
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo_),
                        "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"
                        + (f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), host-bootstrapped "
-                          "communicator; not an xGMI measurement)" if a.host_comm else "")},
+                          "communicator; not an xGMI measurement)" if a.host_comm and world > torch.cuda.device_count()
+                          else " (host-bootstrapped communicator: RCCL failed to initialise)" if a.host_comm else "")},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
                          "frac": round(busbw / peak, 4), "traffic": None,
                          "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
             "check": "ok" if ok else "MISMATCH",
         }
+        if rccl_error:
+            res["rccl_init_error"] = rccl_error
         res.update(extra)
         return res
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: smoke, GPU tests, bench, rocprof. Every GPU step has its
 # own time limit; a fault/abort/timeout (exit >= 124) stops the script there.
-# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host dist1 dist2h dist4h
+# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host dist1 dist2h dist4h dist2f peer2
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -33,6 +33,7 @@ for s in "${steps[@]}"; do
     hosttrace) run hosttrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/htrace -o run -- python3 tools/engine_trace.py --host --ranks 2 --topo 2 --elements 268435456 --host-chunk-bytes 4194304 --iters 2 ;;
     dist2h) FTAR_BENCH_BUDGET_S=150 run dist2h 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --host-comm --steps 5 --warmup 2 ;;
     dist4h) FTAR_BENCH_BUDGET_S=150 run dist4h 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29535 bench.py --host-comm --steps 5 --warmup 2 ;;
+    dist2f) FTAR_BENCH_BUDGET_S=150 run dist2f 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29537 bench.py --steps 5 --warmup 2 ;;
     peer2) run peer2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29536 tools/peer_rehearsal.py ;;
     dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
