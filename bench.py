@@ -439,13 +439,27 @@ def bench_distributed(a):
         flag = torch.tensor([1 if ok5 else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         alg5 = nb * 2 / (ms5 * 1e-3) / 1e9
+        # the other widths the cost model weighed (every ordered factorization of P, and the ring), a few
+        # timed calls each with the same data movement: does its choice hold on this node?
+        widths = {}
+        for tp in ["1"] + [",".join(map(str, f)) for f in _factorizations(world)]:
+            tw = ftar.topo(tp)
+            if str(tw) == str(t5) or world < 2:
+                continue
+            try:
+                mw = timed(lambda: comm.allreduce(xb, yb, nb, "bf16", "sum", topo_=tw, stream=stream), 3, 1)
+                widths[str(tw)] = {"ms": round(mw, 4), "cost_model_s": round(ftar.topo_cost(tw, world, nb * 2), 6)}
+            except Exception as e:  # noqa: BLE001
+                widths[str(tw)] = {"error": str(e)[:120]}
         del xb, yb
         return {"workload": f"{world}xMI355X FlexTree AllReduce, bf16 2^{nb.bit_length() - 1} elements per rank "
                             "(BASELINE configs[4])", "topology": str(t5), "form": base_form,
                 "chunk_bytes": default_chunk, "ms": round(ms5, 4), "value_GBps": round(world * alg5, 2),
                 "algbw_GBps_per_rank": round(alg5, 2),
                 "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
-                "check": "ok" if bool(flag.item()) else "MISMATCH"}
+                "check": "ok" if bool(flag.item()) else "MISMATCH",
+                "cost_model_s": round(ftar.topo_cost(t5, world, nb * 2), 6),
+                "other_widths": widths}
 
     def measure_host():
         """The reference's setting: the bucket lives in host memory (MPI send/recv buffers,
