@@ -373,7 +373,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
 
 // xGMI probe (diagnostic, collective): every rank runs the same copy pattern
 // at the same time between barriers, timed with events on the comm stream.
-ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int nout) {
+ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int nout, size_t max_wg_per_seg) {
   const int P = c->nranks, me = c->rank;
   FTAR_RETURN_IF(ensure_xbuf(c, 2 * (size_t)P * bytes));  // P send slots + P receive slots
   Transport* tp = c->tp.get();
@@ -399,10 +399,11 @@ ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int
     }
     out[mode] = 0.0;
     if (segs.empty()) continue;
-    if ((st = launch_gather(segs.data(), (int)segs.size(), c->comm_s)) != FTAR_SUCCESS) break;  // warm
+    if ((st = launch_gather(segs.data(), (int)segs.size(), c->comm_s, true, max_wg_per_seg)) != FTAR_SUCCESS) break;  // warm
     if ((st = tp->barrier(c->comm_s)) != FTAR_SUCCESS) break;
     if (hipEventRecord(e0, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
-    for (int i = 0; i < iters && st == FTAR_SUCCESS; ++i) st = launch_gather(segs.data(), (int)segs.size(), c->comm_s);
+    for (int i = 0; i < iters && st == FTAR_SUCCESS; ++i)
+      st = launch_gather(segs.data(), (int)segs.size(), c->comm_s, true, max_wg_per_seg);
     if (st == FTAR_SUCCESS && hipEventRecord(e1, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
     if (st == FTAR_SUCCESS) st = tp->barrier(c->comm_s);
     if (st == FTAR_SUCCESS && hipStreamSynchronize(c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
@@ -974,7 +975,17 @@ ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters
   if (!comm || !gbps || n <= 0 || iters <= 0 || bytes_per_peer == 0) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   FTAR_CHECK_HIP(hipSetDevice(comm->device));
-  return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n);
+  return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n, 0);
+}
+
+// Test/tuning hook (not in ftar.h): the probe with at most wg_per_peer
+// workgroups of 256 threads per peer segment -- how many CUs saturate xGMI.
+ftar_status_t ftar_debug_xgmi_probe_cap(ftar_comm_t comm, size_t bytes_per_peer, int iters, size_t wg_per_peer,
+                                        double* gbps, int n) {
+  if (!comm || !gbps || n <= 0 || iters <= 0 || bytes_per_peer == 0) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n, wg_per_peer);
 }
 
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {

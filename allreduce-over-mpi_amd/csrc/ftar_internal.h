@@ -122,7 +122,8 @@ struct Segment {
 };
 // nt: nontemporal loads and stores (the default: cold copies, data not
 // re-read soon); false keeps both in the caches.
-ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true);
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true,
+                            size_t max_wg_per_seg = 0);  // 0: enough workgroups for one pass
 size_t dtype_size(ftar_dtype_t dt);
 
 // ---------------------------------------------------------------------------

@@ -802,7 +802,7 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
   return false;
 }
 
-ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt) {
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt, size_t max_wg_per_seg) {
   if (nsegs < 0 || nsegs > FTAR_MAX_K) return FTAR_ERR_INVALID_ARG;
   SegArgs a{};
   int m = 0;
@@ -818,6 +818,7 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, 
   if (!m) return FTAR_SUCCESS;
   size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
   bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
+  if (max_wg_per_seg) bx = std::min(bx, max_wg_per_seg);
   if (nt)
     hipLaunchKernelGGL(gather_kernel<true>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
   else

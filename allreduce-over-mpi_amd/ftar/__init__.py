@@ -112,6 +112,7 @@ _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
+_lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_comm_set_phase_timing.argtypes = [_vp, _int]
 _lib.ftar_comm_register.argtypes = [_vp, _vp, _sz, ctypes.POINTER(_int)]
 _HOST_ALLGATHER = ctypes.CFUNCTYPE(_int, _vp, _vp, _sz, _vp)
@@ -404,11 +405,16 @@ class Comm:
         _lib.ftar_comm_phase_json(self.handle, buf, n + 1)
         return [tuple(p) for p in json.loads(buf.value.decode())]
 
-    def xgmi_probe(self, bytes_per_peer=64 << 20, iters=10):
+    def xgmi_probe(self, bytes_per_peer=64 << 20, iters=10, wg_per_peer=0):
         """Collective xGMI calibration (ftar_xgmi_probe): GB/s of copy kernels through the exchange buffers,
-        every rank running the same pattern at once."""
+        every rank running the same pattern at once.  wg_per_peer > 0 caps the copy kernel at that many
+        256-thread workgroups per peer (how many CUs it takes to fill the links)."""
         out = (ctypes.c_double * 5)()
-        _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, 5), "ftar_xgmi_probe")
+        if wg_per_peer:
+            _check(_lib.ftar_debug_xgmi_probe_cap(self.handle, bytes_per_peer, iters, wg_per_peer, out, 5),
+                   "ftar_debug_xgmi_probe_cap")
+        else:
+            _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, 5), "ftar_xgmi_probe")
         return dict(zip(("local_copy", "read_one_peer", "read_all_peers", "write_one_peer", "write_all_peers"),
                         (round(v, 2) for v in out)))
 

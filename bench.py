@@ -590,6 +590,14 @@ def bench_distributed(a):
                                                     for i, k in enumerate(pr)}
                 state["line"]["xgmi_probe_GBps"]["note"] = ("[min, max] over ranks; 64 MiB per peer per copy, "
                                                             "10 launches, all ranks at once")
+                # how many CUs fill the links: the same copies capped at w workgroups (256 threads) per peer
+                by_cap = {}
+                for w in (4, 8, 16, 32, 64):
+                    pc = comm.xgmi_probe(64 << 20, iters=5, wg_per_peer=w)
+                    v = torch.tensor([pc["read_all_peers"], pc["write_all_peers"]], dtype=torch.float64)
+                    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+                    by_cap[w] = {"read_all_peers": round(v[0].item(), 1), "write_all_peers": round(v[1].item(), 1)}
+                state["line"]["xgmi_probe_GBps"]["by_workgroups_per_peer"] = by_cap
             except Exception as e:  # noqa: BLE001
                 state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
         stop = torch.tensor([1 if time.time() - sweep_t0 > sweep_budget else 0], dtype=torch.int32)
