@@ -564,6 +564,19 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
   }
+  if (host && c->peer_direct && peer_eligible(plan)) {
+    // host buffers over the peer forms (e.g. a communicator bootstrapped over
+    // MPI with no RCCL, ftar_comm_init_host): the whole bucket in, the peer
+    // exchange in HBM, the whole bucket out -- same plan, same bits, not
+    // pipelined piece by piece like the p2p path below
+    const size_t bytes = count * esz;
+    FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
+    FTAR_CHECK_HIP(hipMemcpyAsync(c->staging, host->src, bytes, hipMemcpyHostToDevice, stream));
+    FTAR_RETURN_IF(grow_events(c, 5));
+    FTAR_RETURN_IF(peer_allreduce(nullptr, c->staging, count, dt, op, plan, c, stream));
+    FTAR_CHECK_HIP(hipMemcpyAsync(host->dst, c->staging, bytes, hipMemcpyDeviceToHost, stream));
+    return FTAR_SUCCESS;
+  }
 
   // Host mode: the buffers are in host memory and move through a device
   // staging buffer, piece by piece, so H2D (PCIe in), the exchange, and D2H

@@ -10,7 +10,8 @@
 //   ring/tree over MPI_Isend/Irecv          ftar_allreduce_host: H2D, RCCL p2p + HIP reduce and
 //   + 14-thread OpenMP reduce               D2H pipelined piece by piece (PCIe in and out overlap)
 //   MPI_Comm_split every call, leaked       nothing per call; RCCL comm built once
-//   (:1541-1548)
+//   (:1541-1548)                            (or, FTAR_MPI_TRANSPORT=ipc / RCCL failing, a
+//                                           communicator bootstrapped over MPI: peer forms)
 // The caller's buffers are page-locked on first use (hipHostRegister, cached)
 // so the copies run at PCIe DMA speed; set FTAR_MPI_REGISTER=0 to disable.
 #include <hip/hip_runtime_api.h>
@@ -19,6 +20,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <string>
 #include <utility>
 
 #include "ftar_mpi.h"
@@ -29,6 +31,8 @@ struct Entry {
   ftar_comm_t comm = nullptr;
   int rank = 0, size = 1, device = 0;
   hipStream_t stream = nullptr;
+  MPI_Comm boot = MPI_COMM_NULL;  // ipc transport: the duplicate the communicator bootstraps over
+  bool ipc = false;
 };
 
 std::mutex g_mu;
@@ -48,26 +52,65 @@ int pick_device(MPI_Comm comm) {
   return local % n;
 }
 
+// the host collective of an ipc-transport communicator (ftar_comm_init_host)
+int mpi_allgather(const void* mine, void* all, size_t bytes, void* user) {
+  MPI_Comm c = *static_cast<MPI_Comm*>(user);
+  return MPI_Allgather(mine, (int)bytes, MPI_BYTE, all, (int)bytes, MPI_BYTE, c) == MPI_SUCCESS ? 0 : 1;
+}
+
+// FTAR_MPI_TRANSPORT: rccl (RCCL p2p, every form), ipc (a communicator
+// bootstrapped over MPI itself: the peer-direct read form over IPC-mapped
+// buffers, no RCCL), auto (default: RCCL, and ipc on every rank when the RCCL
+// communicator fails to come up on any rank -- e.g. ranks sharing a GPU)
 int entry_for(MPI_Comm comm, Entry** out) {
   auto it = g_entries.find(comm);
   if (it != g_entries.end()) {
     *out = &it->second;
     return MPI_SUCCESS;
   }
-  Entry e;
+  Entry& e = g_entries.emplace(comm, Entry{}).first->second;  // stable address: `boot` is the callback's state
+  auto fail = [&](int rc) {
+    if (e.boot != MPI_COMM_NULL) MPI_Comm_free(&e.boot);
+    g_entries.erase(comm);
+    return rc;
+  };
   MPI_Comm_rank(comm, &e.rank);
   MPI_Comm_size(comm, &e.size);
   e.device = pick_device(comm);
   if (e.size > 1) {
-    ftar_unique_id_t id;
-    memset(&id, 0, sizeof id);
-    int ok = e.rank == 0 ? ftar_get_unique_id(&id) == FTAR_SUCCESS : 1;
-    MPI_Bcast(&ok, 1, MPI_INT, 0, comm);
-    if (!ok) return MPI_ERR_OTHER;
-    MPI_Bcast(&id, (int)sizeof id, MPI_BYTE, 0, comm);
-    if (ftar_comm_init_rank(&e.comm, e.size, id, e.rank, e.device) != FTAR_SUCCESS) return MPI_ERR_OTHER;
+    const char* m = getenv("FTAR_MPI_TRANSPORT");
+    const std::string mode = m && *m ? m : "auto";
+    if (mode != "rccl" && mode != "ipc" && mode != "auto") return fail(MPI_ERR_ARG);
+    int rccl_ok = 0;
+    if (mode != "ipc") {
+      ftar_unique_id_t id;
+      memset(&id, 0, sizeof id);
+      int ok = e.rank == 0 ? ftar_get_unique_id(&id) == FTAR_SUCCESS : 1;
+      MPI_Bcast(&ok, 1, MPI_INT, 0, comm);
+      if (ok) {
+        MPI_Bcast(&id, (int)sizeof id, MPI_BYTE, 0, comm);
+        rccl_ok = ftar_comm_init_rank(&e.comm, e.size, id, e.rank, e.device) == FTAR_SUCCESS;
+      }
+      int all_ok = rccl_ok;
+      MPI_Allreduce(&rccl_ok, &all_ok, 1, MPI_INT, MPI_MIN, comm);  // every rank takes the same path
+      if (!all_ok && e.comm) {
+        ftar_comm_destroy(e.comm);
+        e.comm = nullptr;
+      }
+      rccl_ok = all_ok;
+      if (!rccl_ok && mode == "rccl") return fail(MPI_ERR_OTHER);
+    }
+    if (!rccl_ok) {
+      if (MPI_Comm_dup(comm, &e.boot) != MPI_SUCCESS) return fail(MPI_ERR_OTHER);
+      if (ftar_comm_init_host(&e.comm, e.size, e.rank, e.device, mpi_allgather, &e.boot) != FTAR_SUCCESS)
+        return fail(MPI_ERR_OTHER);
+      int pd = 0;
+      if (ftar_comm_get_peer_direct(e.comm, &pd) == FTAR_SUCCESS && pd == 0)
+        (void)ftar_comm_set_peer_direct(e.comm, FTAR_PEER_READ);
+      e.ipc = true;
+    }
   }
-  *out = &g_entries.emplace(comm, e).first->second;
+  *out = &e;
   return MPI_SUCCESS;
 }
 
@@ -187,6 +230,7 @@ int MPI_Allreduce_FT_finalize(void) {
     if (e.stream) (void)hipStreamSynchronize(e.stream);
     if (e.comm) ftar_comm_destroy(e.comm);
     if (e.stream) (void)hipStreamDestroy(e.stream);
+    if (e.boot != MPI_COMM_NULL) MPI_Comm_free(&e.boot);
   }
   g_entries.clear();
   for (auto& kv : g_registered) (void)hipHostUnregister(kv.first);

@@ -14,6 +14,10 @@
  * re-fitted cost model instead of the reference's exit(1)).  Underneath:
  * one GPU per rank (node-local rank % visible devices, or FTAR_DEVICE),
  * H2D -> device AllReduce (RCCL p2p over xGMI + HIP reduce kernel) -> D2H.
+ * FTAR_MPI_TRANSPORT=auto (default) | rccl | ipc: ipc bootstraps over `comm`
+ * itself (MPI_Allgather) and moves blocks with kernel loads through
+ * IPC-mapped buffers, no RCCL; auto takes it on every rank when RCCL cannot
+ * initialise on some rank (e.g. ranks sharing a GPU).
  * Results are bit-identical to the reference for the same FT_TOPO.
  *
  * Errors: the reference always returns 0 and exit(1)s on bad input

@@ -56,3 +56,24 @@ def test_harness_device_resident_single_rank(tmp_path):
     rc, out = run(1, ["--size", "1048576", "--repeat", "3", "--warmup", "1", "--check", "--device"], tmp_path)
     assert rc == 0, out
     assert "(test passed)" in out and '"resident":"device"' in out
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,extra", [(2, "2", []), (2, "1", []), (4, "2,2", []), (4, "4", ["--device"]),
+                                              (2, "2", ["--to-file", "--tag", "ipc"])])
+def test_harness_ranks_sharing_a_gpu_fall_back_to_ipc(tmp_path, ranks, topo, extra):
+    """MPI_Allreduce_FT with several MPI ranks on the box's one GPU: RCCL refuses ranks that share a device,
+    every rank agrees to fall back (FTAR_MPI_TRANSPORT=auto) to a communicator bootstrapped over MPI itself,
+    and the peer-direct read form moves the blocks through IPC-mapped buffers -- the whole drop-in path
+    (host buffers, H2D, exchange, D2H) across real processes, checked like benchmark.cpp:195-210."""
+    rc, out = run(ranks, ["--size", "1048577", "--repeat", "3", "--check"] + extra, tmp_path, {"FT_TOPO": topo})
+    assert rc == 0, out
+    assert out.count("(test passed)") == ranks, out
+
+
+@needs
+@pytest.mark.gpu
+def test_harness_rccl_only_fails_cleanly_on_a_shared_gpu(tmp_path):
+    rc, out = run(2, ["--size", "4096", "--repeat", "1"], tmp_path, {"FT_TOPO": "2", "FTAR_MPI_TRANSPORT": "rccl"})
+    assert rc != 0, out
