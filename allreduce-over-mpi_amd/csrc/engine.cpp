@@ -564,11 +564,12 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
   }
-  if (host && c->peer_direct && peer_eligible(plan)) {
-    // host buffers over the peer forms (e.g. a communicator bootstrapped over
-    // MPI with no RCCL, ftar_comm_init_host): the whole bucket in, the peer
-    // exchange in HBM, the whole bucket out -- same plan, same bits, not
-    // pipelined piece by piece like the p2p path below
+  if (host && c->peer_direct && !c->tp->has_p2p() && peer_eligible(plan)) {
+    // host buffers on a transport without p2p (a communicator bootstrapped
+    // over MPI with no RCCL, ftar_comm_init_host): the whole bucket in, the
+    // peer exchange in HBM, the whole bucket out -- same plan, same bits, not
+    // pipelined piece by piece like the p2p path below (which transports with
+    // p2p keep using for host buffers even in peer-direct mode)
     const size_t bytes = count * esz;
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     FTAR_CHECK_HIP(hipMemcpyAsync(c->staging, host->src, bytes, hipMemcpyHostToDevice, stream));

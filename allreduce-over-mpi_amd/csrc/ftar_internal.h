@@ -158,6 +158,8 @@ class Transport {
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
   // map_peers exports and opens IPC handles (false: one address space)
   virtual bool uses_ipc() const { return false; }
+  // send/recv available (false: the peer-direct forms are the only data path)
+  virtual bool has_p2p() const { return true; }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {

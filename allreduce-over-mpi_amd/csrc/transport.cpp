@@ -501,6 +501,7 @@ class HostTransport final : public Transport {
   ftar_status_t allgather(const void*, void*, size_t, int, int, hipStream_t) override { return unsupported(); }
   const char* name() const override { return "host"; }
   bool uses_ipc() const override { return true; }
+  bool has_p2p() const override { return false; }
   // everything before it on s, on every rank, is complete when it returns
   ftar_status_t barrier(hipStream_t s) override {
     FTAR_CHECK_HIP(hipStreamSynchronize(s));
