@@ -1,0 +1,46 @@
+"""bench.py's N > 1 path, end to end, on the box's one GPU: P ranks under torchrun share it, the communicator
+is bootstrapped over gloo (--host-comm, or RCCL refusing the shared GPU and every rank falling back), and the
+peer-direct forms move the data through IPC.  Everything the driver's 8-GPU run executes except the RCCL forms:
+the timed default, the validated sweep with registration and tuning variants, the xGMI probe, phase timelines,
+the 256 MiB (80 Mi elements > 2^26) and C5 line items, and the single JSON line."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(ranks, extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
+           "--steps", "2", "--warmup", "1", "--elements", str(5 << 24), "--elements-c5", str(1 << 22)] + extra
+    env = dict(os.environ, FTAR_BENCH_BUDGET_S="100", FTAR_BENCH_SWEEP_S="60")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("ranks,extra", [(2, ["--host-comm"]), (4, ["--host-comm"]), (2, [])])
+def test_bench_n_gt_1_rehearsal(ranks, extra):
+    d = _bench(ranks, extra)
+    assert d["n_gpus"] == ranks and d["check"] == "ok" and d["config"]["form"].startswith("peer-")
+    assert "watchdog" not in d
+    ok = [r for r in d["sweep"] if r.get("check") == "ok"]
+    assert len(ok) >= 8 and not [r for r in d["sweep"] if r.get("check") == "MISMATCH"], d["sweep"]
+    assert d["c5_bf16"]["check"] == "ok", d["c5_bf16"]
+    assert "ms" in d["bucket_256MiB"], d["bucket_256MiB"]
+    assert d["xgmi_probe_GBps"]["read_all_peers"][0] > 0
+    if not extra:   # RCCL refused the shared GPU on every rank and every rank fell back
+        assert "rccl_init_error" in d
