@@ -295,23 +295,28 @@ def test_random_soak_all_forms(seed):
     """Seeded random cases (topologies incl. lonely, dtypes, ops, ragged sizes, pieces) through every
     data-movement form: reduce-scatter stages|direct x all-gather stages|direct|collective x peer
     off|read|write (peer forms fall back to p2p where the plan is not one-round).  Bit-exact vs the oracle.
-    FTAR_SOAK scales the case count (default 40 per seed)."""
+    FTAR_SOAK scales the case count (default 100 per seed); P up to 16 (folds of k = 2..16)."""
     import os
     import random
     import random_cases
-    per = int(os.environ.get("FTAR_SOAK", "40"))
+    per = int(os.environ.get("FTAR_SOAK", "100"))
     rng = random.Random(1000 + seed)
-    for c in random_cases.cases(seed=500 + seed, count=per, max_p=12):
+    for c in random_cases.cases(seed=500 + seed, count=per, max_p=16):
         rs = rng.choice(["stages", "direct"])
         ag = rng.choice(["stages", "direct", "collective"])
         peer = rng.choice([0, 0, "read", "write"])
+        nt, lds = rng.random() < 0.7, rng.random() < 0.7   # peer tuning variants (bench.py sweeps them)
         g = group(c["P"])
         g.set_peer_direct(peer)
+        for cm in g.comms:
+            cm.peer_tuning(nt=nt, lds=lds)
         try:
             outs = run_group(c["ins"], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1,
                              c["oop"], chunk_bytes=c["chunk"], ag=ag, rs=rs)
         finally:
             g.set_peer_direct(0)
+            for cm in g.comms:
+                cm.peer_tuning()
         for r in range(c["P"]):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"],
                                                                 rs, ag, peer, r)
