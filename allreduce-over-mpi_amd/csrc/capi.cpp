@@ -16,6 +16,8 @@
 #include <map>
 #include "ftar_internal.h"
 
+using ftar::hip_ignore;
+
 namespace ftar {
 
 namespace {

@@ -28,6 +28,8 @@
 
 #include "ftar_internal.h"
 
+using ftar::hip_ignore;
+
 struct ftar_comm {
   int rank = 0, nranks = 1, device = 0;
   std::unique_ptr<ftar::Transport> tp;
@@ -139,22 +141,22 @@ ftar_status_t comm_setup(ftar_comm* c) {
 }
 
 void comm_teardown(ftar_comm* c) {
-  (void)hipSetDevice(c->device);
+  hip_ignore(hipSetDevice(c->device));
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
-    if (st) (void)hipStreamSynchronize(st);
+    if (st) hip_ignore(hipStreamSynchronize(st));
   if (c->tp) {
     c->tp->unmap_peers(&c->xpeers, c->rank);
     for (auto& r : c->regs) c->tp->unmap_peers(&r.second.peers, c->rank);
   }
   c->regs.clear();
-  if (c->xbuf) (void)hipFree(c->xbuf);
+  if (c->xbuf) hip_ignore(hipFree(c->xbuf));
   c->tp.reset();
-  for (auto e : c->events) (void)hipEventDestroy(e);
-  for (auto e : c->tev) (void)hipEventDestroy(e);
-  if (c->scratch) (void)hipFree(c->scratch);
-  if (c->staging) (void)hipFree(c->staging);
+  for (auto e : c->events) hip_ignore(hipEventDestroy(e));
+  for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
+  if (c->scratch) hip_ignore(hipFree(c->scratch));
+  if (c->staging) hip_ignore(hipFree(c->staging));
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
-    if (st) (void)hipStreamDestroy(st);
+    if (st) hip_ignore(hipStreamDestroy(st));
 }
 
 // ---------------------------------------------------------------------------
@@ -214,25 +216,12 @@ ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   Transport* tp = c->tp.get();
   FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still touches the old X
   FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-  const size_t want = tp->uses_ipc() ? ipc_safe_size(std::max(bytes, c->xbuf_bytes)) : std::max(bytes, c->xbuf_bytes);
-  trace("rank %d: exchange buffer %zu -> %zu bytes", c->rank, c->xbuf_bytes, want);
+  trace("rank %d: exchange buffer %zu -> >= %zu bytes", c->rank, c->xbuf_bytes, std::max(bytes, c->xbuf_bytes));
   void* fresh = nullptr;
-  std::vector<void*> set_aside;
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    if (hipMalloc(&fresh, want) != hipSuccess) {
-      fresh = nullptr;
-      set_error("exchange buffer: hipMalloc of " + std::to_string(want) + " bytes failed", __FILE__, __LINE__);
-      break;
-    }
-    IpcRef probe;
-    if (!tp->uses_ipc() || ipc_export(fresh, &probe) == FTAR_SUCCESS) break;
-    trace("rank %d: %p not exportable, allocating another", c->rank, fresh);
-    set_aside.push_back(fresh);
-    fresh = nullptr;
-  }
-  for (void* p : set_aside) (void)hipFree(p);
+  size_t want = 0;
+  (void)alloc_exportable(std::max(bytes, c->xbuf_bytes), tp->uses_ipc(), &fresh, &want);
   tp->unmap_peers(&c->xpeers, c->rank);
-  if (c->xbuf) (void)hipFree(c->xbuf);  // (no early return: the peers are on their way to the exchange)
+  if (c->xbuf) hip_ignore(hipFree(c->xbuf)); // (no early return: the peers are on their way to the exchange)
   c->xbuf = fresh;
   c->xbuf_bytes = fresh ? want : 0;
   trace("rank %d: exchange buffer at %p, map peers", c->rank, fresh);
@@ -411,8 +400,8 @@ ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int
     if (st == FTAR_SUCCESS && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) st = FTAR_ERR_HIP;
     if (st == FTAR_SUCCESS && ms > 0.f) out[mode] = (double)segs.size() * bytes * iters / (ms * 1e-3) / 1e9;
   }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
+  hip_ignore(hipEventDestroy(e0));
+  hip_ignore(hipEventDestroy(e1));
   return st;
 }
 
@@ -564,12 +553,12 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
   }
-  if (host && c->peer_direct && !c->tp->has_p2p() && peer_eligible(plan)) {
+  if (host && c->peer_direct && !c->tp->async_p2p() && peer_eligible(plan)) {
     // host buffers on a transport without p2p (a communicator bootstrapped
     // over MPI with no RCCL, ftar_comm_init_host): the whole bucket in, the
     // peer exchange in HBM, the whole bucket out -- same plan, same bits, not
     // pipelined piece by piece like the p2p path below (which transports with
-    // p2p keep using for host buffers even in peer-direct mode)
+    // stream-ordered p2p keep using for host buffers even in peer-direct mode)
     const size_t bytes = count * esz;
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     FTAR_CHECK_HIP(hipMemcpyAsync(c->staging, host->src, bytes, hipMemcpyHostToDevice, stream));
@@ -654,7 +643,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   for (const auto& step : order) {
     const size_t s = step.first, k = step.second, lo = k * chunk;
     const Stage& st = plan.stages[s];
-    if (moves[s]) {
+    if (moves[s] || tp->collective_groups()) {  // (an idle rank still joins the host transport's step)
       if (host && !comm_has_input[k]) {
         FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k), 0));
         comm_has_input[k] = 1;
@@ -901,7 +890,7 @@ ftar_status_t ftar_debug_peer_selftest(ftar_comm_t comm) {
   if (st == FTAR_SUCCESS) st = comm->tp->barrier(comm->comm_s);
   if (st == FTAR_SUCCESS && hipStreamSynchronize(comm->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
   comm->tp->unmap_peers(&peers, comm->rank);
-  (void)hipFree(buf);
+  hip_ignore(hipFree(buf));
   return st;
 }
 

@@ -13,14 +13,24 @@
 
 namespace ftar {
 
+// A failed HIP call also leaves the thread's "last error" set, and the next
+// kernel-launch check (hipGetLastError) would report it against an innocent
+// launch: every failure path clears it once reported (clear_hip_error).
 #define FTAR_CHECK_HIP(expr)                                                                   \
   do {                                                                                         \
     hipError_t _e = (expr);                                                                    \
     if (_e != hipSuccess) {                                                                    \
       ::ftar::set_error(std::string(#expr) + ": " + hipGetErrorString(_e), __FILE__, __LINE__); \
+      (void)hipGetLastError();                                                                 \
       return FTAR_ERR_HIP;                                                                     \
     }                                                                                          \
   } while (0)
+
+// best-effort HIP call (cleanup paths): a failure is dropped, and so is the
+// sticky "last error" it would leave for the next launch check
+inline void hip_ignore(hipError_t e) {
+  if (e != hipSuccess) (void)hipGetLastError();
+}
 
 #define FTAR_RETURN_IF(st)          \
   do {                              \
@@ -158,8 +168,12 @@ class Transport {
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
   // map_peers exports and opens IPC handles (false: one address space)
   virtual bool uses_ipc() const { return false; }
-  // send/recv available (false: the peer-direct forms are the only data path)
-  virtual bool has_p2p() const { return true; }
+  // send/recv are stream-ordered and need no peer participation beyond the
+  // matching operation (RCCL, local).  false: the host transport, whose
+  // send/recv complete inside group_end through host collectives, so every
+  // rank must call group_start/group_end for every step (collective_groups).
+  virtual bool async_p2p() const { return true; }
+  virtual bool collective_groups() const { return false; }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {
@@ -190,6 +204,13 @@ ftar_status_t ipc_export(const void* p, IpcRef* out);
 // around them (ipc_safe_size).
 bool ipc_size_guard();
 size_t ipc_safe_size(size_t bytes);
+// A device buffer of `bytes` for IPC export (ipc = true: rounded by
+// ipc_safe_size and export-checked; an allocation whose export fails -- a
+// fresh hipMalloc landing on a recently closed IPC mapping can -- is set aside
+// and another taken).  *out = nullptr on failure, with the error set: callers
+// in a collective still publish (an invalid reference) so every rank fails
+// together.  *got = the size allocated.
+ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got);
 // opens ref; *base = the mapped allocation (for hipIpcCloseMemHandle), *p = base + offset
 ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p);
 

@@ -18,6 +18,7 @@
 //                   on a single GPU (tests) and in single-process groups.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -44,6 +45,33 @@ size_t ipc_safe_size(size_t bytes) {
   return (ipc_size_guard() && (bytes & bit31)) ? (bytes | mask4g) + 1 : bytes;  // up to the next 4 GiB
 }
 
+ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got) {
+  const size_t want = ipc ? ipc_safe_size(bytes) : bytes;
+  *out = nullptr;
+  *got = 0;
+  std::vector<void*> set_aside;
+  ftar_status_t st = FTAR_ERR_HIP;
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    void* fresh = nullptr;
+    if (hipMalloc(&fresh, want) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("hipMalloc of " + std::to_string(want) + " bytes failed", __FILE__, __LINE__);
+      break;
+    }
+    IpcRef probe;
+    if (!ipc || ipc_export(fresh, &probe) == FTAR_SUCCESS) {
+      *out = fresh;
+      *got = want;
+      st = FTAR_SUCCESS;
+      break;
+    }
+    trace("%p not exportable, allocating another", fresh);
+    set_aside.push_back(fresh);
+  }
+  for (void* p : set_aside) hip_ignore(hipFree(p));
+  return st;
+}
+
 ftar_status_t ipc_export(const void* p, IpcRef* out) {
   memset(out, 0, sizeof *out);
   hipDeviceptr_t base = nullptr;
@@ -60,6 +88,7 @@ ftar_status_t ipc_export(const void* p, IpcRef* out) {
   out->offset = static_cast<uint64_t>(static_cast<const char*>(p) - static_cast<const char*>(base));
   const hipError_t e = hipIpcGetMemHandle(&out->handle, base);
   if (e != hipSuccess) {
+    (void)hipGetLastError();  // not sticky: the next launch check must not see it
     memset(&out->handle, 0, sizeof out->handle);
     set_error(std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e), __FILE__, __LINE__);
     trace("ipc_export %p failed: %s", p, hipGetErrorString(e));
@@ -100,7 +129,7 @@ class RcclTransport final : public Transport {
   explicit RcclTransport(ncclComm_t c) : comm_(c) {}
   ~RcclTransport() override {
     if (comm_) ncclCommDestroy(comm_);
-    if (scratch_) (void)hipFree(scratch_);
+    if (scratch_) hip_ignore(hipFree(scratch_));
   }
   // a 4-byte all-reduce: complete on any rank's stream only once every rank's
   // stream has reached it
@@ -129,7 +158,7 @@ class RcclTransport final : public Transport {
       set_error("peer map: handle exchange failed", __FILE__, __LINE__);
       st = FTAR_ERR_RCCL;
     }
-    (void)hipStreamDestroy(s);
+    hip_ignore(hipStreamDestroy(s));
     FTAR_RETURN_IF(st);
     peers->assign(nranks, nullptr);
     for (int q = 0; q < nranks && why.empty(); ++q)  // a failed export anywhere: nobody opens anything
@@ -186,7 +215,7 @@ class RcclTransport final : public Transport {
       handed_.erase(h);
       if (it != imports_.end() && --it->second.refs == 0) {
         trace("ipc close %p", it->second.base);
-        (void)hipIpcCloseMemHandle(it->second.base);
+        hip_ignore(hipIpcCloseMemHandle(it->second.base));
         imports_.erase(it);
       }
     }
@@ -244,7 +273,7 @@ class RcclTransport final : public Transport {
               ncclAllReduce(word, word, 1, ncclInt32, ncclSum, comm_, s) == ncclSuccess &&
               hipMemcpyAsync(total, word, sizeof *total, hipMemcpyDeviceToHost, s) == hipSuccess &&
               hipStreamSynchronize(s) == hipSuccess;
-    (void)hipStreamDestroy(s);
+    hip_ignore(hipStreamDestroy(s));
     if (!ok) {
       set_error("peer map: failure agreement failed", __FILE__, __LINE__);
       return FTAR_ERR_RCCL;
@@ -293,8 +322,8 @@ struct LocalHub {
     hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
     bool taken = false;
     ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
-      if (ready) (void)hipEventDestroy(ready);
-      if (done) (void)hipEventDestroy(done);
+      if (ready) hip_ignore(hipEventDestroy(ready));
+      if (done) hip_ignore(hipEventDestroy(done));
     }
   };
   // every rank's value of one rendezvous (barriers, peer pointers)
@@ -374,7 +403,7 @@ class LocalTransport final : public Transport {
   // each rank's stream waits for every other rank's event recorded at the barrier
   ftar_status_t barrier(hipStream_t s) override {
     auto e = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [](hipEvent_t* p) {
-      if (*p) (void)hipEventDestroy(*p);
+      if (*p) hip_ignore(hipEventDestroy(*p));
       delete p;
     });
     FTAR_RETURN_IF(event(e.get()));
@@ -401,6 +430,12 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
 
+  static ftar_status_t unsupported() {
+    set_error("host transport: point-to-point transfers are off (peer-direct forms only; FTAR_HOST_P2P=1 enables "
+              "the experimental bounce-buffer p2p)",
+              __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
   ftar_status_t flush() {
     std::vector<Op> ops;
     ops.swap(ops_);
@@ -443,7 +478,7 @@ class LocalTransport final : public Transport {
       hipEvent_t done = nullptr;
       FTAR_RETURN_IF(event(&done));
       if (hipEventRecord(done, o.s) != hipSuccess) {
-        (void)hipEventDestroy(done);
+        hip_ignore(hipEventDestroy(done));
         set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
         return FTAR_ERR_HIP;
       }
@@ -491,17 +526,75 @@ std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, i
 // ---------------------------------------------------------------------------
 namespace {
 class HostTransport final : public Transport {
+  struct Op {
+    bool is_send;
+    void* buf;
+    size_t bytes;
+    int peer;
+    hipStream_t s;
+  };
+  struct Desc {  // one staged send, published to every rank
+    int32_t peer;
+    int32_t pad;
+    uint64_t off;
+    uint64_t bytes;
+  };
+
  public:
   HostTransport(int nranks, int rank, ftar_host_allgather_fn fn, void* user)
-      : nranks_(nranks), rank_(rank), fn_(fn), user_(user) {}
-  ftar_status_t group_start() override { return FTAR_SUCCESS; }
-  ftar_status_t send(const void*, size_t, int, hipStream_t) override { return unsupported(); }
-  ftar_status_t recv(void*, size_t, int, hipStream_t) override { return unsupported(); }
-  ftar_status_t group_end() override { return FTAR_SUCCESS; }
-  ftar_status_t allgather(const void*, void*, size_t, int, int, hipStream_t) override { return unsupported(); }
+      : nranks_(nranks), rank_(rank), fn_(fn), user_(user) {
+    const char* e = getenv("FTAR_HOST_P2P");
+    p2p_ = e && *e && *e != '0';
+  }
+  ~HostTransport() override {
+    unmap_peers(&ppeers_, rank_);
+    if (pbuf_) hip_ignore(hipFree(pbuf_));
+  }
+  // Point-to-point through a bounce buffer (EXPERIMENTAL, FTAR_HOST_P2P=1),
+  // completed inside group_end with host collectives (no RCCL): every sender copies its blocks into its own
+  // IPC-exported buffer B, the ranks publish (peer, offset, bytes) of every
+  // staged block, every receiver copies its blocks out of the senders' B in
+  // per-pair posting order (MPI/RCCL matching), and a last host collective
+  // lets the senders reuse B.  Host-synchronous, so every rank takes part in
+  // every step (collective_groups) -- the engine joins idle ranks in.
+  ftar_status_t group_start() override {
+    ++depth_;
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+    if (!p2p_) return unsupported();
+    ops_.push_back({true, const_cast<void*>(buf), bytes, peer, s});
+    return depth_ ? FTAR_SUCCESS : flush();
+  }
+  ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+    if (!p2p_) return unsupported();
+    ops_.push_back({false, buf, bytes, peer, s});
+    return depth_ ? FTAR_SUCCESS : flush();
+  }
+  ftar_status_t group_end() override {
+    if (depth_ <= 0) return FTAR_ERR_INVALID_ARG;
+    if (--depth_ == 0) return p2p_ ? flush() : FTAR_SUCCESS;
+    return FTAR_SUCCESS;
+  }
+  // every rank's block of `bytes` -> recv[q * bytes], through the bounce buffers
+  ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) override {
+    if (!p2p_) return unsupported();
+    for (int q = 0; q < nranks; ++q) {
+      if (q == rank) continue;
+      ops_.push_back({true, const_cast<void*>(send), bytes, q, s});
+      ops_.push_back({false, static_cast<char*>(recv) + (size_t)q * bytes, bytes, q, s});
+    }
+    ftar_status_t st = flush();
+    if (st == FTAR_SUCCESS && static_cast<char*>(recv) + (size_t)rank * bytes != send && bytes) {
+      const Segment own{send, static_cast<char*>(recv) + (size_t)rank * bytes, bytes};
+      st = launch_gather(&own, 1, s);
+    }
+    return st;
+  }
   const char* name() const override { return "host"; }
   bool uses_ipc() const override { return true; }
-  bool has_p2p() const override { return false; }
+  bool async_p2p() const override { return false; }
+  bool collective_groups() const override { return p2p_; }
   // everything before it on s, on every rank, is complete when it returns
   ftar_status_t barrier(hipStream_t s) override {
     FTAR_CHECK_HIP(hipStreamSynchronize(s));
@@ -551,7 +644,7 @@ class HostTransport final : public Transport {
       auto it = q == rank ? bases_.end() : bases_.find((*peers)[q]);
       if (it == bases_.end()) continue;
       trace("ipc close %p", it->second);
-      (void)hipIpcCloseMemHandle(it->second);
+      hip_ignore(hipIpcCloseMemHandle(it->second));
       bases_.erase(it);
     }
     peers->clear();
@@ -559,9 +652,99 @@ class HostTransport final : public Transport {
 
  private:
   static ftar_status_t unsupported() {
-    set_error("host transport: point-to-point transfers are not available (peer-direct forms only)", __FILE__,
-              __LINE__);
+    set_error("host transport: point-to-point transfers are off (peer-direct forms only; FTAR_HOST_P2P=1 enables "
+              "the experimental bounce-buffer p2p)",
+              __FILE__, __LINE__);
     return FTAR_ERR_UNSUPPORTED;
+  }
+  ftar_status_t flush() {
+    std::vector<Op> ops;
+    ops.swap(ops_);
+    ftar_status_t st = FTAR_SUCCESS;
+    auto keep = [&](ftar_status_t e) {
+      if (st == FTAR_SUCCESS) st = e;
+    };
+    std::vector<hipStream_t> streams;
+    for (const Op& o : ops) {
+      if (o.peer < 0 || o.peer >= nranks_ || o.peer == rank_) keep(FTAR_ERR_INVALID_ARG);
+      if (std::find(streams.begin(), streams.end(), o.s) == streams.end()) streams.push_back(o.s);
+    }
+    auto sync = [&] {
+      for (hipStream_t s : streams)
+        if (hipStreamSynchronize(s) != hipSuccess) keep(FTAR_ERR_HIP);
+    };
+    // 1. the bounce buffer holds this step's largest send volume on any rank (collective growth)
+    uint64_t need = 0;
+    for (const Op& o : ops)
+      if (o.is_send) need += (o.bytes + 255) & ~uint64_t(255);
+    std::vector<uint64_t> needs(nranks_);
+    FTAR_RETURN_IF(gather(&need, needs.data(), sizeof need));
+    const uint64_t most = *std::max_element(needs.begin(), needs.end());
+    if (most > pbuf_bytes_ || (most && ppeers_.empty())) keep(grow(most));
+    // 2. stage my sends in my buffer
+    std::vector<Desc> mine;
+    uint64_t off = 0;
+    for (const Op& o : ops) {
+      if (!o.is_send) continue;
+      if (st == FTAR_SUCCESS && o.bytes) {
+        const Segment seg{o.buf, static_cast<char*>(pbuf_) + off, o.bytes};
+        keep(launch_gather(&seg, 1, o.s));
+      }
+      mine.push_back({o.peer, 0, off, o.bytes});
+      off += (o.bytes + 255) & ~uint64_t(255);
+    }
+    sync();
+    // 3. publish every rank's staged sends
+    int32_t cnt = (int32_t)mine.size();
+    std::vector<int32_t> cnts(nranks_);
+    FTAR_RETURN_IF(gather(&cnt, cnts.data(), sizeof cnt));
+    const int32_t maxc = *std::max_element(cnts.begin(), cnts.end());
+    std::vector<Desc> all((size_t)nranks_ * maxc);
+    if (maxc) {
+      mine.resize(maxc, Desc{-1, 0, 0, 0});
+      FTAR_RETURN_IF(gather(mine.data(), all.data(), sizeof(Desc) * maxc));
+    }
+    // 4. my receives, in posting order per peer, out of the senders' buffers
+    std::vector<size_t> next(nranks_, 0);
+    for (const Op& o : ops) {
+      if (o.is_send || st != FTAR_SUCCESS) continue;
+      const Desc* d = nullptr;
+      for (size_t& i = next[o.peer]; i < (size_t)cnts[o.peer] && !d; ++i)
+        if (all[(size_t)o.peer * maxc + i].peer == rank_) d = &all[(size_t)o.peer * maxc + i];
+      if (!d || d->bytes != o.bytes) {
+        set_error("host transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
+        keep(FTAR_ERR_INTERNAL);
+        continue;
+      }
+      if (o.bytes) {
+        const Segment seg{ppeers_[o.peer] + d->off, o.buf, o.bytes};
+        keep(launch_gather(&seg, 1, o.s));
+      }
+    }
+    sync();
+    // 5. all copies out are done (the senders may reuse their buffers); agree on the outcome
+    int32_t bad = st == FTAR_SUCCESS ? 0 : 1;
+    std::vector<int32_t> bads(nranks_);
+    FTAR_RETURN_IF(gather(&bad, bads.data(), sizeof bad));
+    for (int32_t b : bads)
+      if (b && st == FTAR_SUCCESS) {
+        set_error("host transport: a peer's transfer failed", __FILE__, __LINE__);
+        st = FTAR_ERR_INTERNAL;
+      }
+    return st;
+  }
+  // collective: every rank calls it with the same `bytes` (the step's maximum)
+  ftar_status_t grow(uint64_t bytes) {
+    unmap_peers(&ppeers_, rank_);
+    void* fresh = nullptr;
+    size_t got = 0;
+    (void)alloc_exportable(std::max<uint64_t>(bytes, 2 * pbuf_bytes_), true, &fresh, &got);
+    if (pbuf_) hip_ignore(hipFree(pbuf_));
+    pbuf_ = fresh;
+    pbuf_bytes_ = fresh ? got : 0;
+    const ftar_status_t st = map_peers(pbuf_, rank_, nranks_, &ppeers_);
+    if (st != FTAR_SUCCESS) pbuf_bytes_ = 0;
+    return st;
   }
   ftar_status_t gather(const void* mine, void* all, size_t bytes) {
     trace("host gather %zu bytes", bytes);
@@ -575,6 +758,12 @@ class HostTransport final : public Transport {
   ftar_host_allgather_fn fn_;
   void* user_;
   std::map<char*, void*> bases_;
+  std::vector<Op> ops_;
+  int depth_ = 0;
+  bool p2p_ = false;      // FTAR_HOST_P2P: the bounce-buffer p2p below (experimental, off by default)
+  void* pbuf_ = nullptr;  // bounce buffer of the p2p steps, IPC-mapped by every rank
+  size_t pbuf_bytes_ = 0;
+  std::vector<char*> ppeers_;
 };
 }  // namespace
 

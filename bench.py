@@ -395,23 +395,35 @@ def bench_distributed(a):
     def check_y(fn):
         """y (from the timed calls) against the fp64 sample and across ranks; then one more call on the
         negated inputs must give exactly -y everywhere (round-to-nearest-even is sign-symmetric), which
-        proves the call read this call's data (no stale copies) over the whole bucket."""
+        proves the call read this call's data (no stale copies) over the whole bucket.  Returns (ok, what
+        failed on any rank: "" | "sample" | "ranks differ" | "negation")."""
         x, y = fn.xin, fn.yout
         torch.cuda.synchronize()
         mine = y[idx].float().cpu()
         ally = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(ally, mine)
-        ok = all(torch.equal(ally[0], t) for t in ally) and bool(((mine.double() - ref64).abs() <= tol).all())
+        bits = 0
+        if not all(torch.equal(ally[0], t) for t in ally):
+            bits |= 2
+        if not bool(((mine.double() - ref64).abs() <= tol).all()):
+            bits |= 1
         y1 = y.clone()
         x.neg_()
-        fn()
-        torch.cuda.synchronize()
-        ok = ok and bool(torch.equal(y, y1.neg_()))
-        x.neg_()
+        try:
+            fn()
+            torch.cuda.synchronize()
+        finally:
+            x.neg_()   # the inputs stay intact for the next configuration, whatever happened
+        if not torch.equal(y, y1.neg_()):
+            bits |= 4
         del y1
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item())
+        allb = [torch.zeros(1, dtype=torch.int32) for _ in range(world)]   # every rank's failures, OR-ed
+        dist.all_gather(allb, torch.tensor([bits], dtype=torch.int32))
+        bits = 0
+        for b in allb:
+            bits |= int(b.item())
+        why = ", ".join(w for bit, w in ((1, "sample"), (2, "ranks differ"), (4, "negation")) if bits & bit)
+        return bits == 0, why
 
     def measure_c5():
         nb = a.n_c5 or (1 << 29)
@@ -538,10 +550,10 @@ def bench_distributed(a):
     default_chunk = a.chunk_bytes or comm.chunk_bytes
     fn_default = run_with(default_topo, default_chunk, base_form)
     ms_default = timed(fn_default, a.steps, a.warmup)
-    ok_default = check_y(fn_default)
+    ok_default, why_default = check_y(fn_default)
     default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": base_form,
                     "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
-                    "check": "ok" if ok_default else "MISMATCH"}
+                    "check": "ok" if ok_default else f"MISMATCH ({why_default})"}
     state["line"] = make_result(ms_default, default_topo, default_chunk, base_form, ok_default, a.steps, a.warmup,
                                 {"config_selection": "default (sweep not reached)", "default_config": default_info})
 
@@ -558,7 +570,9 @@ def bench_distributed(a):
         seen.add(key)
         forms = ["direct"] + (["collective"] if (not t.ring and n % world == 0) else []) + ["stages"]
         if a.host_comm:
-            forms = []   # no point-to-point transport: the peer forms only
+            # the host transport's p2p is a host-synchronous bounce-buffer fallback (RCCL-less MPI runs), not a
+            # data path to time; long runs of it stalled in the host collective, so the peer forms only
+            forms = []
         for form in forms:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
@@ -610,12 +624,12 @@ def bench_distributed(a):
         try:
             fn = run_with(t, chunk, form)
             ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
-            ok_ = check_y(fn)   # every configuration's own output, before it may be chosen
+            ok_, why_ = check_y(fn)   # every configuration's own output, before it may be chosen
         except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
             sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "error": str(e)[:200]})
             continue
         sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "ms": round(ms_, 4),
-                      "busbw_GBps": round(bws(ms_)[1], 2), "check": "ok" if ok_ else "MISMATCH"})
+                      "busbw_GBps": round(bws(ms_)[1], 2), "check": "ok" if ok_ else f"MISMATCH ({why_})"})
     state["line"]["sweep"] = sweep
 
     # 3. the sweep's best validated configuration, re-timed like the default, if it is faster
@@ -626,7 +640,7 @@ def bench_distributed(a):
         best_topo = ftar.topo("1" if best["topology"] == "ring" else best["topology"])
         fn_best = run_with(best_topo, best["chunk_bytes"], best["form"])
         ms = timed(fn_best, a.steps, a.warmup)
-        ok = check_y(fn_best)
+        ok, _ = check_y(fn_best)
         if ok and ms < ms_default:
             carry = {k: state["line"][k] for k in ("xgmi_probe_GBps",) if k in state["line"]}
             state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,

@@ -11,8 +11,15 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
+# (topo, lonely, reduce-scatter form, all-gather form, chunk bytes) for the bounce-buffer p2p path
+P2P_CASES = {2: [("1", 0, "stages", "stages", 1 << 16), ("2", 0, "direct", "collective", 0),
+                 ("1", 0, "direct", "direct", 4096)],
+             4: [("2,2", 0, "stages", "stages", 1 << 16), ("1", 0, "stages", "stages", 0),
+                 ("2,2", 0, "direct", "collective", 1 << 15), ("4", 0, "direct", "direct", 0)],
+             5: [("2,2", 1, "stages", "stages", 1 << 16), ("2,2", 1, "direct", "direct", 0)]}
 CASES = {2: [("1", "f32"), ("2", "bf16"), ("1", "i16")],
-         4: [("1", "f32"), ("2,2", "f32"), ("4", "bf16"), ("1", "i16")]}
+         4: [("1", "f32"), ("2,2", "f32"), ("4", "bf16"), ("1", "i16")],
+         5: [("1", "f32"), ("5", "bf16")]}
 
 
 def _free_port():
@@ -25,7 +32,7 @@ def _worker(rank, world, port, n, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FTAR_HOST_P2P="1")
     import torch
     import torch.distributed as dist
     import ftar
@@ -54,13 +61,21 @@ def _worker(rank, world, port, n, q):
                         for r in regs:
                             comm.deregister(r)
                         dist.barrier()
-        # p2p is not available on this transport: a staged plan fails cleanly, on every rank
+        # point-to-point through the bounce buffers (host-synchronous): every other form, lonely plans,
+        # host buffers (pipelined path), all across the process boundary
         comm.peer_direct = 0
-        try:
-            comm.allreduce(None, torch.zeros(n, device="cuda"), n, "f32", "sum", topo_="1")
-            out["p2p"] = "ran"
-        except ftar.FtarError as e:
-            out["p2p"] = e.status
+        for topo, lonely, rs, ag, chunk in P2P_CASES[world]:
+            x = fi.fill("f32", 23, rank, n)
+            xt = torch.from_numpy(x.copy()).cuda()
+            comm.reduce_scatter, comm.allgather, comm.chunk_bytes = rs, ag, chunk
+            comm.allreduce(None, xt, n, "f32", "sum", topo_=topo, lonely=lonely)
+            torch.cuda.synchronize()
+            out[("p2p", topo, lonely, rs, ag)] = xt.cpu().numpy().tobytes()
+        hx = torch.from_numpy(fi.fill("f32", 23, rank, n).copy()).pin_memory()
+        comm.reduce_scatter, comm.allgather, comm.chunk_bytes = "direct", "direct", 1 << 16
+        comm.allreduce_host(None, hx, n, "f32", "sum", topo_=P2P_CASES[world][0][0], lonely=P2P_CASES[world][0][1])
+        torch.cuda.synchronize()
+        out["host"] = hx.numpy().tobytes()
         comm.destroy()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001  report, don't hang the parent
@@ -68,7 +83,7 @@ def _worker(rank, world, port, n, q):
     q.put((rank, out))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 5])
 def test_peer_forms_across_processes(world):
     import ftar_inputs as fi
     import oracle_lib
@@ -92,7 +107,13 @@ def test_peer_forms_across_processes(world):
         for key in keys:
             for r in range(world):
                 assert res[r][key] == ref[r].tobytes(), (world, key, r)
-    assert all(res[r]["p2p"] == 2 for r in range(world)), [res[r]["p2p"] for r in range(world)]
+    ins = [fi.fill("f32", 23, r, n) for r in range(world)]
+    for topo, lonely, rs, ag, _ in P2P_CASES[world]:
+        ref = oracle_lib.allreduce(ins, topo, lonely)
+        for r in range(world):
+            assert res[r][("p2p", topo, lonely, rs, ag)] == ref[r].tobytes(), (world, topo, lonely, rs, ag, r)
+    ref = oracle_lib.allreduce(ins, P2P_CASES[world][0][0], P2P_CASES[world][0][1])
+    assert all(res[r]["host"] == ref[r].tobytes() for r in range(world))
 
 
 def _big_worker(rank, world, port, n, q):
