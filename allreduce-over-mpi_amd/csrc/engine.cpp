@@ -149,7 +149,10 @@ void comm_teardown(ftar_comm* c) {
     for (auto& r : c->regs) c->tp->unmap_peers(&r.second.peers, c->rank);
   }
   c->regs.clear();
-  if (c->xbuf) hip_ignore(hipFree(c->xbuf));
+  if (c->xbuf) {
+    forget_token(c->xbuf);
+    hip_ignore(hipFree(c->xbuf));
+  }
   c->tp.reset();
   for (auto e : c->events) hip_ignore(hipEventDestroy(e));
   for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
@@ -216,19 +219,49 @@ ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   Transport* tp = c->tp.get();
   FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still touches the old X
   FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
-  trace("rank %d: exchange buffer %zu -> >= %zu bytes", c->rank, c->xbuf_bytes, std::max(bytes, c->xbuf_bytes));
+  const size_t need = std::max(bytes, c->xbuf_bytes);
+  trace("rank %d: exchange buffer %zu -> >= %zu bytes", c->rank, c->xbuf_bytes, need);
+  // The new X is allocated, stamped and mapped while the old X and the old
+  // mappings are still alive (a fresh allocation or import landing on an
+  // address range just released is where the runtime went wrong); a mapping
+  // that fails verification on any rank is retried by all, the failed
+  // allocation kept until the end so the next one lands elsewhere.
+  std::vector<void*> failed;
+  std::vector<char*> peers;
   void* fresh = nullptr;
-  size_t want = 0;
-  (void)alloc_exportable(std::max(bytes, c->xbuf_bytes), tp->uses_ipc(), &fresh, &want);
+  size_t got = 0;
+  ftar_status_t st = FTAR_ERR_HIP;
+  for (int attempt = 0; attempt < 3 && st != FTAR_SUCCESS; ++attempt) {
+    fresh = nullptr;
+    got = 0;
+    if (alloc_exportable(need, tp->uses_ipc(), &fresh, &got) == FTAR_SUCCESS && tp->uses_ipc() &&
+        stamp_token(fresh) != FTAR_SUCCESS) {
+      hip_ignore(hipFree(fresh));
+      fresh = nullptr;
+    }
+    st = tp->map_peers(fresh, c->rank, c->nranks, &peers);
+    trace("rank %d: exchange buffer at %p, map peers -> %d", c->rank, fresh, (int)st);
+    if (st != FTAR_SUCCESS && fresh) failed.push_back(fresh);
+  }
   tp->unmap_peers(&c->xpeers, c->rank);
-  if (c->xbuf) hip_ignore(hipFree(c->xbuf)); // (no early return: the peers are on their way to the exchange)
+  if (c->xbuf) {
+    forget_token(c->xbuf);
+    hip_ignore(hipFree(c->xbuf));
+  }
+  c->xbuf = nullptr;
+  c->xbuf_bytes = 0;
+  for (void* f : failed) {
+    forget_token(f);
+    hip_ignore(hipFree(f));
+  }
+  if (st != FTAR_SUCCESS) {
+    if (fresh && std::find(failed.begin(), failed.end(), fresh) == failed.end()) hip_ignore(hipFree(fresh));
+    return st;
+  }
   c->xbuf = fresh;
-  c->xbuf_bytes = fresh ? want : 0;
-  trace("rank %d: exchange buffer at %p, map peers", c->rank, fresh);
-  const ftar_status_t st = tp->map_peers(c->xbuf, c->rank, c->nranks, &c->xpeers);
-  trace("rank %d: map peers -> %d", c->rank, (int)st);
-  if (st != FTAR_SUCCESS) c->xpeers.clear();
-  return st;
+  c->xbuf_bytes = got;
+  c->xpeers.swap(peers);
+  return FTAR_SUCCESS;
 }
 
 // the plan's fold of my block with operand i read from where(i)

@@ -187,8 +187,11 @@ class Transport {
 struct IpcRef {
   hipIpcMemHandle_t handle;
   uint64_t offset;
-  uint64_t valid;  // 1 when the export succeeded: peers never open a failed rank's handle
-  uint64_t pad[6];
+  uint64_t valid;     // 1 when the export succeeded: peers never open a failed rank's handle
+  uint64_t size;      // the exported allocation's size
+  uint64_t stamped;   // 1: the first 16 bytes at the pointer are a fresh random token (stamp_token) ...
+  uint64_t token[2];  // ... whose value this is; the importer reads them back through its mapping
+  uint64_t pad[2];
 };
 static_assert(sizeof(IpcRef) == 128, "IpcRef layout");
 // On failure *out is still a well-formed reference with valid = 0, so the
@@ -211,7 +214,15 @@ size_t ipc_safe_size(size_t bytes);
 // in a collective still publish (an invalid reference) so every rank fails
 // together.  *got = the size allocated.
 ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got);
-// opens ref; *base = the mapped allocation (for hipIpcCloseMemHandle), *p = base + offset
+// Writes a fresh random token into the first 16 bytes at p (a buffer ftar
+// owns), so that its IPC reference can be verified by every importer: under
+// HIP 7.0 an import occasionally maps the wrong memory after buffers were
+// regrown (tools/p2p_rehearsal.py), silently.
+ftar_status_t stamp_token(void* p);
+void forget_token(const void* p);  // before the stamped buffer is freed
+// opens ref and verifies the mapping (allocation size; the token when
+// stamped) -- a mismatch closes it and fails like a failed open;
+// *base = the mapped allocation (for hipIpcCloseMemHandle), *p = base + offset
 ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p);
 
 std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_t& id, int rank,

@@ -19,9 +19,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
+#include <random>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
+#include <unistd.h>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -43,6 +46,16 @@ bool ipc_size_guard() {
 size_t ipc_safe_size(size_t bytes) {
   const size_t bit31 = size_t(1) << 31, mask4g = (size_t(1) << 32) - 1;
   return (ipc_size_guard() && (bytes & bit31)) ? (bytes | mask4g) + 1 : bytes;  // up to the next 4 GiB
+}
+
+namespace {
+std::mutex g_tokens_mu;
+std::map<const void*, std::array<uint64_t, 2>> g_tokens;  // stamped buffers (owned exchange/bounce buffers)
+}
+
+void forget_token(const void* p) {
+  std::lock_guard<std::mutex> g(g_tokens_mu);
+  g_tokens.erase(p);
 }
 
 ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got) {
@@ -94,7 +107,24 @@ ftar_status_t ipc_export(const void* p, IpcRef* out) {
     trace("ipc_export %p failed: %s", p, hipGetErrorString(e));
     return FTAR_ERR_HIP;
   }
+  out->size = size;
+  std::lock_guard<std::mutex> g(g_tokens_mu);
+  auto it = g_tokens.find(p);
+  if (it != g_tokens.end()) {
+    out->stamped = 1;
+    out->token[0] = it->second[0];
+    out->token[1] = it->second[1];
+  }
   out->valid = 1;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t stamp_token(void* p) {
+  static std::mt19937_64 rng(std::random_device{}() ^ (uint64_t)getpid() << 32);
+  std::array<uint64_t, 2> t{rng(), rng()};
+  FTAR_CHECK_HIP(hipMemcpy(p, t.data(), sizeof t, hipMemcpyHostToDevice));
+  std::lock_guard<std::mutex> g(g_tokens_mu);
+  g_tokens[p] = t;
   return FTAR_SUCCESS;
 }
 
@@ -106,7 +136,33 @@ ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p) {
   trace("ipc_import: open (offset %llu)", (unsigned long long)ref.offset);
   FTAR_CHECK_HIP(hipIpcOpenMemHandle(base, ref.handle, hipIpcMemLazyEnablePeerAccess));
   *p = static_cast<char*>(*base) + ref.offset;
-  trace("ipc_import: mapped at %p", *base);
+  // verify the mapping: the runtime has been seen to map the wrong memory after regrowth
+  std::string bad;
+  hipDeviceptr_t b2 = nullptr;
+  size_t sz = 0;
+  if (hipMemGetAddressRange(&b2, &sz, *p) == hipSuccess) {
+    if (sz != ref.size) bad = "size " + std::to_string(sz) + " != " + std::to_string(ref.size);
+  } else {
+    (void)hipGetLastError();
+  }
+  if (bad.empty() && ref.stamped) {
+    uint64_t got[2] = {0, 0};
+    if (hipMemcpy(got, *p, sizeof got, hipMemcpyDeviceToHost) != hipSuccess) {
+      (void)hipGetLastError();
+      bad = "token unreadable";
+    } else if (got[0] != ref.token[0] || got[1] != ref.token[1]) {
+      bad = "token mismatch";
+    }
+  }
+  if (!bad.empty()) {
+    trace("ipc_import: mapping at %p rejected (%s)", *base, bad.c_str());
+    hip_ignore(hipIpcCloseMemHandle(*base));
+    *base = nullptr;
+    *p = nullptr;
+    set_error("ipc_import: the mapping does not show the peer's buffer (" + bad + ")", __FILE__, __LINE__);
+    return FTAR_ERR_HIP;
+  }
+  trace("ipc_import: mapped at %p (verified)", *base);
   return FTAR_SUCCESS;
 }
 
@@ -548,7 +604,10 @@ class HostTransport final : public Transport {
   }
   ~HostTransport() override {
     unmap_peers(&ppeers_, rank_);
-    if (pbuf_) hip_ignore(hipFree(pbuf_));
+    if (pbuf_) {
+      forget_token(pbuf_);
+      hip_ignore(hipFree(pbuf_));
+    }
   }
   // Point-to-point through a bounce buffer (EXPERIMENTAL, FTAR_HOST_P2P=1),
   // completed inside group_end with host collectives (no RCCL): every sender copies its blocks into its own
@@ -669,10 +728,13 @@ class HostTransport final : public Transport {
       if (o.peer < 0 || o.peer >= nranks_ || o.peer == rank_) keep(FTAR_ERR_INVALID_ARG);
       if (std::find(streams.begin(), streams.end(), o.s) == streams.end()) streams.push_back(o.s);
     }
-    auto sync = [&] {
+    auto sync = [&](const char* what) {
+      trace("rank %d: p2p step %llu: sync %s (%zu streams)", rank_, (unsigned long long)steps_, what, streams.size());
       for (hipStream_t s : streams)
         if (hipStreamSynchronize(s) != hipSuccess) keep(FTAR_ERR_HIP);
+      trace("rank %d: p2p step %llu: synced %s", rank_, (unsigned long long)steps_, what);
     };
+    ++steps_;
     // 1. the bounce buffer holds this step's largest send volume on any rank (collective growth)
     uint64_t need = 0;
     for (const Op& o : ops)
@@ -693,7 +755,7 @@ class HostTransport final : public Transport {
       mine.push_back({o.peer, 0, off, o.bytes});
       off += (o.bytes + 255) & ~uint64_t(255);
     }
-    sync();
+    sync("staged sends");
     // 3. publish every rank's staged sends
     int32_t cnt = (int32_t)mine.size();
     std::vector<int32_t> cnts(nranks_);
@@ -721,7 +783,7 @@ class HostTransport final : public Transport {
         keep(launch_gather(&seg, 1, o.s));
       }
     }
-    sync();
+    sync("receives");
     // 5. all copies out are done (the senders may reuse their buffers); agree on the outcome
     int32_t bad = st == FTAR_SUCCESS ? 0 : 1;
     std::vector<int32_t> bads(nranks_);
@@ -735,19 +797,50 @@ class HostTransport final : public Transport {
   }
   // collective: every rank calls it with the same `bytes` (the step's maximum)
   ftar_status_t grow(uint64_t bytes) {
-    unmap_peers(&ppeers_, rank_);
+    // new buffer mapped first, old mappings and buffer released after (see ensure_xbuf)
+    std::vector<char*> peers;
     void* fresh = nullptr;
     size_t got = 0;
-    (void)alloc_exportable(std::max<uint64_t>(bytes, 2 * pbuf_bytes_), true, &fresh, &got);
-    if (pbuf_) hip_ignore(hipFree(pbuf_));
-    pbuf_ = fresh;
-    pbuf_bytes_ = fresh ? got : 0;
-    const ftar_status_t st = map_peers(pbuf_, rank_, nranks_, &ppeers_);
-    if (st != FTAR_SUCCESS) pbuf_bytes_ = 0;
+    const ftar_status_t st = map_fresh(std::max<uint64_t>(bytes, 2 * pbuf_bytes_), &fresh, &got, &peers);
+    unmap_peers(&ppeers_, rank_);
+    if (pbuf_) {
+      forget_token(pbuf_);
+      hip_ignore(hipFree(pbuf_));
+    }
+    pbuf_ = st == FTAR_SUCCESS ? fresh : nullptr;
+    pbuf_bytes_ = st == FTAR_SUCCESS ? got : 0;
+    ppeers_.swap(peers);
+    return st;
+  }
+  // collective: a fresh stamped buffer of >= bytes mapped by every rank; a
+  // mapping that fails verification on any rank is retried (all ranks agree)
+  // with the failed allocation kept alive, so the next one lands elsewhere
+  ftar_status_t map_fresh(size_t bytes, void** buf, size_t* have, std::vector<char*>* peers) {
+    std::vector<void*> failed;
+    ftar_status_t st = FTAR_ERR_HIP;
+    for (int attempt = 0; attempt < 3 && st != FTAR_SUCCESS; ++attempt) {
+      void* fresh = nullptr;
+      size_t got = 0;
+      if (alloc_exportable(bytes, true, &fresh, &got) == FTAR_SUCCESS && stamp_token(fresh) != FTAR_SUCCESS) {
+        hip_ignore(hipFree(fresh));
+        fresh = nullptr;
+      }
+      st = map_peers(fresh, rank_, nranks_, peers);
+      if (st == FTAR_SUCCESS) {
+        *buf = fresh;
+        *have = got;
+      } else if (fresh) {
+        trace("rank %d: mapping of %p failed (%s), retrying", rank_, fresh, last_error());
+        failed.push_back(fresh);
+      }
+    }
+    for (void* f : failed) {
+      forget_token(f);
+      hip_ignore(hipFree(f));
+    }
     return st;
   }
   ftar_status_t gather(const void* mine, void* all, size_t bytes) {
-    trace("host gather %zu bytes", bytes);
     if (fn_(mine, all, bytes, user_) != 0) {
       set_error("host transport: the caller's allgather failed", __FILE__, __LINE__);
       return FTAR_ERR_INTERNAL;
@@ -760,6 +853,7 @@ class HostTransport final : public Transport {
   std::map<char*, void*> bases_;
   std::vector<Op> ops_;
   int depth_ = 0;
+  unsigned long long steps_ = 0;  // p2p steps so far (trace)
   bool p2p_ = false;      // FTAR_HOST_P2P: the bounce-buffer p2p below (experimental, off by default)
   void* pbuf_ = nullptr;  // bounce buffer of the p2p steps, IPC-mapped by every rank
   size_t pbuf_bytes_ = 0;

@@ -569,9 +569,9 @@ def bench_distributed(a):
             continue
         seen.add(key)
         forms = ["direct"] + (["collective"] if (not t.ring and n % world == 0) else []) + ["stages"]
-        if a.host_comm:
-            # the host transport's p2p is a host-synchronous bounce-buffer fallback (RCCL-less MPI runs), not a
-            # data path to time; long runs of it stalled in the host collective, so the peer forms only
+        if a.host_comm and os.environ.get("FTAR_HOST_P2P", "0") in ("", "0"):
+            # the host transport's p2p is an experimental host-synchronous bounce-buffer fallback (FTAR_HOST_P2P=1,
+            # DESIGN §4), not a data path to time: without it, the peer forms only
             forms = []
         for form in forms:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
