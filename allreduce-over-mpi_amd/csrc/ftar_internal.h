@@ -189,8 +189,9 @@ struct IpcRef {
   uint64_t offset;
   uint64_t valid;     // 1 when the export succeeded: peers never open a failed rank's handle
   uint64_t size;      // the exported allocation's size
-  uint64_t stamped;   // 1: the first 16 bytes at the pointer are a fresh random token (stamp_token) ...
-  uint64_t token[2];  // ... whose value this is; the importer reads them back through its mapping
+  uint64_t stamped;   // 1: the first 16 bytes at the pointer are a fresh random token (stamp_token);
+                      // 2: they are a caller's buffer's current content (registration) ...
+  uint64_t token[2];  // ... and this is their value; the importer reads them back through its mapping
   uint64_t pad[2];
 };
 static_assert(sizeof(IpcRef) == 128, "IpcRef layout");

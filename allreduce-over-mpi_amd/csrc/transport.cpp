@@ -108,12 +108,20 @@ ftar_status_t ipc_export(const void* p, IpcRef* out) {
     return FTAR_ERR_HIP;
   }
   out->size = size;
-  std::lock_guard<std::mutex> g(g_tokens_mu);
-  auto it = g_tokens.find(p);
-  if (it != g_tokens.end()) {
-    out->stamped = 1;
-    out->token[0] = it->second[0];
-    out->token[1] = it->second[1];
+  {
+    std::lock_guard<std::mutex> g(g_tokens_mu);
+    auto it = g_tokens.find(p);
+    if (it != g_tokens.end()) {
+      out->stamped = 1;
+      out->token[0] = it->second[0];
+      out->token[1] = it->second[1];
+    }
+  }
+  if (!out->stamped && size - out->offset >= sizeof out->token) {
+    // a caller's buffer (registration): its first 16 bytes as they are now -- the importers must read the
+    // same through their mappings (the buffer may not be written while it is being registered)
+    if (hipMemcpy(out->token, p, sizeof out->token, hipMemcpyDeviceToHost) == hipSuccess) out->stamped = 2;
+    else (void)hipGetLastError();
   }
   out->valid = 1;
   return FTAR_SUCCESS;

@@ -211,6 +211,8 @@ ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode);
  * peers' outputs, two barriers, no copy.  Mixing registered and unregistered
  * buffers across ranks in one call is undefined.  deregister is local; the
  * buffer must not be freed before it (or before the calls using it ended).
+ * The buffer must not be written while it is being registered: every peer
+ * verifies its mapping against the owner's current first 16 bytes.
  * Under HIP runtimes older than 7.2 an allocation whose size has bit 31 set
  * cannot be registered (FTAR_ERR_HIP on every rank): those runtimes block in
  * hipIpcOpenMemHandle for such sizes.  FTAR_IPC_SIZE_GUARD=0|1 overrides. */
