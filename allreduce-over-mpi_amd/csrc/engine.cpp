@@ -408,24 +408,51 @@ ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int
   FTAR_CHECK_HIP(hipEventCreate(&e1));
   ftar_status_t st = FTAR_SUCCESS;
   const int nxt = (me + 1) % P, prv = (me + P - 1) % P;
-  // 0 local copy | 1 read from one peer | 2 read from all | 3 write to one | 4 write to all
-  for (int mode = 0; mode < std::min(nout, 5) && st == FTAR_SUCCESS; ++mode) {
+  // DMA modes: one hipMemcpyAsync per peer, each on its own stream (forked from and joined back into the
+  // comm stream), so the copy engines rather than CUs move the bytes
+  std::vector<hipStream_t> ds;
+  std::vector<hipEvent_t> dj;
+  hipEvent_t fork = nullptr;
+  auto dma = [&](const std::vector<Segment>& segs) -> ftar_status_t {
+    if (!fork) FTAR_CHECK_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    while (ds.size() < segs.size()) {
+      hipStream_t t;
+      hipEvent_t e;
+      FTAR_CHECK_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+      FTAR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      ds.push_back(t);
+      dj.push_back(e);
+    }
+    FTAR_CHECK_HIP(hipEventRecord(fork, c->comm_s));
+    for (size_t i = 0; i < segs.size(); ++i) {
+      FTAR_CHECK_HIP(hipStreamWaitEvent(ds[i], fork, 0));
+      FTAR_CHECK_HIP(hipMemcpyAsync(segs[i].dst, segs[i].src, segs[i].bytes, hipMemcpyDeviceToDevice, ds[i]));
+      FTAR_CHECK_HIP(hipEventRecord(dj[i], ds[i]));
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, dj[i], 0));
+    }
+    return FTAR_SUCCESS;
+  };
+  // 0 local copy | 1 read from one peer | 2 read from all | 3 write to one | 4 write to all (copy kernels)
+  // 5 read from all | 6 write to all (DMA engines)
+  for (int mode = 0; mode < std::min(nout, 7) && st == FTAR_SUCCESS; ++mode) {
     std::vector<Segment> segs;
     if (mode == 0) segs.push_back({send_slot(X, 0), recv_slot(X, 0), bytes});
     if (mode == 1 && P > 1) segs.push_back({send_slot(Xq[nxt], me), recv_slot(X, nxt), bytes});
     if (mode == 3 && P > 1) segs.push_back({send_slot(X, prv), recv_slot(Xq[prv], me), bytes});
     for (int q = 0; q < P; ++q) {
       if (q == me) continue;
-      if (mode == 2) segs.push_back({send_slot(Xq[q], me), recv_slot(X, q), bytes});
-      if (mode == 4) segs.push_back({send_slot(X, q), recv_slot(Xq[q], me), bytes});
+      if (mode == 2 || mode == 5) segs.push_back({send_slot(Xq[q], me), recv_slot(X, q), bytes});
+      if (mode == 4 || mode == 6) segs.push_back({send_slot(X, q), recv_slot(Xq[q], me), bytes});
     }
     out[mode] = 0.0;
     if (segs.empty()) continue;
-    if ((st = launch_gather(segs.data(), (int)segs.size(), c->comm_s, true, max_wg_per_seg)) != FTAR_SUCCESS) break;  // warm
+    auto copy = [&]() {
+      return mode >= 5 ? dma(segs) : launch_gather(segs.data(), (int)segs.size(), c->comm_s, true, max_wg_per_seg);
+    };
+    if ((st = copy()) != FTAR_SUCCESS) break;  // warm
     if ((st = tp->barrier(c->comm_s)) != FTAR_SUCCESS) break;
     if (hipEventRecord(e0, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
-    for (int i = 0; i < iters && st == FTAR_SUCCESS; ++i)
-      st = launch_gather(segs.data(), (int)segs.size(), c->comm_s, true, max_wg_per_seg);
+    for (int i = 0; i < iters && st == FTAR_SUCCESS; ++i) st = copy();
     if (st == FTAR_SUCCESS && hipEventRecord(e1, c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
     if (st == FTAR_SUCCESS) st = tp->barrier(c->comm_s);
     if (st == FTAR_SUCCESS && hipStreamSynchronize(c->comm_s) != hipSuccess) st = FTAR_ERR_HIP;
@@ -433,6 +460,10 @@ ftar_status_t xgmi_probe(ftar_comm* c, size_t bytes, int iters, double* out, int
     if (st == FTAR_SUCCESS && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) st = FTAR_ERR_HIP;
     if (st == FTAR_SUCCESS && ms > 0.f) out[mode] = (double)segs.size() * bytes * iters / (ms * 1e-3) / 1e9;
   }
+  hip_ignore(hipStreamSynchronize(c->comm_s));
+  for (hipStream_t t : ds) hip_ignore(hipStreamDestroy(t));
+  for (hipEvent_t e : dj) hip_ignore(hipEventDestroy(e));
+  if (fork) hip_ignore(hipEventDestroy(fork));
   hip_ignore(hipEventDestroy(e0));
   hip_ignore(hipEventDestroy(e1));
   return st;

@@ -409,14 +409,15 @@ class Comm:
         """Collective xGMI calibration (ftar_xgmi_probe): GB/s of copy kernels through the exchange buffers,
         every rank running the same pattern at once.  wg_per_peer > 0 caps the copy kernel at that many
         256-thread workgroups per peer (how many CUs it takes to fill the links)."""
-        out = (ctypes.c_double * 5)()
+        k = 5 if wg_per_peer else 7   # (the DMA modes do not depend on a workgroup cap)
+        out = (ctypes.c_double * k)()
         if wg_per_peer:
-            _check(_lib.ftar_debug_xgmi_probe_cap(self.handle, bytes_per_peer, iters, wg_per_peer, out, 5),
+            _check(_lib.ftar_debug_xgmi_probe_cap(self.handle, bytes_per_peer, iters, wg_per_peer, out, k),
                    "ftar_debug_xgmi_probe_cap")
         else:
-            _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, 5), "ftar_xgmi_probe")
-        return dict(zip(("local_copy", "read_one_peer", "read_all_peers", "write_one_peer", "write_all_peers"),
-                        (round(v, 2) for v in out)))
+            _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, k), "ftar_xgmi_probe")
+        return dict(zip(("local_copy", "read_one_peer", "read_all_peers", "write_one_peer", "write_all_peers",
+                         "dma_read_all_peers", "dma_write_all_peers"), (round(v, 2) for v in out)))
 
     @property
     def host_chunk_bytes(self):

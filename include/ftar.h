@@ -261,7 +261,9 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
  * for copy kernels through the peer-direct exchange buffers, all ranks running
  * the same pattern at once -- gbps[0] local HBM copy, [1] read from one peer
  * (ring neighbour), [2] read from all peers at once (aggregate), [3] write to
- * one peer, [4] write to all peers at once (aggregate).  bytes_per_peer per
+ * one peer, [4] write to all peers at once (aggregate), all by copy kernels;
+ * [5] read from / [6] write to all peers by the DMA engines (one
+ * hipMemcpyAsync per peer, each on its own stream).  bytes_per_peer per
  * copy, `iters` timed launches; grows the exchange buffer to 2*P*bytes. */
 ftar_status_t ftar_xgmi_probe(ftar_comm_t comm, size_t bytes_per_peer, int iters, double* gbps, int n);
 /* Phase timing of the last call on this communicator (diagnostic; off by
