@@ -45,6 +45,12 @@ struct ftar_comm {
   // peer-form tuning (ftar_debug_set_peer_tuning; bench.py sweeps both on a
   // real node): nontemporal copies, LDS-staged fold (false: register kernel)
   bool peer_nt = true, peer_lds = true;
+  // peer_dma: the xGMI copies of the peer forms (gather, scatter, push) by the DMA engines, one
+  // hipMemcpyAsync per peer on its own stream forked from and joined back into comm_s
+  bool peer_dma = false;
+  std::vector<hipStream_t> dma_s;
+  std::vector<hipEvent_t> dma_ev;
+  hipEvent_t dma_fork = nullptr;
   void* xbuf = nullptr;            // peer-direct exchange buffer (IPC-exported), grow-only
   size_t xbuf_bytes = 0;
   std::vector<char*> xpeers;       // every rank's exchange buffer, mapped here
@@ -154,6 +160,9 @@ void comm_teardown(ftar_comm* c) {
     hip_ignore(hipFree(c->xbuf));
   }
   c->tp.reset();
+  for (hipStream_t t : c->dma_s) hip_ignore(hipStreamDestroy(t));
+  for (hipEvent_t e : c->dma_ev) hip_ignore(hipEventDestroy(e));
+  if (c->dma_fork) hip_ignore(hipEventDestroy(c->dma_fork));
   for (auto e : c->events) hip_ignore(hipEventDestroy(e));
   for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
   if (c->scratch) hip_ignore(hipFree(c->scratch));
@@ -299,6 +308,32 @@ char* reg_peer(const ftar_comm::Reg* r, const void* p, int peer) {
 }
 }  // namespace
 
+namespace {
+// the peer forms' cross-GPU copies: one copy-kernel launch over every segment (every link at once), or with
+// peer_dma one DMA copy per segment, each on its own stream, all joined back into comm_s
+ftar_status_t peer_copy(ftar_comm* c, const std::vector<Segment>& segs) {
+  if (!c->peer_dma) return launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt);
+  if (!c->dma_fork) FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->dma_fork, hipEventDisableTiming));
+  while (c->dma_s.size() < segs.size()) {
+    hipStream_t t;
+    hipEvent_t e;
+    FTAR_CHECK_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    FTAR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->dma_s.push_back(t);
+    c->dma_ev.push_back(e);
+  }
+  FTAR_CHECK_HIP(hipEventRecord(c->dma_fork, c->comm_s));
+  for (size_t i = 0; i < segs.size(); ++i) {
+    if (!segs[i].bytes) continue;
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->dma_s[i], c->dma_fork, 0));
+    FTAR_CHECK_HIP(hipMemcpyAsync(segs[i].dst, segs[i].src, segs[i].bytes, hipMemcpyDeviceToDevice, c->dma_s[i]));
+    FTAR_CHECK_HIP(hipEventRecord(c->dma_ev[i], c->dma_s[i]));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, c->dma_ev[i], 0));
+  }
+  return FTAR_SUCCESS;
+}
+}  // namespace
+
 ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                              const Plan& plan, ftar_comm* c, hipStream_t stream) {
   const size_t esz = dtype_size(dt), bytes = count * esz;
@@ -336,7 +371,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     for (const Transfer& x : ag.recvs)
       segs.push_back({reg_peer(rout, out, x.peer) + x.off * esz, out + x.off * esz, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
+    FTAR_RETURN_IF(peer_copy(c, segs));
     FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my buffers after the call
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -356,7 +391,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     // all-gather: every owner's final block from its exchange buffer, one launch
     for (const ReduceItem& r : rs.reduces) segs.push_back({X + r.off * esz, out + r.off * esz, r.len * esz});
     for (const Transfer& x : ag.recvs) segs.push_back({Xq[x.peer] + x.off * esz, out + x.off * esz, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
+    FTAR_RETURN_IF(peer_copy(c, segs));
     FTAR_RETURN_IF(mark(c, "gather (remote reads)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -364,7 +399,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     // scatter my copy of every peer's block into its slot for me, all links at once
     for (const Transfer& x : rs.sends)
       segs.push_back({in + x.off * esz, Xq[x.peer] + (size_t)c->rank * slot_bytes, x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
+    FTAR_RETURN_IF(peer_copy(c, segs));
     FTAR_RETURN_IF(mark(c, "scatter (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -377,7 +412,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     for (const Transfer& x : ag.sends)
       segs.push_back({out + x.off * esz, (zc ? reg_peer(rout, out, x.peer) : Xq[x.peer] + final_at) + x.off * esz,
                       x.len * esz});
-    FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
+    FTAR_RETURN_IF(peer_copy(c, segs));
     FTAR_RETURN_IF(mark(c, "push (remote writes)", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -972,6 +1007,13 @@ ftar_status_t ftar_debug_set_peer_tuning(ftar_comm_t comm, int nt, int lds) {
   std::lock_guard<std::mutex> g(comm->mu);
   comm->peer_nt = nt != 0;
   comm->peer_lds = lds != 0;
+  return FTAR_SUCCESS;
+}
+// Test/tuning hook (not in ftar.h): the peer forms' cross-GPU copies by the DMA engines.
+ftar_status_t ftar_debug_set_peer_dma(ftar_comm_t comm, int dma) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->peer_dma = dma != 0;
   return FTAR_SUCCESS;
 }
 

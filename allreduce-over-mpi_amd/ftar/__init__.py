@@ -110,6 +110,7 @@ _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_
                                            ctypes.POINTER(Topo), ctypes.POINTER(_vp), _int, ctypes.POINTER(_vp)]
 _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
+_lib.ftar_debug_set_peer_dma.argtypes = [_vp, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
@@ -377,10 +378,12 @@ class Comm:
     def peer_direct(self, mode):
         _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
 
-    def peer_tuning(self, nt=True, lds=True):
-        """Peer forms: nontemporal copies (nt) and the LDS-staged fold (lds; False = register kernel).
-        Tuning hook for bench.py's sweep (ftar_debug_set_peer_tuning); results are identical either way."""
+    def peer_tuning(self, nt=True, lds=True, dma=False):
+        """Peer forms: nontemporal copies (nt), the LDS-staged fold (lds; False = register kernel), and the
+        cross-GPU copies by the DMA engines (dma).  Tuning hook for bench.py's sweep
+        (ftar_debug_set_peer_tuning / _dma); results are identical either way."""
         _check(_lib.ftar_debug_set_peer_tuning(self.handle, 1 if nt else 0, 1 if lds else 0), "peer_tuning")
+        _check(_lib.ftar_debug_set_peer_dma(self.handle, 1 if dma else 0), "peer_dma")
 
     def register(self, buf, nbytes):
         """Collective: register this rank's buffer (device pointer or tensor) for the peer forms' in-place

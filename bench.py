@@ -352,9 +352,10 @@ def bench_distributed(a):
         return t.item() / max(1, steps) * 1e3
 
     def run_with(topo, chunk, form="direct"):
-        # peer-form tuning suffix: ":plain" = plain (not nontemporal) copies, ":vec" = register-kernel fold
+        # peer-form tuning suffix: ":plain" = plain (not nontemporal) copies, ":vec" = register-kernel fold,
+        # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
-        comm.peer_tuning(nt=tune != "plain", lds=tune != "vec")
+        comm.peer_tuning(nt=tune != "plain", lds=tune != "vec", dma=tune == "dma")
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
         rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
         kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
@@ -584,7 +585,8 @@ def bench_distributed(a):
             plan += [(t, default_chunk, f) for f in ("peer-read", "peer-write", "peer-read-reg", "peer-write-reg")]
             if key == str(default_topo):  # copy policy and fold kernel over xGMI (same bits)
                 plan += [(t, default_chunk, f) for f in ("peer-read-reg:plain", "peer-write-reg:plain",
-                                                         "peer-read-reg:vec", "peer-write-reg:vec")]
+                                                         "peer-read-reg:vec", "peer-write-reg:vec",
+                                                         "peer-read-reg:dma", "peer-write-reg:dma", "peer-read:dma")]
     plan.sort(key=lambda p: p[2].startswith("peer-"))  # stable: every RCCL configuration before any peer one
     sweep_t0 = time.time()
     probed = False

@@ -305,11 +305,11 @@ def test_random_soak_all_forms(seed):
         rs = rng.choice(["stages", "direct"])
         ag = rng.choice(["stages", "direct", "collective"])
         peer = rng.choice([0, 0, "read", "write"])
-        nt, lds = rng.random() < 0.7, rng.random() < 0.7   # peer tuning variants (bench.py sweeps them)
+        nt, lds, dma = rng.random() < 0.7, rng.random() < 0.7, rng.random() < 0.2   # bench.py's peer variants
         g = group(c["P"])
         g.set_peer_direct(peer)
         for cm in g.comms:
-            cm.peer_tuning(nt=nt, lds=lds)
+            cm.peer_tuning(nt=nt, lds=lds, dma=dma)
         try:
             outs = run_group(c["ins"], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1,
                              c["oop"], chunk_bytes=c["chunk"], ag=ag, rs=rs)

@@ -317,16 +317,17 @@ def test_peer_registered_phases_skip_the_local_pass():
 
 
 @pytest.mark.parametrize("mode", ["read", "write"])
-@pytest.mark.parametrize("nt,lds", [(False, True), (True, False), (False, False)])
+@pytest.mark.parametrize("nt,lds,dma", [(False, True, False), (True, False, False), (False, False, False),
+                                        (True, True, True)])
 @pytest.mark.parametrize("P,topo,dt", [(4, "4", "f32"), (8, "2,4", "f32"), (4, "1", "bf16"), (8, "8", "bf16")])
-def test_peer_tuning_same_bits(mode, nt, lds, P, topo, dt):
-    """bench.py's peer tuning variants (plain copies, register-kernel fold) change no bit: the fold's
+def test_peer_tuning_same_bits(mode, nt, lds, dma, P, topo, dt):
+    """bench.py's peer tuning variants (plain copies, register-kernel fold, DMA-engine copies) change no bit: the fold's
     operands and order are the plan's either way ("2,4" folds nested)."""
     n = 200_003
     ins = [fi.fill(dt, 91, r, n) for r in range(P)]
     g = group(P)
     for c in g.comms:
-        c.peer_tuning(nt=nt, lds=lds)
+        c.peer_tuning(nt=nt, lds=lds, dma=dma)
     try:
         got = run_peer(ins, topo, dtype=fi.BY_NAME[dt], mode=mode, registered=True, outofplace=True)
     finally:
