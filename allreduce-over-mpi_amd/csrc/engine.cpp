@@ -215,14 +215,13 @@ bool peer_eligible(const Plan& plan) {
 namespace {
 // grow-only exchange buffer, exported and mapped by every rank (collective)
 //
-// The new buffer is allocated while the old one and the old peer mappings are
-// still alive, and it must pass an export check before it is used: a fresh
-// allocation whose address range was recently an IPC mapping (closed) can
-// fail hipIpcGetMemHandle with "invalid argument" (seen on ROCm 7.2 with
-// dmabuf IPC, tools/peer_rehearsal.py), so such an allocation is set aside
-// and another one taken.  Nothing here returns before map_peers: every rank
-// must reach the exchange, a failed rank publishes an invalid reference and
-// all ranks fail together.
+// Under the HIP runtime torch bundles (7.0), a fresh allocation whose address
+// range was an IPC mapping a moment before can fail hipIpcGetMemHandle
+// (alloc_exportable sets such allocations aside), and an import can map the
+// wrong memory after regrowth (ipc_import verifies every mapping against the
+// owner's stamped token).  Nothing here returns before map_peers: every rank
+// must reach the exchange; a failed rank publishes an invalid reference and
+// all ranks fail, and retry, together.
 ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   if (bytes <= c->xbuf_bytes && !c->xpeers.empty()) return FTAR_SUCCESS;
   Transport* tp = c->tp.get();

@@ -18,17 +18,18 @@
 //                   on a single GPU (tests) and in single-process groups.
 #include <rccl/rccl.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <array>
-#include <random>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
-#include <unistd.h>
 #include <cstring>
 #include <deque>
 #include <map>
 #include <mutex>
+#include <random>
 
 #include "ftar_internal.h"
 
@@ -128,8 +129,12 @@ ftar_status_t ipc_export(const void* p, IpcRef* out) {
 }
 
 ftar_status_t stamp_token(void* p) {
-  static std::mt19937_64 rng(std::random_device{}() ^ (uint64_t)getpid() << 32);
-  std::array<uint64_t, 2> t{rng(), rng()};
+  std::array<uint64_t, 2> t;
+  {
+    std::lock_guard<std::mutex> g(g_tokens_mu);
+    static std::mt19937_64 rng(std::random_device{}() ^ (uint64_t)getpid() << 32);
+    t = {rng(), rng()};
+  }
   FTAR_CHECK_HIP(hipMemcpy(p, t.data(), sizeof t, hipMemcpyHostToDevice));
   std::lock_guard<std::mutex> g(g_tokens_mu);
   g_tokens[p] = t;
@@ -227,10 +232,10 @@ class RcclTransport final : public Transport {
     peers->assign(nranks, nullptr);
     for (int q = 0; q < nranks && why.empty(); ++q)  // a failed export anywhere: nobody opens anything
       if (all[q].valid != 1) why = std::string("rank ") + std::to_string(q) + " could not export its buffer";
-    // The ranks open the peers' handles one rank at a time: two processes
-    // opening each other's handles at the same moment can block each other
-    // for good inside hipIpcOpenMemHandle (seen with 2 GiB buffers on ROCm 7.2
-    // dmabuf IPC, tools/peer_rehearsal.py).  Each turn ends with a host-side
+    // The ranks open the peers' handles one rank at a time (a precaution
+    // taken while chasing the 2 GiB open hang, ipc_size_guard, which turned
+    // out to be a runtime size bug; turns cost P host agreements per mapping,
+    // nothing per call).  Each turn ends with a host-side
     // agreement on the failures so far, so every rank also learns whether
     // every rank mapped every peer (a rank that failed alone would otherwise
     // leave the others waiting in the next barrier).
@@ -494,12 +499,6 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
 
-  static ftar_status_t unsupported() {
-    set_error("host transport: point-to-point transfers are off (peer-direct forms only; FTAR_HOST_P2P=1 enables "
-              "the experimental bounce-buffer p2p)",
-              __FILE__, __LINE__);
-    return FTAR_ERR_UNSUPPORTED;
-  }
   ftar_status_t flush() {
     std::vector<Op> ops;
     ops.swap(ops_);
