@@ -1,4 +1,4 @@
-"""The N>1 path on the CPU: world_size 2..5 processes over gloo.
+"""The N>1 path on the CPU: world_size 2..8 processes over gloo.
 
 Each process builds ONLY its own rank's plan with libftar (exactly what
 ftar_allreduce does on its GPU), then executes it with gloo point-to-point
@@ -80,7 +80,10 @@ CASES = ["ar_P2_t1_l0_f32_op0_n1003", "ar_P2_t2_l0_f32_op0_n65541", "ar_P4_t2-2_
          "ar_P4_t1_l0_f32_op0_n17", "ar_P5_t2-2_l1_f32_op0_n1003", "ar_P4_t2-2_l0_f32_op0_n1003_oop",
          # the one-round forms at a node's size: direct ring and direct multi-stage trees, 8 processes
          "ar_P4_t2-2_l0_f64_op0_n1003", "ar_P8_t2-2-2_l0_f32_op0_n1003", "ar_P8_t2-4_l0_f32_op0_n65541",
-         "ar_P8_t1_l0_f32_op0_n1003"]
+         "ar_P8_t1_l0_f32_op0_n1003",
+         # C5's width-8 tree and the other factorization of 8; a lonely rank at 7 and a 6-rank mixed radix
+         "ar_P8_t8_l0_f32_op0_n65541", "ar_P8_t4-2_l0_f32_op0_n1003", "ar_P7_t2-3_l1_f32_op0_n1003",
+         "ar_P6_t3-2_l0_f32_op0_n17"]
 
 
 @pytest.mark.parametrize("case_id", CASES)
