@@ -25,7 +25,9 @@ a = ap.parse_args()
 
 def rows(path, counter):
     with open(path) as f:
-        return [r for r in csv.DictReader(f) if r["Counter_Name"] == counter and ("reduce_lds_kernel" in r["Kernel_Name"] or "reduce_vec_kernel" in r["Kernel_Name"])]
+        # only the bench workload's kernel (k = a.k); bench.py also launches a k = 8 line item
+        return [r for r in csv.DictReader(f) if r["Counter_Name"] == counter and f"F32Sum, {a.k}," in r["Kernel_Name"]
+                and ("reduce_lds_kernel" in r["Kernel_Name"] or "reduce_vec_kernel" in r["Kernel_Name"])]
 
 
 def values(path, counter):
