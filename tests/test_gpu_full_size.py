@@ -78,3 +78,42 @@ def test_allreduce_full_size_properties(P, n, dt, topo, form):
         xs.clear()
         ys.clear()
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("topo", ["1", "2"])
+def test_allreduce_past_int32_elements(topo):
+    """2^31 + 77 u8 elements per rank (the reference's `int count` stops below 2^31, mpi_mod.hpp:1724): block
+    offsets and piece indices past 2^31 in the engine.  u8 sums wrap and are associative, so the sample check is
+    exact in any order; then linearity over the whole bucket: inputs + 1 on every rank give result + P (mod 256)."""
+    import torch
+
+    import ftar
+    P, n = 2, (1 << 31) + 77
+    dev = torch.device("cuda", 0)
+    g = ftar.Comm.init_local(P)
+    xs, ys = [], []
+    try:
+        for r in range(P):
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(777 + r)
+            xs.append(torch.randint(0, 256, (n,), generator=gen, dtype=torch.uint8, device=dev))
+            ys.append(torch.empty(n, dtype=torch.uint8, device=dev))
+        idx = _sample_index(n, P)
+        it = torch.from_numpy(idx).to(dev)
+        g.allreduce(xs, ys, n, "u8", "sum", topo_=topo)
+        torch.cuda.synchronize()
+        exp = sum(x[it].to(torch.int64) for x in xs) % 256
+        assert torch.equal(ys[0][it].to(torch.int64), exp)
+        assert torch.equal(ys[1], ys[0])
+        y0 = ys[0].clone()
+        for x in xs:
+            x.add_(1)
+        g.allreduce(xs, ys, n, "u8", "sum", topo_=topo)
+        torch.cuda.synchronize()
+        assert torch.equal(ys[0], y0.add_(P)), "linearity: inputs + 1 must give result + P (mod 256)"
+        assert torch.equal(ys[1], ys[0])
+    finally:
+        g.destroy()
+        xs.clear()
+        ys.clear()
+        torch.cuda.empty_cache()
