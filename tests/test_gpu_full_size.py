@@ -117,3 +117,49 @@ def test_allreduce_past_int32_elements(topo):
         xs.clear()
         ys.clear()
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("P,n,dt,topo", [
+    (8, 1 << 28, "f32", "1"),     # C4 through the MPI_Allreduce_FT path (host buffers, in place)
+    (8, 1 << 29, "bf16", "8"),    # C5, same
+])
+def test_host_allreduce_full_size_properties(P, n, dt, topo):
+    """ftar_allreduce_host (H2D / exchange / D2H pipelined per piece) on pinned host buckets of BASELINE's full
+    size, in place like benchmark.cpp:161: the sampled per-element fold, rank agreement, negation symmetry."""
+    import torch
+
+    import ftar
+    tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
+    dev = torch.device("cuda", 0)
+    g = ftar.Comm.init_local(P)
+    hs, orig = [], []
+    try:
+        for r in range(P):
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(5151 + r)
+            hs.append((torch.rand(n, generator=gen, device=dev) * 2 - 1).to(tdt).cpu().pin_memory())
+        orig.extend(h.clone() for h in hs)
+        idx = _sample_index(n, P)
+        it = torch.from_numpy(idx)
+        samp = np.stack([h[it].float().numpy() for h in hs])
+        g.allreduce(None, hs, n, dt, "sum", topo_=topo, host=True)
+        torch.cuda.synchronize()
+        exp = sample_fold.fold(samp, idx, n, "ring" if topo == "1" else "tree", bf16=dt == "bf16")
+        got = hs[0][it].float().numpy()
+        bad = np.nonzero(got.view(np.uint32) != exp.view(np.uint32))[0]
+        assert bad.size == 0, f"{bad.size} sampled elements differ, first at {idx[bad[0]]}"
+        for r in range(1, P):
+            assert torch.equal(hs[r], hs[0]), f"rank {r} differs from rank 0"
+        y0 = hs[0].clone()
+        for h, x in zip(hs, orig):
+            torch.neg(x, out=h)
+        g.allreduce(None, hs, n, dt, "sum", topo_=topo, host=True)
+        torch.cuda.synchronize()
+        assert torch.equal(hs[0], y0.neg_()), "negated inputs did not give the negated result"
+        for r in range(1, P):
+            assert torch.equal(hs[r], hs[0]), f"rank {r} differs from rank 0 (negated call)"
+    finally:
+        g.destroy()
+        hs.clear()
+        orig.clear()
+        torch.cuda.empty_cache()
