@@ -172,3 +172,36 @@ def test_reduce_nested_rejects_bad_shapes():
         with pytest.raises(ftar.FtarError):
             ftar.reduce([p] * 4, p, 4, "f32", "sum", shape=shape)
     ftar.reduce([p] * 4, p, 0, "f32", "sum", shape=[2, 2])   # zero count: no-op
+
+
+@pytest.mark.parametrize("shape", [None, [2, 4]])
+def test_reduce_captures_into_a_hip_graph(shape):
+    """ftar_reduce / ftar_reduce_nested are stream-ordered launches with no host synchronisation, so a bucket's
+    reduce chain can be captured once into a HIP graph and replayed (the launch-bound small-bucket regime):
+    replays give the eager call's bits, and a replay after the sources change reads the new data."""
+    import ftar
+    import torch
+    k, n = 8, (1 << 20) + 3
+    srcs = [torch.from_numpy(fi.fill("f32", 61, j, n)).cuda() for j in range(k)]
+    ptrs = [s.data_ptr() for s in srcs]
+    eager = torch.empty(n, dtype=torch.float32, device="cuda")
+    ftar.reduce(ptrs, eager.data_ptr(), n, "f32", "sum", stream=torch.cuda.current_stream(), shape=shape)
+    out = torch.empty_like(eager)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for _ in range(3):   # a chain of launches in one graph
+                ftar.reduce(ptrs, out.data_ptr(), n, "f32", "sum", stream=side, shape=shape)
+    torch.cuda.current_stream().wait_stream(side)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), eager.view(torch.int32))
+    srcs[0].neg_()
+    srcs[1].neg_()
+    g.replay()
+    ftar.reduce(ptrs, eager.data_ptr(), n, "f32", "sum", stream=torch.cuda.current_stream(), shape=shape)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), eager.view(torch.int32))
