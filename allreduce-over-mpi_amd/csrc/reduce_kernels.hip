@@ -6,17 +6,23 @@
 //   dst[i] = src0[i] OP src1[i] OP ... OP src{k-1}[i]      strictly left to right
 //
 // Design (bandwidth-bound: (k+1)*n*sizeof(T) bytes, ~0 flops per byte, no MFMA):
-//   * 16 B per lane per access (global_load_dwordx4 / global_store_dwordx4),
-//     one wave instruction = 1 KiB contiguous per source: fully coalesced;
-//   * each lane keeps U=2 vectors of every source in flight before combining
-//     (2K outstanding 16-B loads per lane); loads carry the nontemporal hint
-//     (streamed once), stores do not (the next ring step sends that block);
-//     one-shot grid of ceil(nvec / 512) workgroups of 256 (>> 256 CUs);
-//   * source pointers travel in the kernarg segment (no device-side pointer
-//     table, no extra dependent load); K is a template parameter for 2..16;
+//   * 16 B per lane per access, one wave instruction = 1 KiB contiguous per
+//     source: fully coalesced;
+//   * k = 2..16 (fp32/bf16; k = 2 for every type): reduce_lds_kernel stages
+//     U tiles of every source per wave through LDS with LDS-DMA
+//     (global_load_lds_dwordx4, nontemporal) and folds tile by tile as each
+//     tile lands (counted vmcnt); stores are nontemporal too (cold data: every
+//     piece of an AllReduce is new); (U, waves per workgroup) per k below;
+//   * other k / types: reduce_vec_kernel, registers, 2 vectors of every source
+//     per lane in flight, runtime k up to FTAR_MAX_K;
+//   * one-shot grids (>> 256 CUs); source pointers travel in the kernarg
+//     segment (no device-side pointer table);
 //   * unaligned heads/tails (block offsets need not be 16-B aligned) are done
 //     element-wise by workgroup 0 in the same launch; sources whose alignment
-//     differs from dst's take a dword-granular kernel instead;
+//     differs from dst's take an element-wise kernel instead;
+//   * dst may alias a source (the ring folds in place, mpi_mod.hpp:1699):
+//     every lane loads its element of every source before it stores that
+//     element, so no pointer is declared __restrict__;
 //   * arithmetic follows the reference's C++ semantics bit for bit:
 //       float/double in their own precision (no FMA: pure adds),
 //       narrow integers wrap (promotion + truncating store == modular add),
@@ -26,6 +32,7 @@
 #include <algorithm>
 #include <initializer_list>
 #include <type_traits>
+#include <utility>
 
 #include "ftar_internal.h"
 
@@ -42,20 +49,26 @@ constexpr int kTreeLevels = kMaxFoldLevels;
 //    stores; rewriting the same destination back to back -- the reference
 //    harness's loop -- favours plain stores instead, because the MALL absorbs
 //    part of the writes, a regime the hot path never sees);
-//  * k = 2..16 (fp32/bf16; 2..8 for the other types): staged through LDS (LDS-DMA): every wave streams U tiles of 1 KiB
-//    per source into LDS with global_load_lds_dwordx4 (no VGPR landing zone),
-//    waits on its own vmcnt and folds from LDS -- f32 +1 % at k = 2 and +3-5 %
-//    at k = 4..8 over the best register variant with U = 4; 16-bit sums (more
-//    ALU per byte) keep occupancy with fewer tiles as k grows, and so does
-//    every type past k = 9 (LDS holds 4 waves x k x U KiB <= 160 KiB);
+//  * k = 2..16: staged through LDS (LDS-DMA, no VGPR landing zone) -- f32
+//    +1 % at k = 2 and +3-5 % at k = 4..8 over the best register variant
+//    (round 1); folding each tile as it lands instead of after all K x U
+//    loads: +0.5-2 % for f32, up to +8 % for bf16 at k = 8 (round 2);
 //  * larger k (runtime k): registers, 2 vectors per lane, 512-thread workgroups.
 constexpr int kUnroll = 2;
 constexpr int kVecThreads = 512;
 constexpr bool kNtLoads = true, kNtStores = true;
+// Tiles per wave (U) and waves per workgroup (W) of the LDS-staged kernel by
+// element size and k, from a cold-data sweep of 14 (U, W) shapes x k = 2..16
+// x {f32, bf16} on MI355X (tools/kbench_cold.py variants 40-53,
+// profiles/r02/kbench_cold_prog_shapes.log).  Up to k = 4 deep per-wave
+// queues win (U = 3-4); from k = 5 on, two workgroups per CU of 2-6 waves.
 template <class Tr, int K>
-constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? (K <= 8 ? 4 : 2)
-                                                     : (K <= 4 ? 4 : (K <= 6 ? 3 : 2));
-// LDS per workgroup = 4 waves x K x U x 1 KiB (<= 160 KiB): k = 16 at U = 2 stages 128 KiB
+constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 4 : K <= 4 ? 3 : K <= 6 ? 2 : K <= 10 ? 4 : 2)
+                                                     : (K <= 4 ? 4 : K == 5 ? 2 : K == 6 ? 5 : K <= 10 ? 4 : 2);
+template <class Tr, int K>
+constexpr int kLdsWaves = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 4 : K <= 6 ? 6 : K <= 10 ? 2 : 4)
+                                                     : (K <= 4 ? 4 : K == 5 ? 5 : K <= 10 ? 2 : 4);
+// LDS per workgroup = W waves x K x U x 1 KiB (<= 160 KiB): k = 16 at U = 2 stages 128 KiB
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -242,7 +255,7 @@ struct Srcs {
 // ---------------------------------------------------------------------------
 template <class Tr, int K, int U, bool NTL, bool NTS, int BS = kThreads>
 __global__ void __launch_bounds__(BS)
-    reduce_vec_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, void* __restrict__ dst, size_t nvec, int head,
+    reduce_vec_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, void* dst, size_t nvec, int head,
                       int tail) {
   using S = typename Tr::S;
   constexpr int KK = K > 0 ? K : FTAR_MAX_K;
@@ -303,20 +316,32 @@ __global__ void __launch_bounds__(BS)
 }
 
 // LDS-staged reduce: the production kernel for k = 2..16 (launch_k; A/B
-// variants 20/21/31-33 in tools/kbench_cold.py).  Each wave streams U tiles of
-// every source into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
-// instruction, nontemporal, no VGPR destination), waits on its own vmcnt, then
-// every lane reads back its own 16 B with ds_read_b128 and folds.  Nothing is
-// shared between lanes in an element-wise sum, so LDS serves as the landing
-// zone of the loads: more bytes in flight per wave than VGPRs allow (K x U KiB
-// per wave).  Workgroup 0 also does the `head` leading and `tail` trailing
-// elements element-wise, as reduce_vec_kernel does.
-template <class Tr, int K, int U, int AUX>
-__global__ void __launch_bounds__(256)
-    reduce_lds_kernel(Srcs<K> src, void* __restrict__ dst, size_t nvec, int head, int tail) {
+// variants in tools/kbench_cold.py).  Each wave streams U tiles of every
+// source into LDS with LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+// instruction, nontemporal, no VGPR destination); every lane reads its own
+// 16 B back with ds_read_b128 and folds.  Nothing is shared between lanes in
+// an element-wise sum, so LDS serves as the landing zone of the loads: K x U
+// KiB in flight per wave without spending VGPRs on them.
+//   PROG (production): the loads are issued tile-major and tile u is folded
+// and stored as soon as its K loads have landed (counted vmcnt: loads return
+// in order, so the stores also in the count can only make a wait longer),
+// while tiles u+1.. are still in flight.  !PROG waits for all K x U loads
+// first (the round-1 kernel, kept as an A/B variant).
+// Workgroup 0 also does the `head` leading and `tail` trailing elements
+// element-wise, as reduce_vec_kernel does.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "gfx9 vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <class Tr, int K, int U, int W, int AUX, bool PROG>
+__global__ void __launch_bounds__(W * 64)
+    reduce_lds_kernel(Srcs<K> src, void* dst, size_t nvec, int head, int tail) {
+  static_assert(W * U * K <= 160, "LDS per workgroup = W x U x K KiB <= 160 KiB");
   using S = typename Tr::S;
   constexpr int VE = 16 / sizeof(S);
-  __shared__ u32x4 lds[4][K][U][64];
+  __shared__ u32x4 lds[W][U][K][64];
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {  // unaligned head / short tail
     const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
     typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
@@ -324,26 +349,30 @@ __global__ void __launch_bounds__(256)
     static_cast<S*>(dst)[e] = Tr::s_fin(a);
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const size_t base = ((size_t)blockIdx.x * 4 + wave) * (U * 64);
+  const size_t base = ((size_t)blockIdx.x * W + wave) * (U * 64);
   u32x4* d = reinterpret_cast<u32x4*>(static_cast<S*>(dst) + head);
   auto sp = [&](int j) { return reinterpret_cast<const u32x4*>(static_cast<const S*>(src.p[j]) + head); };
   if (base + U * 64 <= nvec) {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int j = 0; j < K; ++j) {
         const u32x4* g = sp(j) + base + u * 64 + lane;
         __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
-                                         (__attribute__((address_space(3))) void*)&lds[wave][j][u][0], 16, 0, AUX);
+                                         (__attribute__((address_space(3))) void*)&lds[wave][u][j][0], 16, 0, AUX);
       }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (!PROG) wait_vmcnt<0>();
+    auto tile = [&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      // the K loads of tile u have landed (a count above 63 waits for more: still exact)
+      if constexpr (PROG) wait_vmcnt<((U - 1 - u) * K > 63 ? 63 : (U - 1 - u) * K)>();
+      typename Tr::VA a = Tr::v_init(lds[wave][u][0][lane]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      typename Tr::VA a = Tr::v_init(lds[wave][0][u][lane]);
-#pragma unroll
-      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, lds[wave][j][u][lane]);
+      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, lds[wave][u][j][lane]);
       st16<kNtStores>(d + base + u * 64 + lane, Tr::v_fin(a));
-    }
+    };
+    [&]<int... I>(std::integer_sequence<int, I...>) { (tile(std::integral_constant<int, I>{}), ...); }
+    (std::make_integer_sequence<int, U>{});
   } else {
     for (int u = 0; u < U; ++u) {
       const size_t v = base + u * 64 + lane;
@@ -355,21 +384,25 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-template <class Tr, int K, int U, int AUX>
+template <class Tr, int K, int U, int W = 4, int AUX = 2, bool PROG = true>
 hipError_t launch_lds(const void* const* srcs, void* dst, size_t nvec, hipStream_t s, int head = 0, int tail = 0) {
-  Srcs<K> a{};
-  for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
-  const size_t per_block = (size_t)4 * U * 64;
-  const size_t blocks = (nvec + per_block - 1) / per_block;
-  hipLaunchKernelGGL((reduce_lds_kernel<Tr, K, U, AUX>), dim3((unsigned)(blocks ? blocks : 1)), dim3(256), 0, s, a,
-                     dst, nvec, head, tail);
-  return hipGetLastError();
+  if constexpr (W * U * K > 160) {
+    return hipErrorInvalidValue;
+  } else {
+    Srcs<K> a{};
+    for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
+    const size_t per_block = (size_t)W * U * 64;
+    const size_t blocks = (nvec + per_block - 1) / per_block;
+    hipLaunchKernelGGL((reduce_lds_kernel<Tr, K, U, W, AUX, PROG>), dim3((unsigned)(blocks ? blocks : 1)),
+                       dim3(W * 64), 0, s, a, dst, nvec, head, tail);
+    return hipGetLastError();
+  }
 }
 
 // element-wise fallback for sources not co-aligned with dst
 template <class Tr>
 __global__ void __launch_bounds__(kThreads)
-    reduce_elem_kernel(Srcs<FTAR_MAX_K> src, int k, void* __restrict__ dst, size_t n) {
+    reduce_elem_kernel(Srcs<FTAR_MAX_K> src, int k, void* dst, size_t n) {
   using S = typename Tr::S;
   const size_t stride = (size_t)gridDim.x * kThreads;
   for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < n; e += stride) {
@@ -474,7 +507,7 @@ __device__ __forceinline__ typename Tr::S tree_elem(const void* const* p, int k,
 
 template <class Tr, int K, int U, class Sh = RuntimeShape>
 __global__ void __launch_bounds__(kThreads)
-    reduce_tree_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, TreeCode tc, void* __restrict__ dst, size_t nvec,
+    reduce_tree_kernel(Srcs<(K > 0 ? K : FTAR_MAX_K)> src, int kr, TreeCode tc, void* dst, size_t nvec,
                        int head, int tail) {
   using S = typename Tr::S;
   using O = TreeOps<Tr, true>;
@@ -529,7 +562,7 @@ __global__ void __launch_bounds__(kThreads)
 
 template <class Tr>
 __global__ void __launch_bounds__(kThreads)
-    reduce_tree_elem_kernel(Srcs<FTAR_MAX_K> src, int k, TreeCode tc, void* __restrict__ dst, size_t n) {
+    reduce_tree_elem_kernel(Srcs<FTAR_MAX_K> src, int k, TreeCode tc, void* dst, size_t n) {
   using S = typename Tr::S;
   const size_t stride = (size_t)gridDim.x * kThreads;
   for (size_t e = (size_t)blockIdx.x * kThreads + threadIdx.x; e < n; e += stride)
@@ -605,7 +638,7 @@ hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, in
 template <class Tr, int K>
 hipError_t launch_k(const void* const* srcs, int k, void* dst, size_t nvec, int head, int tail, hipStream_t s) {
   if constexpr (K >= 2)
-    return launch_lds<Tr, K, kLdsTiles<Tr, K>, 2>(srcs, dst, nvec, s, head, tail);
+    return launch_lds<Tr, K, kLdsTiles<Tr, K>, kLdsWaves<Tr, K>>(srcs, dst, nvec, s, head, tail);
   else
     return launch_cfg<Tr, K, kUnroll, kNtLoads, kNtStores, kVecThreads>(srcs, k, dst, nvec, head, tail, s, 0);
 }
@@ -730,6 +763,27 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
 // stores, workgroup size, grid cap) for fp32 and bf16 sums, k in {2, 4, 8}.
 // ---------------------------------------------------------------------------
 namespace {
+// progressive LDS-staged kernel: (tiles per wave U, waves per workgroup W)
+template <class Tr, int K>
+hipError_t variant_prog(int v, const void* const* srcs, void* dst, size_t nvec, hipStream_t s) {
+  switch (v) {
+    case 40: return launch_lds<Tr, K, 4, 4>(srcs, dst, nvec, s);
+    case 41: return launch_lds<Tr, K, 3, 4>(srcs, dst, nvec, s);
+    case 42: return launch_lds<Tr, K, 2, 4>(srcs, dst, nvec, s);
+    case 43: return launch_lds<Tr, K, 4, 2>(srcs, dst, nvec, s);
+    case 44: return launch_lds<Tr, K, 3, 6>(srcs, dst, nvec, s);
+    case 45: return launch_lds<Tr, K, 2, 6>(srcs, dst, nvec, s);
+    case 46: return launch_lds<Tr, K, 2, 8>(srcs, dst, nvec, s);
+    case 47: return launch_lds<Tr, K, 1, 8>(srcs, dst, nvec, s);
+    case 48: return launch_lds<Tr, K, 3, 2>(srcs, dst, nvec, s);
+    case 49: return launch_lds<Tr, K, 6, 2>(srcs, dst, nvec, s);
+    case 50: return launch_lds<Tr, K, 2, 2>(srcs, dst, nvec, s);
+    case 51: return launch_lds<Tr, K, 1, 4>(srcs, dst, nvec, s);
+    case 52: return launch_lds<Tr, K, 5, 2>(srcs, dst, nvec, s);
+    case 53: return launch_lds<Tr, K, 2, 5>(srcs, dst, nvec, s);
+  }
+  return hipErrorInvalidValue;
+}
 template <class Tr, int K>
 hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
   switch (v) {
@@ -757,18 +811,18 @@ hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nv
     case 24: return launch_cfg<Tr, K, 8, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 25: return launch_cfg<Tr, K, 2, true, true, 128>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 26: return launch_cfg<Tr, K, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 31: return launch_lds<Tr, K, (K <= 4 ? 4 : 2), 2>(srcs, dst, nvec, s);
-    case 32: return launch_lds<Tr, K, (K <= 4 ? 4 : (K <= 6 ? 3 : 2)), 2>(srcs, dst, nvec, s);
-    case 33: return launch_lds<Tr, K, 1, 2>(srcs, dst, nvec, s);
+    case 31: return launch_lds<Tr, K, (K <= 4 ? 4 : 2), 4, 2, false>(srcs, dst, nvec, s);
+    case 32: return launch_lds<Tr, K, (K <= 4 ? 4 : (K <= 6 ? 3 : 2)), 4, 2, false>(srcs, dst, nvec, s);
+    case 33: return launch_lds<Tr, K, 1, 4, 2, false>(srcs, dst, nvec, s);
     case 27: return launch_cfg<Tr, 0, 2, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);  // runtime-k loop
     case 28: return launch_cfg<Tr, 0, 4, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 29: return launch_cfg<Tr, 0, 1, true, true, 512>(srcs, k, dst, nvec, 0, 0, s, 0);
     case 30: return launch_cfg<Tr, 0, 2, true, true, 256>(srcs, k, dst, nvec, 0, 0, s, 0);
-    case 20: return launch_lds<Tr, K, 2, 2>(srcs, dst, nvec, s);  // LDS-DMA, nt
-    case 21: return launch_lds<Tr, K, 4, 2>(srcs, dst, nvec, s);
-    case 22: return launch_lds<Tr, K, 2, 0>(srcs, dst, nvec, s);  // LDS-DMA, default policy
+    case 20: return launch_lds<Tr, K, 2, 4, 2, false>(srcs, dst, nvec, s);  // LDS-DMA, nt, wait for all
+    case 21: return launch_lds<Tr, K, 4, 4, 2, false>(srcs, dst, nvec, s);
+    case 22: return launch_lds<Tr, K, 2, 4, 0, false>(srcs, dst, nvec, s);  // LDS-DMA, default policy
   }
-  return hipErrorInvalidValue;
+  return variant_prog<Tr, K>(v, srcs, dst, nvec, s);
 }
 template <class Tr>
 hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
@@ -776,8 +830,13 @@ hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t n
     case 2: return variant_k<Tr, 2>(v, srcs, k, dst, nvec, s);
     case 3: return variant_k<Tr, 3>(v, srcs, k, dst, nvec, s);
     case 4: return variant_k<Tr, 4>(v, srcs, k, dst, nvec, s);
+    case 5: return variant_prog<Tr, 5>(v, srcs, dst, nvec, s);
     case 6: return variant_k<Tr, 6>(v, srcs, k, dst, nvec, s);
+    case 7: return variant_prog<Tr, 7>(v, srcs, dst, nvec, s);
     case 8: return variant_k<Tr, 8>(v, srcs, k, dst, nvec, s);
+    case 10: return variant_prog<Tr, 10>(v, srcs, dst, nvec, s);
+    case 12: return variant_prog<Tr, 12>(v, srcs, dst, nvec, s);
+    case 16: return variant_prog<Tr, 16>(v, srcs, dst, nvec, s);
   }
   return hipErrorInvalidValue;
 }

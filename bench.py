@@ -208,7 +208,8 @@ def bench_single(a):
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / 6
         bw = (kk + 1) * n * esz / (t * 1e-3) / 1e9
-        sweep[kk] = {"ms": round(t, 4), "GBps": round(bw, 1), "frac": round(bw / HBM_PEAK_GBPS, 4)}
+        sweep[kk] = {"ms": round(t, 4), "GBps": round(bw, 1), "frac": round(bw / HBM_PEAK_GBPS, 4),
+                     "traffic": pmc_traffic(f"reduce_k{kk}_{a.dtype}_n{n}")}
         del sw, sd
     res["k_sweep" if a.sweep else "k8"] = sweep if a.sweep else sweep[8]
     if not a.no_cpu_baseline:
