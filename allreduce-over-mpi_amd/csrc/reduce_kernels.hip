@@ -335,18 +335,20 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <class Tr, int K, int U, int W, int AUX, bool PROG>
-__global__ void __launch_bounds__(W * 64)
-    reduce_lds_kernel(Srcs<K> src, void* dst, size_t nvec, int head, int tail) {
+// The staging and tile loop shared by the flat and the nested fold: `fold(get)`
+// combines the K values get(0..K-1) of one 16-B vector slot (get(j) = source
+// j's vector, from LDS or, on the partial tile, from memory), `elem(e)` folds
+// element e alone (unaligned head / short tail, workgroup 0).
+template <class Tr, int K, int U, int W, int AUX, bool PROG, class Fold, class Elem>
+__device__ __forceinline__ void lds_staged(const Srcs<K>& src, void* dst, size_t nvec, int head, int tail, Fold fold,
+                                           Elem elem) {
   static_assert(W * U * K <= 160, "LDS per workgroup = W x U x K KiB <= 160 KiB");
   using S = typename Tr::S;
   constexpr int VE = 16 / sizeof(S);
   __shared__ u32x4 lds[W][U][K][64];
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)(head + tail)) {  // unaligned head / short tail
     const size_t e = threadIdx.x < (unsigned)head ? threadIdx.x : (size_t)head + nvec * VE + (threadIdx.x - head);
-    typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
-    for (int j = 1; j < K; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
-    static_cast<S*>(dst)[e] = Tr::s_fin(a);
+    static_cast<S*>(dst)[e] = elem(e);
   }
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const size_t base = ((size_t)blockIdx.x * W + wave) * (U * 64);
@@ -366,10 +368,7 @@ __global__ void __launch_bounds__(W * 64)
       constexpr int u = decltype(uc)::value;
       // the K loads of tile u have landed (a count above 63 waits for more: still exact)
       if constexpr (PROG) wait_vmcnt<((U - 1 - u) * K > 63 ? 63 : (U - 1 - u) * K)>();
-      typename Tr::VA a = Tr::v_init(lds[wave][u][0][lane]);
-#pragma unroll
-      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, lds[wave][u][j][lane]);
-      st16<kNtStores>(d + base + u * 64 + lane, Tr::v_fin(a));
+      st16<kNtStores>(d + base + u * 64 + lane, fold([&](int j) { return lds[wave][u][j][lane]; }));
     };
     [&]<int... I>(std::integer_sequence<int, I...>) { (tile(std::integral_constant<int, I>{}), ...); }
     (std::make_integer_sequence<int, U>{});
@@ -377,11 +376,28 @@ __global__ void __launch_bounds__(W * 64)
     for (int u = 0; u < U; ++u) {
       const size_t v = base + u * 64 + lane;
       if (v >= nvec) break;
-      typename Tr::VA a = Tr::v_init(ld16<kNtLoads>(sp(0) + v));
-      for (int j = 1; j < K; ++j) a = Tr::v_comb(a, ld16<kNtLoads>(sp(j) + v));
-      st16<kNtStores>(d + v, Tr::v_fin(a));
+      st16<kNtStores>(d + v, fold([&](int j) { return ld16<kNtLoads>(sp(j) + v); }));
     }
   }
+}
+
+template <class Tr, int K, int U, int W, int AUX, bool PROG>
+__global__ void __launch_bounds__(W * 64)
+    reduce_lds_kernel(Srcs<K> src, void* dst, size_t nvec, int head, int tail) {
+  using S = typename Tr::S;
+  lds_staged<Tr, K, U, W, AUX, PROG>(
+      src, dst, nvec, head, tail,
+      [](auto get) {
+        typename Tr::VA a = Tr::v_init(get(0));
+#pragma unroll
+        for (int j = 1; j < K; ++j) a = Tr::v_comb(a, get(j));
+        return Tr::v_fin(a);
+      },
+      [&](size_t e) {
+        typename Tr::SA a = Tr::s_init(static_cast<const S*>(src.p[0])[e]);
+        for (int j = 1; j < K; ++j) a = Tr::s_comb(a, static_cast<const S*>(src.p[j])[e]);
+        return Tr::s_fin(a);
+      });
 }
 
 template <class Tr, int K, int U, int W = 4, int AUX = 2, bool PROG = true>
@@ -569,6 +585,29 @@ __global__ void __launch_bounds__(kThreads)
     static_cast<S*>(dst)[e] = tree_elem<Tr>(src.p, k, tc, e);
 }
 
+// The nested fold on the LDS-staged tile loop (lds_staged): the production
+// path for the multi-stage trees' one-round reduce-scatter up to 16 ranks.
+// Compile-time shapes (Sh = StaticShape) fold to straight-line adds; other
+// shapes read the leaf codes from the kernarg.
+template <class Tr, int K, int U, int W, class Sh>
+__global__ void __launch_bounds__(W * 64)
+    reduce_tree_lds_kernel(Srcs<K> src, TreeCode tc, void* dst, size_t nvec, int head, int tail) {
+  using O = TreeOps<Tr, true>;
+  lds_staged<Tr, K, U, W, 2, true>(
+      src, dst, nvec, head, tail,
+      [&](auto get) {
+        typename O::A acc[kTreeLevels][1], v[1];
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          v[0] = Tr::v_init(get(j));
+          if constexpr (std::is_same_v<Sh, RuntimeShape>) tree_push<O, 1>(acc, v, tc.c[j]);
+          else tree_push<O, 1>(acc, v, Sh::code(j));
+        }
+        return Tr::v_fin(v[0]);
+      },
+      [&](size_t e) { return tree_elem<Tr>(src.p, K, tc, e); });
+}
+
 // ---------------------------------------------------------------------------
 // multi-segment copy: the peer-direct all-gather pulls every rank's final block
 // (over xGMI) into the caller's buffer in ONE launch.  Workgroup w copies
@@ -671,9 +710,22 @@ hipError_t launch_tree_k(const void* const* srcs, int k, const TreeCode& tc, voi
   return hipGetLastError();
 }
 
+template <class Tr, int K, class Sh = RuntimeShape>
+hipError_t launch_tree_lds(const void* const* srcs, const TreeCode& tc, void* dst, size_t nvec, int head, int tail,
+                           hipStream_t s) {
+  constexpr int U = kLdsTiles<Tr, K>, W = kLdsWaves<Tr, K>;
+  Srcs<K> a{};
+  for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
+  const size_t per_block = (size_t)W * U * 64;
+  const size_t blocks = (nvec + per_block - 1) / per_block;
+  hipLaunchKernelGGL((reduce_tree_lds_kernel<Tr, K, U, W, Sh>), dim3((unsigned)(blocks ? blocks : 1)), dim3(W * 64),
+                     0, s, a, tc, dst, nvec, head, tail);
+  return hipGetLastError();
+}
+
 template <class Tr>
 hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const int* shape, int nlevels, void* dst,
-                       size_t count, hipStream_t s) {
+                       size_t count, hipStream_t s, bool lds) {
   using S = typename Tr::S;
   constexpr size_t VE = 16 / sizeof(S);
   const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
@@ -692,23 +744,49 @@ hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const
   if (head > count) head = count;
   const size_t nvec = (count - head) / VE;
   const int tail = (int)(count - head - nvec * VE);
+  const int h = (int)head;
   auto is = [&](std::initializer_list<int> w) {
     return (int)w.size() == nlevels && std::equal(w.begin(), w.end(), shape);
   };
-  // the multi-stage trees of 4, 8 and 16 ranks: compile-time shapes
-  if (is({2, 2})) return launch_tree_k<Tr, 4, 2, StaticShape<2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-  if (is({2, 4})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 4>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-  if (is({4, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<4, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-  if (is({2, 2, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-  if (is({4, 4})) return launch_tree_k<Tr, 16, 1, StaticShape<4, 4>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-  if (is({2, 2, 2, 2}))
-    return launch_tree_k<Tr, 16, 1, StaticShape<2, 2, 2, 2>>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+  // the multi-stage trees of 4, 8 and 16 ranks: compile-time shapes.
+  // LDS-staged (production, round 2): cold A/B against the register kernel
+  // (profiles/r02/kbench_cold_nested_lds.log): fp32 +4 to +10 % on every
+  // shape; bf16 +4 to +8 % on the two-level shapes, but its per-level rounds
+  // make deeper and runtime-coded folds ALU-bound at the LDS kernel's
+  // occupancy (-2 to -25 %), so those keep the register kernel.
+  if (lds) {
+    if (is({2, 2})) return launch_tree_lds<Tr, 4, StaticShape<2, 2>>(srcs, tc, dst, nvec, h, tail, s);
+    if (is({2, 4})) return launch_tree_lds<Tr, 8, StaticShape<2, 4>>(srcs, tc, dst, nvec, h, tail, s);
+    if (is({4, 2})) return launch_tree_lds<Tr, 8, StaticShape<4, 2>>(srcs, tc, dst, nvec, h, tail, s);
+    if (is({4, 4})) return launch_tree_lds<Tr, 16, StaticShape<4, 4>>(srcs, tc, dst, nvec, h, tail, s);
+  }
+  if (lds && sizeof(S) >= 4) {
+    if (is({2, 2, 2})) return launch_tree_lds<Tr, 8, StaticShape<2, 2, 2>>(srcs, tc, dst, nvec, h, tail, s);
+    if (is({2, 2, 2, 2})) return launch_tree_lds<Tr, 16, StaticShape<2, 2, 2, 2>>(srcs, tc, dst, nvec, h, tail, s);
+    switch (k) {  // other shapes: runtime leaf codes
+      case 4: return launch_tree_lds<Tr, 4>(srcs, tc, dst, nvec, h, tail, s);
+      case 6: return launch_tree_lds<Tr, 6>(srcs, tc, dst, nvec, h, tail, s);
+      case 8: return launch_tree_lds<Tr, 8>(srcs, tc, dst, nvec, h, tail, s);
+      case 9: return launch_tree_lds<Tr, 9>(srcs, tc, dst, nvec, h, tail, s);
+      case 12: return launch_tree_lds<Tr, 12>(srcs, tc, dst, nvec, h, tail, s);
+      case 16: return launch_tree_lds<Tr, 16>(srcs, tc, dst, nvec, h, tail, s);
+      default: break;
+    }
+    return launch_tree_k<Tr, 0, 2>(srcs, k, tc, dst, nvec, h, tail, s);
+  }
+  // registers (round 1; the A/B reference of ftar_debug_reduce_nested_lds)
+  if (is({2, 2})) return launch_tree_k<Tr, 4, 2, StaticShape<2, 2>>(srcs, k, tc, dst, nvec, h, tail, s);
+  if (is({2, 4})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 4>>(srcs, k, tc, dst, nvec, h, tail, s);
+  if (is({4, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<4, 2>>(srcs, k, tc, dst, nvec, h, tail, s);
+  if (is({2, 2, 2})) return launch_tree_k<Tr, 8, 2, StaticShape<2, 2, 2>>(srcs, k, tc, dst, nvec, h, tail, s);
+  if (is({4, 4})) return launch_tree_k<Tr, 16, 1, StaticShape<4, 4>>(srcs, k, tc, dst, nvec, h, tail, s);
+  if (is({2, 2, 2, 2})) return launch_tree_k<Tr, 16, 1, StaticShape<2, 2, 2, 2>>(srcs, k, tc, dst, nvec, h, tail, s);
   switch (k) {  // other shapes: runtime leaf codes; 16 sources fit one vector per lane
-    case 4: return launch_tree_k<Tr, 4, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-    case 6: return launch_tree_k<Tr, 6, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-    case 8: return launch_tree_k<Tr, 8, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-    case 16: return launch_tree_k<Tr, 16, 1>(srcs, k, tc, dst, nvec, (int)head, tail, s);
-    default: return launch_tree_k<Tr, 0, 2>(srcs, k, tc, dst, nvec, (int)head, tail, s);
+    case 4: return launch_tree_k<Tr, 4, 2>(srcs, k, tc, dst, nvec, h, tail, s);
+    case 6: return launch_tree_k<Tr, 6, 2>(srcs, k, tc, dst, nvec, h, tail, s);
+    case 8: return launch_tree_k<Tr, 8, 2>(srcs, k, tc, dst, nvec, h, tail, s);
+    case 16: return launch_tree_k<Tr, 16, 1>(srcs, k, tc, dst, nvec, h, tail, s);
+    default: return launch_tree_k<Tr, 0, 2>(srcs, k, tc, dst, nvec, h, tail, s);
   }
 }
 
@@ -903,9 +981,9 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
     TreeCode tc;
     if (!shape || !make_tree_code(shape, nlevels, k, &tc)) return FTAR_ERR_INVALID_ARG;
     switch (dt) {
-      case FTAR_FLOAT32: e = launch_tree<F32Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
-      case FTAR_FLOAT64: e = launch_tree<F64Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
-      default: e = launch_tree<BF16Sum>(srcs, k, tc, shape, nlevels, dst, count, s); break;
+      case FTAR_FLOAT32: e = launch_tree<F32Sum>(srcs, k, tc, shape, nlevels, dst, count, s, lds); break;
+      case FTAR_FLOAT64: e = launch_tree<F64Sum>(srcs, k, tc, shape, nlevels, dst, count, s, false); break;
+      default: e = launch_tree<BF16Sum>(srcs, k, tc, shape, nlevels, dst, count, s, lds); break;
     }
     FTAR_CHECK_HIP(e);
     return FTAR_SUCCESS;
@@ -938,6 +1016,14 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
 }
 
 }  // namespace ftar
+
+// A/B of the nested fold: lds = 1 the LDS-staged kernel (production), 0 the
+// register kernel of round 1 (tools/kbench_cold.py --shapes).
+extern "C" ftar_status_t ftar_debug_reduce_nested_lds(int lds, const void* const* srcs, int k, void* dst, size_t count,
+                                                      int dtype, const int* shape, int nlevels, void* stream) {
+  return ftar::launch_reduce(srcs, k, dst, count, (ftar_dtype_t)dtype, FTAR_SUM, static_cast<hipStream_t>(stream),
+                             false, shape, nlevels, lds != 0);
+}
 
 extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, int dtype, const void* const* srcs, int k, void* dst,
                                                    size_t count, void* stream) {

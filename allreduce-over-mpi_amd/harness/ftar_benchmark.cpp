@@ -11,6 +11,8 @@
 // every call; prints "CHECK <rank>: data[9..23]" per rank and
 // "DONE, average time: <avg>, min time: <min>" (:125-240).
 // Extras: --device (time the device-resident entry, buffers already in HBM),
+// --dump PREFIX (every rank writes its final buffer to PREFIX.<rank>.bin, raw
+// fp32: the parity tests compare it with the reference's own output),
 // --warmup W (untimed calls first; the reference's first call pays one-time
 // setup), and one JSON summary line on rank 0.
 // --check is two-sided here: the reference only flags results that are too
@@ -45,7 +47,7 @@ int main(int argc, char** argv) {
   size_t data_len = 35;
   int repeat = 1, warmup = 0;
   bool to_file = false, check = false, device = false;
-  std::string tag, comm_type = "flextree";
+  std::string tag, comm_type = "flextree", dump;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -60,6 +62,7 @@ int main(int argc, char** argv) {
     else if (a == "--tag") tag = next();
     else if (a == "--check") check = true;
     else if (a == "--device") device = true;
+    else if (a == "--dump") dump = next();
     else if (a == "--version") {
       if (rank == 0) printf("ftar_benchmark: %s\n", ftar_version());
       MPI_Finalize();
@@ -127,6 +130,13 @@ int main(int argc, char** argv) {
   }
   if (device && hipMemcpy(data.data(), dptr, data_len * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
     die(rank, "hipMemcpy failed");
+
+  if (!dump.empty()) {
+    const std::string path = dump + "." + std::to_string(rank) + ".bin";
+    std::ofstream f(path, std::ios::binary);
+    f.write(reinterpret_cast<const char*>(data.data()), (std::streamsize)(data_len * sizeof(float)));
+    if (!f) die(rank, "cannot write " + path);
+  }
 
   // validity: expected i * 0.1 * P^repeat (benchmark.cpp:195-210), two-sided
   size_t bad = 0, first_bad = 0;

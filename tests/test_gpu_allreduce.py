@@ -61,6 +61,21 @@ def test_allreduce_matches_reference_golden(case, ag):
         gc.check_output(case, r, outs[r])
 
 
+_LINEAR = gc.allreduce_cases(filt=lambda c: c.get("init") == "linear")
+
+
+@pytest.mark.parametrize("ag", ["direct", "stages"])
+@pytest.mark.parametrize("case", [c for c in _LINEAR if c["n"] > 70000], ids=lambda c: c["id"])
+def test_allreduce_reference_benchmark_workload(case, ag):
+    """benchmark.cpp's own workload at BASELINE configs[0]'s size (C1: 2 ranks, ring, 2^20 fp32,
+    data[i] = i*0.1f): the reference's per-rank output bits (the golden filter above stops at 70,000)."""
+    ins = gc.case_inputs(case)
+    outs = run_group(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                     repeat=case["repeat"], ag=ag)
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
 @pytest.mark.parametrize("P,topo,lonely", [(2, "1", 0), (4, "1", 0), (8, "1", 0), (4, "2,2", 0), (8, "8", 0),
                                            (8, "2,2,2", 0), (8, "4,2", 0), (5, "2,2", 1), (8, "3,2", 2)])
 @pytest.mark.parametrize("chunk_bytes", [256, 4096])
@@ -234,6 +249,17 @@ def run_group_host(ins, topo, lonely=0, dtype=6, op=0, outofplace=False, host_ch
                          ids=lambda c: c["id"])
 def test_host_allreduce_matches_reference_golden(case):
     """MPI_Allreduce_FT's own setting (host buffers): every golden case, bit-exact per rank."""
+    ins = gc.case_inputs(case)
+    outs = run_group_host(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
+                          repeat=case["repeat"])
+    for r in range(case["P"]):
+        gc.check_output(case, r, outs[r])
+
+
+@pytest.mark.parametrize("case", _LINEAR, ids=lambda c: c["id"])
+def test_host_allreduce_reference_benchmark_workload(case):
+    """The same two benchmark.cpp workloads (C1 at 2^20, and 8 ranks tree(8)) through ftar_allreduce_host,
+    MPI_Allreduce_FT's own path: host buffers in, host buffers out, the reference's bits per rank."""
     ins = gc.case_inputs(case)
     outs = run_group_host(ins, case["topo"], case["lonely"], case["dtype"], case["op"], case["outofplace"],
                           repeat=case["repeat"])

@@ -74,6 +74,29 @@ def test_harness_ranks_sharing_a_gpu_fall_back_to_ipc(tmp_path, ranks, topo, ext
 
 @needs
 @pytest.mark.gpu
+@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
+@pytest.mark.parametrize("case_id", ["ar_P2_t1_l0_f32_op0_n1048576_lin", "ar_P8_t8_l0_f32_op0_n65536_lin"])
+def test_harness_reproduces_reference_benchmark_output(tmp_path, case_id, device):
+    """The reference's own benchmark.cpp workload (data[i] = i*0.1f in place, one call; C1 = 2 ranks, ring,
+    2^20 fp32) through MPI_Allreduce_FT (host buffers) or MPI_Allreduce_FT_device in ftar_benchmark, one MPI
+    process per rank on the box's GPU: every rank's final buffer must have the sha256 the unmodified
+    reference produced (tests/golden/manifest.json, oracle/gen_golden.py)."""
+    import hashlib
+
+    import golden_cases as gc
+    case = next(c for c in gc.manifest()["cases"] if c["id"] == case_id)
+    args = ["--size", str(case["n"]), "--repeat", "1", "--check", "--dump", "out"] + (["--device"] if device else [])
+    rc, out = run(case["P"], args, tmp_path, {"FT_TOPO": case["topo"]})
+    assert rc == 0, out
+    for r in range(case["P"]):
+        with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
+            data = f.read()
+        assert len(data) == case["n"] * 4
+        assert hashlib.sha256(data).hexdigest() == case["sha256"][r], f"{case_id} rank {r}"
+
+
+@needs
+@pytest.mark.gpu
 def test_harness_rccl_only_fails_cleanly_on_a_shared_gpu(tmp_path):
     rc, out = run(2, ["--size", "4096", "--repeat", "1"], tmp_path, {"FT_TOPO": "2", "FTAR_MPI_TRANSPORT": "rccl"})
     assert rc != 0, out

@@ -29,11 +29,20 @@ ap.add_argument("--variants", default="0,1,2,4,12,13,14,15,16,17,18")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=12)
 ap.add_argument("--dtypes", default="f32")
+ap.add_argument("--shapes", default="", help='nested folds instead of flat variants, e.g. "2,4;4,2;2,2,2": variant 1 '
+                                             '= LDS-staged (production), 0 = register kernel (round 1)')
 a = ap.parse_args()
 lib = ftar.lib()
 lib.ftar_debug_reduce_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+lib.ftar_debug_reduce_nested_lds.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p]
 n = a.elements
+shapes = [[int(w) for w in sh.split(",")] for sh in a.shapes.split(";")] if a.shapes else []
+if shapes:
+    a.ks = ",".join(str(__import__("math").prod(sh)) for sh in shapes)
+    a.variants = "0,1"
 ks = [int(k) for k in a.ks.split(",")]
 setss = [int(x) for x in a.sets.split(",")]
 variants = [int(v) for v in a.variants.split(",")]
@@ -47,10 +56,15 @@ for r in range(a.rounds):
     for d in a.dtypes.split(","):
         m = n * 4 // ESZ[d]   # the same bytes per buffer
         for sets in setss:
-            for k in ks:
+            for si, k in enumerate(ks):
                 arrs = [(ctypes.c_void_p * k)(*[t.data_ptr() for t in bufs[i][:k]]) for i in range(sets)]
+                sh = shapes[si] if shapes else None
+                sh_c = (ctypes.c_int * len(sh))(*sh) if sh else None
                 for v in variants:
                     def launch(i):
+                        if sh:
+                            return lib.ftar_debug_reduce_nested_lds(v, arrs[i % sets], k, bufs[i % sets][K].data_ptr(),
+                                                                    m, ftar.DTYPE[d], sh_c, len(sh), stream.cuda_stream)
                         return lib.ftar_debug_reduce_variant(v, ftar.DTYPE[d], arrs[i % sets], k,
                                                              bufs[i % sets][K].data_ptr(), m, stream.cuda_stream)
                     if launch(0) != 0:  # variant not built for this k (or its LDS would exceed 160 KiB)
@@ -63,9 +77,11 @@ for r in range(a.rounds):
                         launch(i)
                     e1.record(stream)
                     torch.cuda.synchronize()
-                    res.setdefault((d, sets, k, v), []).append(e0.elapsed_time(e1) / a.reps)
-for (d, sets, k, v), ts in sorted(res.items()):
+                    key = (d, sets, ",".join(map(str, sh)) if sh else k, v)
+                    res.setdefault(key, []).append(e0.elapsed_time(e1) / a.reps)
+for (d, sets, k, v), ts in sorted(res.items(), key=lambda kv: str(kv[0])):
     med = statistics.median(ts)
-    byts = (k + 1) * n * 4
+    kk = __import__("math").prod(int(w) for w in str(k).split(","))
+    byts = (kk + 1) * n * 4
     print(json.dumps({"dtype": d, "sets": sets, "k": k, "variant": v, "bytes_per_buffer": n * 4, "ms_med": round(med, 4),
                       "GBps_med": round(byts / med / 1e6, 1), "GBps_max": round(byts / min(ts) / 1e6, 1)}), flush=True)
