@@ -227,6 +227,63 @@ def sample_index(n, dev, m=4096):
     return idx
 
 
+def link_rate_from_probe(probe, world):
+    """Per-link, per-direction GB/s measured by ftar_xgmi_probe (every rank copying at once, so each link
+    carries one direction per mode): the best of read/write from one peer and of read/write from all
+    peers divided by the P-1 links they spread over.  None when the probe did not run or measured nothing."""
+    if not probe or world < 2:
+        return None
+    rates = []
+    for key, per in (("read_one_peer", 1), ("write_one_peer", 1), ("read_all_peers", world - 1),
+                     ("write_all_peers", world - 1), ("dma_read_all_peers", world - 1),
+                     ("dma_write_all_peers", world - 1)):
+        v = probe.get(key)
+        if isinstance(v, (list, tuple)):   # bench line form: [min, max] over ranks -> the slowest rank
+            v = v[0]
+        if isinstance(v, (int, float)) and v > 0:
+            rates.append(v / per)
+    return max(rates) if rates else None
+
+
+def allreduce_roofline(world, gpus, bucket, ms, links, probe_link_gbps=None):
+    """Roofline object of one N>1 AllReduce line (ms per call, bucket bytes per rank).
+
+    - P = 1: nothing crosses a link; the call is one pass over the bucket (read + write), so the bound is
+      HBM and achieved = 2 * bucket / t.
+    - ranks sharing GPUs (the --host-comm rehearsal): neither an xGMI nor a per-GPU HBM figure; None.
+    - P > 1: busBW = algBW * 2(P-1)/P (bytes each rank sends, and receives, per second) against
+      links x per-link rate in ONE direction: the probe's measured rate when it ran, else the spec
+      76.8 GB/s (153.6 GB/s bidirectional).  A probe rate the run beats falls back to the spec.
+    Never returns a frac outside (0, 1]: a denominator the work exceeds does not describe it, and the
+    object then carries frac None and says why."""
+    if ms <= 0 or bucket <= 0:
+        return None
+    algbw = bucket / (ms * 1e-3) / 1e9
+    if world == 1:
+        ach = 2 * algbw
+        return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "note": "P=1: the AllReduce is one local pass over the bucket (read + write), no link crossed"}
+    if world > gpus:
+        return None
+    busbw = algbw * 2 * (world - 1) / world
+    links = max(1, min(XGMI_LINKS, links))
+    cands = []
+    if probe_link_gbps:
+        cands.append((probe_link_gbps, "measured by ftar_xgmi_probe (this run)"))
+    cands.append((XGMI_LINK_GBPS, "spec, 153.6 GB/s bidirectional"))
+    for rate, src in cands:
+        peak = links * rate
+        if 0 < busbw / peak <= 1:
+            return {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 2), "unit": "GB/s",
+                    "frac": round(busbw / peak, 4), "traffic": None,
+                    "note": f"busBW vs {links} xGMI link(s) x {rate:.1f} GB/s per direction ({src})"}
+    return {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(links * XGMI_LINK_GBPS, 2),
+            "unit": "GB/s", "frac": None, "traffic": None,
+            "note": f"busBW exceeds {links} link(s) x {XGMI_LINK_GBPS} GB/s per direction: the link count "
+                    "does not describe this run's data movement; no fraction reported"}
+
+
 def _factorizations(n):
     out = []
 
@@ -519,8 +576,9 @@ def bench_distributed(a):
             links = 1
         else:
             links = min(XGMI_LINKS, max(topo_.widths) - 1)
-        links = max(1, links)
-        peak = links * XGMI_LINK_GBPS
+        probe = state.get("line", {}).get("xgmi_probe_GBps") if isinstance(state.get("line"), dict) else None
+        roof = allreduce_roofline(world, torch.cuda.device_count(), bucket, ms, links,
+                                  link_rate_from_probe(probe, world))
         res = {
             "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
             "value": round(world * algbw, 2), "unit": "GB/s", "n_gpus": world, "steps": steps,
@@ -530,14 +588,14 @@ def bench_distributed(a):
                                    f"{'IPC-mapped ' + form if form.startswith('peer-') else 'RCCL p2p'} "
                                    "(BASELINE configs[2-3])",
                        "bucket_bytes": bucket, "elements_per_rank": n, "topology": str(topo_),
-                       "chunk_bytes": chunk, "form": form, "parallelism": f"dp{world}"
+                       "chunk_bytes": chunk, "form": form, "xgmi_links": links, "parallelism": f"dp{world}"
                        + (f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), host-bootstrapped "
                           "communicator; not an xGMI measurement)" if a.host_comm and world > torch.cuda.device_count()
                           else " (host-bootstrapped communicator: RCCL failed to initialise)" if a.host_comm else "")},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
-            "roofline": {"bound": "xgmi", "achieved": round(busbw, 2), "peak": peak, "unit": "GB/s",
-                         "frac": round(busbw / peak, 4), "traffic": None,
-                         "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s unidirectional"},
+            "roofline": roof,
+            "value_convention": "value = N x bucket bytes / t (aggregate algBW); algbw = bucket / t per rank; "
+                                "busbw = algbw x 2(P-1)/P",
             "check": "ok" if ok else "MISMATCH",
         }
         if rccl_error:
@@ -655,6 +713,11 @@ def bench_distributed(a):
             state["line"]["config_selection"] = "default (sweep best not faster when re-timed)"
     else:
         state["line"]["config_selection"] = "default (fastest validated configuration)"
+    # the roofline again, now against the probe's per-link rate if the sweep reached the probe
+    hl = state["line"]
+    hl["roofline"] = allreduce_roofline(world, torch.cuda.device_count(), bucket, hl["ms_per_step"],
+                                        hl["config"]["xgmi_links"],
+                                        link_rate_from_probe(hl.get("xgmi_probe_GBps"), world))
 
     # phase timelines (rank 0's view) of the default and of the fastest validated configuration of each form:
     # where a call's time goes (transfer rounds vs folds vs barriers), for the next round's tuning

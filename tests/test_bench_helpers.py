@@ -22,3 +22,53 @@ def test_factorizations():
     import bench
     assert bench._factorizations(8) == [[2, 2, 2], [2, 4], [4, 2], [8]]
     assert bench._factorizations(1) == []
+
+
+def test_roofline_world_size_one_is_hbm():
+    """P = 1 crosses no link: the line's roofline is the local pass over the bucket (read + write) against
+    HBM, never an xGMI fraction (the round-1 world-size-1 rehearsal printed xgmi frac 38.29)."""
+    import bench
+    r = bench.allreduce_roofline(1, 1, 1 << 30, 0.35, 7)
+    assert r["bound"] == "hbm" and r["peak"] == bench.HBM_PEAK_GBPS
+    assert r["achieved"] == pytest.approx(2 * (1 << 30) / 0.35e-3 / 1e9, rel=1e-4)
+    assert 0 < r["frac"] <= 1
+
+
+def test_roofline_rehearsal_has_none():
+    import bench
+    assert bench.allreduce_roofline(4, 1, 1 << 28, 10.0, 3) is None
+
+
+@pytest.mark.parametrize("world,links", [(2, 1), (4, 3), (8, 7)])
+def test_roofline_xgmi_frac_in_range(world, links):
+    import bench
+    bucket = 1 << 30
+    for ms in (3.0, 10.0, 50.0, 100.0):
+        r = bench.allreduce_roofline(world, 8, bucket, ms, links)
+        alg = bucket / (ms * 1e-3) / 1e9
+        assert r["achieved"] == pytest.approx(alg * 2 * (world - 1) / world, rel=1e-3)
+        if r["frac"] is not None:
+            assert 0 < r["frac"] <= 1
+            assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], abs=1e-4)
+    # a run faster than the links allow: no fraction at all
+    r = bench.allreduce_roofline(world, 8, bucket, 0.01, links)
+    assert r["frac"] is None and "no fraction" in r["note"]
+
+
+def test_roofline_uses_probe_rate_and_falls_back_to_spec():
+    import bench
+    probe = {"read_one_peer": [60.0, 62.0], "read_all_peers": [400.0, 410.0], "write_one_peer": [50.0, 51.0],
+             "write_all_peers": [350.0, 360.0], "note": "x"}
+    rate = bench.link_rate_from_probe(probe, 8)
+    assert rate == pytest.approx(60.0)   # the slowest rank's best per-link mode: one peer beats 400/7
+    bucket = 1 << 30
+    ms = bucket * 2 * 7 / 8 / (7 * 50.0 * 1e9) * 1e3   # busBW 50 GB/s per link
+    r = bench.allreduce_roofline(8, 8, bucket, ms, 7, rate)
+    assert "ftar_xgmi_probe" in r["note"] and r["peak"] == pytest.approx(420.0, rel=1e-3)
+    assert r["frac"] == pytest.approx(50.0 / 60.0, abs=1e-4)
+    ms2 = bucket * 2 * 7 / 8 / (7 * 70.0 * 1e9) * 1e3  # beats the probe's rate: spec denominator
+    r2 = bench.allreduce_roofline(8, 8, bucket, ms2, 7, rate)
+    assert "spec" in r2["note"] and 0 < r2["frac"] <= 1
+    assert bench.link_rate_from_probe(None, 8) is None
+    assert bench.link_rate_from_probe({"error": "x"}, 8) is None
+    assert bench.link_rate_from_probe(probe, 1) is None
