@@ -63,14 +63,76 @@ namespace {
 // figures (DESIGN.md §Cost model); FTAR_COST_{ALPHA_US,LINK_GBPS,HBM_GBPS}
 // override them.
 // ---------------------------------------------------------------------------
+// Process-wide constants set by ftar_cost_set_params (e.g. fitted from
+// ftar_xgmi_probe by bench.py); 0 = unset.  The environment overrides both.
+std::mutex g_cost_mu;
+double g_alpha = 0, g_link = 0, g_hbm = 0;
+
 struct CostConsts {
   double alpha = 20e-6, link = 48e9, hbm = 6.3e12;  // hbm: measured k=2..8 reduce (profiles/r01/kbench3)
   CostConsts() {
+    {
+      std::lock_guard<std::mutex> g(g_cost_mu);
+      if (g_alpha > 0) alpha = g_alpha;
+      if (g_link > 0) link = g_link;
+      if (g_hbm > 0) hbm = g_hbm;
+    }
     if (const char* e = getenv("FTAR_COST_ALPHA_US")) alpha = atof(e) * 1e-6;
     if (const char* e = getenv("FTAR_COST_LINK_GBPS")) link = atof(e) * 1e9;
     if (const char* e = getenv("FTAR_COST_HBM_GBPS")) hbm = atof(e) * 1e9;
   }
 };
+
+// ---------------------------------------------------------------------------
+// The reference's cost model, restated (cost_model/CostModel.h:1-120), for
+// FTAR_COST_MODEL=reference and for parity (tests/golden/costmodel.jsonl, the
+// reference's own output).  Units are the reference's (undocumented; chunk =
+// its Chunk_size, 100 in cost_model/main.cpp:23).  Same operations in the same
+// order, so the doubles are the reference's bit for bit:
+//   latency_control_overhead(100, w)  (CostModel.h:1-20; the chunk passed is
+//                                      always 100, :92)
+//   memory_read_write_overhead        (:32-79; height 1..9 only)
+//   bandwidth_calculation_overhead    (:22-30)
+// The first candidate's sum starts from an uninitialised `cost` there (:89);
+// here from 0, which is what the reference's default (-O0) build prints.
+// ---------------------------------------------------------------------------
+double ref_latency(double chunk, double tw) {
+  const double lo = 0.004, co = 0.0002;
+  return tw > 9 ? 2 * lo + chunk * (tw - 9) * co : 2 * lo;
+}
+
+double ref_bandwidth(int total, double chunk) {
+  const double bo = 0.0068, n = total;
+  return (((n - 1) / n) * chunk) * bo;
+}
+
+// < 0: a height the reference has no case for (its switch falls off the end)
+double ref_memory(const std::vector<int>& tree, int total, double chunk) {
+  const int th = (int)tree.size();
+  if (th < 1 || th > 9) return -1.0;
+  const double o = 0.0004;
+  // steps = n + 2*t0*..*t{h-2} + ... + 2*t0 + 1 (the switch's cases 1..9)
+  int steps = total + 1, prod = 1;
+  for (int i = 0; i + 1 < th; ++i) {
+    prod *= tree[i];
+    steps += 2 * prod;
+  }
+  return ((steps * chunk) / total) * o;
+}
+
+double ref_cost(const std::vector<int>& tree, int total, double chunk) {
+  double mem = ref_memory(tree, total, chunk);
+  if (mem < 0) return -1.0;
+  double cost = 0;
+  for (int w : tree) cost += ref_latency(100, w);
+  cost += mem;
+  cost += ref_bandwidth(total, chunk);
+  return cost;
+}
+
+// getWidth(P) (GetWidth.h:10-47): ordered factorizations, smallest first
+// factor first, the single factor [P] listed as [1,P], [P,1]
+std::vector<std::vector<int>> ref_getwidth(int P);
 
 double model_cost(const Topology& t, int P, size_t bytes) {
   CostConsts k;
@@ -108,10 +170,100 @@ void factorizations(size_t n, std::vector<size_t>& cur, std::vector<std::vector<
     }
 }
 
+std::vector<std::vector<int>> ref_getwidth(int P) {
+  std::vector<size_t> cur;
+  std::vector<std::vector<size_t>> f;
+  factorizations((size_t)P, cur, f);
+  std::vector<std::vector<int>> out;
+  for (auto& c : f) {
+    if (c.size() == 1) {
+      out.push_back({1, P});
+      out.push_back({P, 1});
+    } else {
+      out.emplace_back(c.begin(), c.end());
+    }
+  }
+  return out;
+}
+
+// a getWidth list as a topology: any width 1 selects the ring (mpi_mod.hpp:1440-1468)
+void ref_list_topology(const std::vector<int>& w, ftar_topo_t* out) {
+  memset(out, 0, sizeof *out);
+  bool ring = false;
+  for (int x : w) ring = ring || x == 1;
+  if (ring) {
+    out->ring = 1;
+    out->nstages = 1;
+    out->stages[0] = 1;
+    return;
+  }
+  out->nstages = (int)std::min<size_t>(w.size(), FTAR_MAX_STAGES);
+  for (int i = 0; i < out->nstages; ++i) out->stages[i] = w[i];
+}
+
 }  // namespace
 }  // namespace ftar
 
 extern "C" {
+
+double ftar_cost_reference(const int* widths, int nwidths, int nranks, double chunk) {
+  if (!widths || nwidths <= 0 || nranks <= 0) return -1.0;
+  return ftar::ref_cost(std::vector<int>(widths, widths + nwidths), nranks, chunk);
+}
+
+ftar_status_t ftar_topo_choose_reference(int nranks, double chunk, ftar_topo_t* out, int* index) {
+  if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  if (nranks == 1) {  // getWidth(1) = one empty list the reference cannot score
+    ftar::ref_list_topology({1}, out);
+    if (index) *index = 0;
+    return FTAR_SUCCESS;
+  }
+  const auto cands = ftar::ref_getwidth(nranks);
+  double best = 1000000000;  // cost_output, CostModel.h:84
+  int at = -1;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    const double c = ftar::ref_cost(cands[i], nranks, chunk);
+    if (c < 0) continue;
+    if (c < best) {  // first minimum wins (:97)
+      best = c;
+      at = (int)i;
+    }
+  }
+  if (at < 0) return FTAR_ERR_UNSUPPORTED;
+  ftar::ref_list_topology(cands[at], out);
+  if (index) *index = at;
+  return FTAR_SUCCESS;
+}
+
+int ftar_cost_reference_candidates(int nranks, int* widths, int max_widths, int* lengths, int max_lists) {
+  if (nranks <= 1) return -FTAR_ERR_INVALID_ARG;
+  const auto cands = ftar::ref_getwidth(nranks);
+  int used = 0;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    if ((int)i < max_lists && lengths) lengths[i] = (int)cands[i].size();
+    for (int w : cands[i]) {
+      if (widths && used < max_widths) widths[used] = w;
+      ++used;
+    }
+  }
+  return (int)cands.size();
+}
+
+ftar_status_t ftar_cost_set_params(double alpha_us, double link_gbps, double hbm_gbps) {
+  std::lock_guard<std::mutex> g(ftar::g_cost_mu);
+  ftar::g_alpha = alpha_us > 0 ? alpha_us * 1e-6 : 0;
+  ftar::g_link = link_gbps > 0 ? link_gbps * 1e9 : 0;
+  ftar::g_hbm = hbm_gbps > 0 ? hbm_gbps * 1e9 : 0;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* hbm_gbps) {
+  ftar::CostConsts k;
+  if (alpha_us) *alpha_us = k.alpha * 1e6;
+  if (link_gbps) *link_gbps = k.link / 1e9;
+  if (hbm_gbps) *hbm_gbps = k.hbm / 1e9;
+  return FTAR_SUCCESS;
+}
 
 const char* ftar_version(void) {
   static char v[64];
@@ -129,6 +281,7 @@ const char* ftar_status_string(ftar_status_t s) {
     case FTAR_ERR_RCCL: return "RCCL error";
     case FTAR_ERR_INTERNAL: return "internal error";
     case FTAR_ERR_TIMEOUT: return "timeout";
+    case FTAR_ERR_NO_MEMORY: return "out of device memory";
   }
   return "unknown";
 }
@@ -202,6 +355,16 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
 
 ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
   if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
+  if (const char* m = getenv("FTAR_COST_MODEL")) {
+    if (!strcmp(m, "reference")) {  // the reference's own scores (CostModel.h), chunk = FTAR_COST_REF_CHUNK
+      const char* ch = getenv("FTAR_COST_REF_CHUNK");
+      return ftar_topo_choose_reference(nranks, ch ? atof(ch) : 100.0, out, nullptr);
+    }
+    if (*m && strcmp(m, "xgmi")) {
+      ftar::set_error(std::string("FTAR_COST_MODEL=") + m + ": expected xgmi or reference", __FILE__, __LINE__);
+      return FTAR_ERR_INVALID_ARG;
+    }
+  }
   ftar::Topology ring;
   ring.ring = true;
   ring.widths = {1};

@@ -75,6 +75,11 @@ struct ftar_comm {
   std::vector<hipEvent_t> tev;
   std::vector<std::string> tnames;
   size_t nmarks = 0;
+  // completion marker of the previous call, recorded on that call's stream after it joined every internal
+  // stream: a call on a different stream waits for it (scratch, staging and exchange buffers are shared)
+  hipEvent_t done_ev = nullptr;
+  hipStream_t done_stream = nullptr;
+  bool done_recorded = false;
   std::mutex mu;
 };
 
@@ -120,6 +125,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
   if (const char* pd = getenv("FTAR_PEER_DIRECT")) {
     const std::string m(pd);
     c->peer_direct = m == "write" ? FTAR_PEER_WRITE : m == "read" ? FTAR_PEER_READ
@@ -163,6 +169,7 @@ void comm_teardown(ftar_comm* c) {
   for (hipStream_t t : c->dma_s) hip_ignore(hipStreamDestroy(t));
   for (hipEvent_t e : c->dma_ev) hip_ignore(hipEventDestroy(e));
   if (c->dma_fork) hip_ignore(hipEventDestroy(c->dma_fork));
+  if (c->done_ev) hip_ignore(hipEventDestroy(c->done_ev));
   for (auto e : c->events) hip_ignore(hipEventDestroy(e));
   for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
   if (c->scratch) hip_ignore(hipFree(c->scratch));
@@ -550,7 +557,7 @@ ftar_status_t ensure_buffer(void** buf, size_t* have, size_t need, std::initiali
     *buf = nullptr;
     *have = 0;
   }
-  FTAR_CHECK_HIP(hipMalloc(buf, need));
+  FTAR_CHECK_ALLOC(hipMalloc(buf, need));
   *have = need;
   return FTAR_SUCCESS;
 }
@@ -620,13 +627,40 @@ std::vector<std::pair<size_t, size_t>> step_order(size_t nst, size_t nchunks, bo
 
 }  // namespace
 
+ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                               const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host);
+
+// One call on a communicator.  Calls share the communicator's scratch, staging
+// and exchange buffers; the internal streams join the caller's stream at entry,
+// so calls on ONE stream are ordered by it.  A call on another stream than the
+// previous call's first waits for that call's completion marker (recorded on
+// its stream after every internal stream joined it), so its transfers cannot
+// overwrite scratch the previous call's reduces are still reading.
 ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                         const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr) {
   if (!c || !recvbuf) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
-  const size_t esz = dtype_size(dt);
   std::lock_guard<std::mutex> g(c->mu);
   FTAR_CHECK_HIP(hipSetDevice(c->device));
+  // under capture the graph's own dependencies order its replays: an event recorded outside the capture
+  // is not waited on inside it, nor is the marker re-recorded by a captured call
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  FTAR_CHECK_HIP(hipStreamIsCapturing(stream, &cs));
+  const bool capturing = cs != hipStreamCaptureStatusNone;
+  if (!capturing && c->done_recorded && c->done_stream != stream)
+    FTAR_CHECK_HIP(hipStreamWaitEvent(stream, c->done_ev, 0));
+  const ftar_status_t st = allreduce_locked(sendbuf, recvbuf, count, dt, op, topo, c, stream, host);
+  if (st == FTAR_SUCCESS && !capturing) {
+    FTAR_CHECK_HIP(hipEventRecord(c->done_ev, stream));
+    c->done_stream = stream;
+    c->done_recorded = true;
+  }
+  return st;
+}
+
+ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                               const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host) {
+  const size_t esz = dtype_size(dt);
   if (sendbuf == recvbuf) sendbuf = nullptr;
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
     if (sendbuf && count && host)
@@ -664,6 +698,13 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
     FTAR_RETURN_IF(peer_allreduce(nullptr, c->staging, count, dt, op, plan, c, stream));
     FTAR_CHECK_HIP(hipMemcpyAsync(host->dst, c->staging, bytes, hipMemcpyDeviceToHost, stream));
     return FTAR_SUCCESS;
+  }
+
+  if (!c->tp->async_p2p()) {  // a transport without p2p (ftar_comm_init_host): refused before anything moves
+    set_error("this communicator has no point-to-point transfers: one-round plans in the peer-direct forms only "
+              "(ftar_comm_set_peer_direct; staged forms and lonely ranks need RCCL)",
+              __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
   }
 
   // Host mode: the buffers are in host memory and move through a device
@@ -741,7 +782,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   for (const auto& step : order) {
     const size_t s = step.first, k = step.second, lo = k * chunk;
     const Stage& st = plan.stages[s];
-    if (moves[s] || tp->collective_groups()) {  // (an idle rank still joins the host transport's step)
+    if (moves[s]) {
       if (host && !comm_has_input[k]) {
         FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k), 0));
         comm_has_input[k] = 1;

@@ -28,6 +28,18 @@ namespace ftar {
 
 // best-effort HIP call (cleanup paths): a failure is dropped, and so is the
 // sticky "last error" it would leave for the next launch check
+// Device allocation: hipErrorOutOfMemory becomes FTAR_ERR_NO_MEMORY (so the MPI
+// shim can answer MPI_ERR_NO_MEM), anything else FTAR_ERR_HIP.
+#define FTAR_CHECK_ALLOC(expr)                                                                 \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) {                                                                    \
+      ::ftar::set_error(std::string(#expr) + ": " + hipGetErrorString(_e), __FILE__, __LINE__); \
+      (void)hipGetLastError();                                                                 \
+      return _e == hipErrorOutOfMemory ? FTAR_ERR_NO_MEMORY : FTAR_ERR_HIP;                    \
+    }                                                                                          \
+  } while (0)
+
 inline void hip_ignore(hipError_t e) {
   if (e != hipSuccess) (void)hipGetLastError();
 }
@@ -169,11 +181,9 @@ class Transport {
   // map_peers exports and opens IPC handles (false: one address space)
   virtual bool uses_ipc() const { return false; }
   // send/recv are stream-ordered and need no peer participation beyond the
-  // matching operation (RCCL, local).  false: the host transport, whose
-  // send/recv complete inside group_end through host collectives, so every
-  // rank must call group_start/group_end for every step (collective_groups).
+  // matching operation (RCCL, local).  false: the host transport, which has
+  // no point-to-point transfers (peer-direct forms only).
   virtual bool async_p2p() const { return true; }
-  virtual bool collective_groups() const { return false; }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {
@@ -218,7 +228,7 @@ ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got);
 // Writes a fresh random token into the first 16 bytes at p (a buffer ftar
 // owns), so that its IPC reference can be verified by every importer: under
 // HIP 7.0 an import occasionally maps the wrong memory after buffers were
-// regrown (tools/p2p_rehearsal.py), silently.
+// regrown (round-1 multi-process rehearsals on one GPU), silently.
 ftar_status_t stamp_token(void* p);
 void forget_token(const void* p);  // before the stamped buffer is freed
 // opens ref and verifies the mapping (allocation size; the token when

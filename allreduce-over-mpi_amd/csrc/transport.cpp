@@ -67,9 +67,11 @@ ftar_status_t alloc_exportable(size_t bytes, bool ipc, void** out, size_t* got) 
   ftar_status_t st = FTAR_ERR_HIP;
   for (int attempt = 0; attempt < 4; ++attempt) {
     void* fresh = nullptr;
-    if (hipMalloc(&fresh, want) != hipSuccess) {
+    const hipError_t me = hipMalloc(&fresh, want);
+    if (me != hipSuccess) {
       (void)hipGetLastError();
       set_error("hipMalloc of " + std::to_string(want) + " bytes failed", __FILE__, __LINE__);
+      if (me == hipErrorOutOfMemory) st = FTAR_ERR_NO_MEMORY;
       break;
     }
     IpcRef probe;
@@ -193,9 +195,58 @@ namespace {
     }                                                                                               \
   } while (0)
 
+// Peer allocations imported into this process: one IPC mapping per allocation
+// (two registered buffers may share one), reference-counted by the pointers
+// handed out, so closing one pointer never unmaps memory another still uses.
+// Shared by the RCCL and the host-bootstrapped transports.
+class PeerImports {
+ public:
+  ftar_status_t open(const IpcRef& ref, char** out) {
+    const std::string key(reinterpret_cast<const char*>(&ref.handle), sizeof ref.handle);
+    auto it = imports_.find(key);
+    if (it == imports_.end()) {
+      void* base = nullptr;
+      char* p = nullptr;
+      FTAR_RETURN_IF(ipc_import(ref, &base, &p));
+      it = imports_.emplace(key, Import{base, 0}).first;
+    }
+    ++it->second.refs;
+    *out = static_cast<char*>(it->second.base) + ref.offset;
+    handed_.emplace(*out, key);
+    return FTAR_SUCCESS;
+  }
+  void close(char* p) {
+    auto h = handed_.find(p);
+    if (h == handed_.end()) return;
+    auto it = imports_.find(h->second);
+    handed_.erase(h);
+    if (it != imports_.end() && --it->second.refs == 0) {
+      trace("ipc close %p", it->second.base);
+      hip_ignore(hipIpcCloseMemHandle(it->second.base));
+      imports_.erase(it);
+    }
+  }
+  // every peer pointer of a map_peers result (the own slot is not an import)
+  void close_all(std::vector<char*>* peers, int rank) {
+    for (int q = 0; q < (int)peers->size(); ++q)
+      if (q != rank && (*peers)[q]) close((*peers)[q]);
+    peers->clear();
+  }
+
+ private:
+  struct Import {
+    void* base;
+    int refs;
+  };
+  std::map<std::string, Import> imports_;     // peer allocation (IPC handle bytes) -> its mapping here
+  std::multimap<char*, std::string> handed_;  // peer pointer handed out -> its allocation
+};
+
 class RcclTransport final : public Transport {
  public:
-  explicit RcclTransport(ncclComm_t c) : comm_(c) {}
+  explicit RcclTransport(ncclComm_t c) : comm_(c) {
+    if (ncclCommCount(comm_, &nranks_) != ncclSuccess || nranks_ < 1) nranks_ = 1;
+  }
   ~RcclTransport() override {
     if (comm_) ncclCommDestroy(comm_);
     if (scratch_) hip_ignore(hipFree(scratch_));
@@ -211,6 +262,7 @@ class RcclTransport final : public Transport {
   // all-gathered over RCCL, opened here (dmabuf IPC; peer access enabled
   // lazily by the runtime)
   ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    if (nranks != nranks_ || rank < 0 || rank >= nranks) return FTAR_ERR_INVALID_ARG;
     FTAR_RETURN_IF(ensure_scratch());
     IpcRef ref;
     std::string why;
@@ -247,22 +299,10 @@ class RcclTransport final : public Transport {
             (*peers)[q] = static_cast<char*>(mine);
             continue;
           }
-          // one mapping per peer allocation (two registered buffers may share one),
-          // reference-counted by the pointers handed out
-          const std::string key(reinterpret_cast<const char*>(&all[q].handle), sizeof all[q].handle);
-          auto it = imports_.find(key);
-          if (it == imports_.end()) {
-            void* base = nullptr;
-            char* p = nullptr;
-            if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
-              why = std::string("rank ") + std::to_string(q) + ": " + last_error();
-              break;
-            }
-            it = imports_.emplace(key, Import{base, 0}).first;
+          if (imports_.open(all[q], &(*peers)[q]) != FTAR_SUCCESS) {
+            why = std::string("rank ") + std::to_string(q) + ": " + last_error();
+            break;
           }
-          ++it->second.refs;
-          (*peers)[q] = static_cast<char*>(it->second.base) + all[q].offset;
-          handed_.emplace((*peers)[q], key);
         }
       }
       FTAR_RETURN_IF(agree_failures(why.empty() ? 0 : 1, &failed));
@@ -275,21 +315,7 @@ class RcclTransport final : public Transport {
     }
     return FTAR_SUCCESS;
   }
-  void unmap_peers(std::vector<char*>* peers, int rank) override {
-    for (int q = 0; q < (int)peers->size(); ++q) {
-      if (q == rank || !(*peers)[q]) continue;
-      auto h = handed_.find((*peers)[q]);
-      if (h == handed_.end()) continue;
-      auto it = imports_.find(h->second);
-      handed_.erase(h);
-      if (it != imports_.end() && --it->second.refs == 0) {
-        trace("ipc close %p", it->second.base);
-        hip_ignore(hipIpcCloseMemHandle(it->second.base));
-        imports_.erase(it);
-      }
-    }
-    peers->clear();
-  }
+  void unmap_peers(std::vector<char*>* peers, int rank) override { imports_.close_all(peers, rank); }
   ftar_status_t group_start() override {
     FTAR_CHECK_NCCL(ncclGroupStart());
     return FTAR_SUCCESS;
@@ -349,18 +375,15 @@ class RcclTransport final : public Transport {
     }
     return FTAR_SUCCESS;
   }
-  ftar_status_t ensure_scratch() {  // barrier word, agreement word, FTAR_MAX_K IPC references
-    if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)FTAR_MAX_K * sizeof(IpcRef)));
+  // barrier word, agreement word, one IPC reference per rank (map_peers all-gathers nranks of them)
+  ftar_status_t ensure_scratch() {
+    if (!scratch_) FTAR_CHECK_HIP(hipMalloc(&scratch_, 256 + (size_t)std::max(nranks_, 1) * sizeof(IpcRef)));
     return FTAR_SUCCESS;
   }
   ncclComm_t comm_;
+  int nranks_ = 1;
   void* scratch_ = nullptr;
-  struct Import {
-    void* base;
-    int refs;
-  };
-  std::map<std::string, Import> imports_;         // peer allocation (IPC handle bytes) -> its mapping here
-  std::multimap<char*, std::string> handed_;      // peer pointer handed out -> its allocation
+  PeerImports imports_;
 };
 
 }  // namespace
@@ -587,80 +610,25 @@ std::unique_ptr<Transport> make_local_transport(std::shared_ptr<LocalHub> hub, i
 // ---------------------------------------------------------------------------
 // caller-bootstrapped processes (ftar_comm_init_host): peer-direct only
 // ---------------------------------------------------------------------------
+// Point-to-point transfers are unsupported: the one-round plans run in the
+// peer-direct forms (kernel loads/stores through IPC-mapped buffers), whose
+// barriers and handle exchanges go through the caller's host allgather.
+// (Round 1 carried an experimental host-synchronous bounce-buffer p2p here; a
+// long 4-process run on one GPU stalled in it, and as no product path used it,
+// it was removed.)
 namespace {
 class HostTransport final : public Transport {
-  struct Op {
-    bool is_send;
-    void* buf;
-    size_t bytes;
-    int peer;
-    hipStream_t s;
-  };
-  struct Desc {  // one staged send, published to every rank
-    int32_t peer;
-    int32_t pad;
-    uint64_t off;
-    uint64_t bytes;
-  };
-
  public:
   HostTransport(int nranks, int rank, ftar_host_allgather_fn fn, void* user)
-      : nranks_(nranks), rank_(rank), fn_(fn), user_(user) {
-    const char* e = getenv("FTAR_HOST_P2P");
-    p2p_ = e && *e && *e != '0';
-  }
-  ~HostTransport() override {
-    unmap_peers(&ppeers_, rank_);
-    if (pbuf_) {
-      forget_token(pbuf_);
-      hip_ignore(hipFree(pbuf_));
-    }
-  }
-  // Point-to-point through a bounce buffer (EXPERIMENTAL, FTAR_HOST_P2P=1),
-  // completed inside group_end with host collectives (no RCCL): every sender copies its blocks into its own
-  // IPC-exported buffer B, the ranks publish (peer, offset, bytes) of every
-  // staged block, every receiver copies its blocks out of the senders' B in
-  // per-pair posting order (MPI/RCCL matching), and a last host collective
-  // lets the senders reuse B.  Host-synchronous, so every rank takes part in
-  // every step (collective_groups) -- the engine joins idle ranks in.
-  ftar_status_t group_start() override {
-    ++depth_;
-    return FTAR_SUCCESS;
-  }
-  ftar_status_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
-    if (!p2p_) return unsupported();
-    ops_.push_back({true, const_cast<void*>(buf), bytes, peer, s});
-    return depth_ ? FTAR_SUCCESS : flush();
-  }
-  ftar_status_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
-    if (!p2p_) return unsupported();
-    ops_.push_back({false, buf, bytes, peer, s});
-    return depth_ ? FTAR_SUCCESS : flush();
-  }
-  ftar_status_t group_end() override {
-    if (depth_ <= 0) return FTAR_ERR_INVALID_ARG;
-    if (--depth_ == 0) return p2p_ ? flush() : FTAR_SUCCESS;
-    return FTAR_SUCCESS;
-  }
-  // every rank's block of `bytes` -> recv[q * bytes], through the bounce buffers
-  ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) override {
-    if (!p2p_) return unsupported();
-    for (int q = 0; q < nranks; ++q) {
-      if (q == rank) continue;
-      ops_.push_back({true, const_cast<void*>(send), bytes, q, s});
-      ops_.push_back({false, static_cast<char*>(recv) + (size_t)q * bytes, bytes, q, s});
-    }
-    ftar_status_t st = flush();
-    if (st == FTAR_SUCCESS && static_cast<char*>(recv) + (size_t)rank * bytes != send && bytes) {
-      const Segment own{send, static_cast<char*>(recv) + (size_t)rank * bytes, bytes};
-      st = launch_gather(&own, 1, s);
-    }
-    return st;
-  }
+      : nranks_(nranks), rank_(rank), fn_(fn), user_(user) {}
+  ftar_status_t group_start() override { return FTAR_SUCCESS; }
+  ftar_status_t send(const void*, size_t, int, hipStream_t) override { return unsupported(); }
+  ftar_status_t recv(void*, size_t, int, hipStream_t) override { return unsupported(); }
+  ftar_status_t group_end() override { return FTAR_SUCCESS; }
+  ftar_status_t allgather(const void*, void*, size_t, int, int, hipStream_t) override { return unsupported(); }
   const char* name() const override { return "host"; }
   bool uses_ipc() const override { return true; }
   bool async_p2p() const override { return false; }
-  bool collective_groups() const override { return p2p_; }
   // everything before it on s, on every rank, is complete when it returns
   ftar_status_t barrier(hipStream_t s) override {
     FTAR_CHECK_HIP(hipStreamSynchronize(s));
@@ -669,6 +637,7 @@ class HostTransport final : public Transport {
     return gather(&mine, all.data(), 1);
   }
   ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    if (nranks != nranks_ || rank != rank_) return FTAR_ERR_INVALID_ARG;
     IpcRef ref;
     const bool exported = ipc_export(mine, &ref) == FTAR_SUCCESS;
     std::vector<IpcRef> all(nranks);
@@ -686,14 +655,7 @@ class HostTransport final : public Transport {
           (*peers)[q] = static_cast<char*>(mine);
           continue;
         }
-        void* base = nullptr;
-        char* p = nullptr;
-        if (ipc_import(all[q], &base, &p) != FTAR_SUCCESS) {
-          failed = 1;
-          break;
-        }
-        (*peers)[q] = p;
-        bases_[p] = base;
+        if (imports_.open(all[q], &(*peers)[q]) != FTAR_SUCCESS) failed = 1;
       }
       FTAR_RETURN_IF(gather(&failed, flags.data(), sizeof failed));
       for (int f : flags) failed |= f;
@@ -705,147 +667,14 @@ class HostTransport final : public Transport {
     }
     return FTAR_SUCCESS;
   }
-  void unmap_peers(std::vector<char*>* peers, int rank) override {
-    for (int q = 0; q < (int)peers->size(); ++q) {
-      auto it = q == rank ? bases_.end() : bases_.find((*peers)[q]);
-      if (it == bases_.end()) continue;
-      trace("ipc close %p", it->second);
-      hip_ignore(hipIpcCloseMemHandle(it->second));
-      bases_.erase(it);
-    }
-    peers->clear();
-  }
+  void unmap_peers(std::vector<char*>* peers, int rank) override { imports_.close_all(peers, rank); }
 
  private:
   static ftar_status_t unsupported() {
-    set_error("host transport: point-to-point transfers are off (peer-direct forms only; FTAR_HOST_P2P=1 enables "
-              "the experimental bounce-buffer p2p)",
+    set_error("host transport: point-to-point transfers are unsupported (one-round plans in the peer-direct "
+              "forms only)",
               __FILE__, __LINE__);
     return FTAR_ERR_UNSUPPORTED;
-  }
-  ftar_status_t flush() {
-    std::vector<Op> ops;
-    ops.swap(ops_);
-    ftar_status_t st = FTAR_SUCCESS;
-    auto keep = [&](ftar_status_t e) {
-      if (st == FTAR_SUCCESS) st = e;
-    };
-    std::vector<hipStream_t> streams;
-    for (const Op& o : ops) {
-      if (o.peer < 0 || o.peer >= nranks_ || o.peer == rank_) keep(FTAR_ERR_INVALID_ARG);
-      if (std::find(streams.begin(), streams.end(), o.s) == streams.end()) streams.push_back(o.s);
-    }
-    auto sync = [&](const char* what) {
-      trace("rank %d: p2p step %llu: sync %s (%zu streams)", rank_, (unsigned long long)steps_, what, streams.size());
-      for (hipStream_t s : streams)
-        if (hipStreamSynchronize(s) != hipSuccess) keep(FTAR_ERR_HIP);
-      trace("rank %d: p2p step %llu: synced %s", rank_, (unsigned long long)steps_, what);
-    };
-    ++steps_;
-    // 1. the bounce buffer holds this step's largest send volume on any rank (collective growth)
-    uint64_t need = 0;
-    for (const Op& o : ops)
-      if (o.is_send) need += (o.bytes + 255) & ~uint64_t(255);
-    std::vector<uint64_t> needs(nranks_);
-    FTAR_RETURN_IF(gather(&need, needs.data(), sizeof need));
-    const uint64_t most = *std::max_element(needs.begin(), needs.end());
-    if (most > pbuf_bytes_ || (most && ppeers_.empty())) keep(grow(most));
-    // 2. stage my sends in my buffer
-    std::vector<Desc> mine;
-    uint64_t off = 0;
-    for (const Op& o : ops) {
-      if (!o.is_send) continue;
-      if (st == FTAR_SUCCESS && o.bytes) {
-        const Segment seg{o.buf, static_cast<char*>(pbuf_) + off, o.bytes};
-        keep(launch_gather(&seg, 1, o.s));
-      }
-      mine.push_back({o.peer, 0, off, o.bytes});
-      off += (o.bytes + 255) & ~uint64_t(255);
-    }
-    sync("staged sends");
-    // 3. publish every rank's staged sends
-    int32_t cnt = (int32_t)mine.size();
-    std::vector<int32_t> cnts(nranks_);
-    FTAR_RETURN_IF(gather(&cnt, cnts.data(), sizeof cnt));
-    const int32_t maxc = *std::max_element(cnts.begin(), cnts.end());
-    std::vector<Desc> all((size_t)nranks_ * maxc);
-    if (maxc) {
-      mine.resize(maxc, Desc{-1, 0, 0, 0});
-      FTAR_RETURN_IF(gather(mine.data(), all.data(), sizeof(Desc) * maxc));
-    }
-    // 4. my receives, in posting order per peer, out of the senders' buffers
-    std::vector<size_t> next(nranks_, 0);
-    for (const Op& o : ops) {
-      if (o.is_send || st != FTAR_SUCCESS) continue;
-      const Desc* d = nullptr;
-      for (size_t& i = next[o.peer]; i < (size_t)cnts[o.peer] && !d; ++i)
-        if (all[(size_t)o.peer * maxc + i].peer == rank_) d = &all[(size_t)o.peer * maxc + i];
-      if (!d || d->bytes != o.bytes) {
-        set_error("host transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
-        keep(FTAR_ERR_INTERNAL);
-        continue;
-      }
-      if (o.bytes) {
-        const Segment seg{ppeers_[o.peer] + d->off, o.buf, o.bytes};
-        keep(launch_gather(&seg, 1, o.s));
-      }
-    }
-    sync("receives");
-    // 5. all copies out are done (the senders may reuse their buffers); agree on the outcome
-    int32_t bad = st == FTAR_SUCCESS ? 0 : 1;
-    std::vector<int32_t> bads(nranks_);
-    FTAR_RETURN_IF(gather(&bad, bads.data(), sizeof bad));
-    for (int32_t b : bads)
-      if (b && st == FTAR_SUCCESS) {
-        set_error("host transport: a peer's transfer failed", __FILE__, __LINE__);
-        st = FTAR_ERR_INTERNAL;
-      }
-    return st;
-  }
-  // collective: every rank calls it with the same `bytes` (the step's maximum)
-  ftar_status_t grow(uint64_t bytes) {
-    // new buffer mapped first, old mappings and buffer released after (see ensure_xbuf)
-    std::vector<char*> peers;
-    void* fresh = nullptr;
-    size_t got = 0;
-    const ftar_status_t st = map_fresh(std::max<uint64_t>(bytes, 2 * pbuf_bytes_), &fresh, &got, &peers);
-    unmap_peers(&ppeers_, rank_);
-    if (pbuf_) {
-      forget_token(pbuf_);
-      hip_ignore(hipFree(pbuf_));
-    }
-    pbuf_ = st == FTAR_SUCCESS ? fresh : nullptr;
-    pbuf_bytes_ = st == FTAR_SUCCESS ? got : 0;
-    ppeers_.swap(peers);
-    return st;
-  }
-  // collective: a fresh stamped buffer of >= bytes mapped by every rank; a
-  // mapping that fails verification on any rank is retried (all ranks agree)
-  // with the failed allocation kept alive, so the next one lands elsewhere
-  ftar_status_t map_fresh(size_t bytes, void** buf, size_t* have, std::vector<char*>* peers) {
-    std::vector<void*> failed;
-    ftar_status_t st = FTAR_ERR_HIP;
-    for (int attempt = 0; attempt < 3 && st != FTAR_SUCCESS; ++attempt) {
-      void* fresh = nullptr;
-      size_t got = 0;
-      if (alloc_exportable(bytes, true, &fresh, &got) == FTAR_SUCCESS && stamp_token(fresh) != FTAR_SUCCESS) {
-        hip_ignore(hipFree(fresh));
-        fresh = nullptr;
-      }
-      st = map_peers(fresh, rank_, nranks_, peers);
-      if (st == FTAR_SUCCESS) {
-        *buf = fresh;
-        *have = got;
-      } else if (fresh) {
-        trace("rank %d: mapping of %p failed (%s), retrying", rank_, fresh, last_error());
-        failed.push_back(fresh);
-      }
-    }
-    for (void* f : failed) {
-      forget_token(f);
-      hip_ignore(hipFree(f));
-    }
-    return st;
   }
   ftar_status_t gather(const void* mine, void* all, size_t bytes) {
     if (fn_(mine, all, bytes, user_) != 0) {
@@ -857,14 +686,7 @@ class HostTransport final : public Transport {
   int nranks_, rank_;
   ftar_host_allgather_fn fn_;
   void* user_;
-  std::map<char*, void*> bases_;
-  std::vector<Op> ops_;
-  int depth_ = 0;
-  unsigned long long steps_ = 0;  // p2p steps so far (trace)
-  bool p2p_ = false;      // FTAR_HOST_P2P: the bounce-buffer p2p below (experimental, off by default)
-  void* pbuf_ = nullptr;  // bounce buffer of the p2p steps, IPC-mapped by every rank
-  size_t pbuf_bytes_ = 0;
-  std::vector<char*> ppeers_;
+  PeerImports imports_;
 };
 }  // namespace
 

@@ -48,7 +48,8 @@ _AG_NAME = {v: k for k, v in ALLGATHER.items()}
 REDUCE_SCATTER = {"stages": 0, "direct": 1}                 # ftar_reduce_scatter_t
 _RS_NAME = {v: k for k, v in REDUCE_SCATTER.items()}
 STATUS = {0: "success", 1: "invalid argument", 2: "unsupported dtype/op", 3: "invalid FT_TOPO/FT_LONELY",
-          4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout"}
+          4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout",
+          8: "out of device memory"}
 MAX_STAGES = 16
 _TORCH_DTYPE_NAMES = {"torch.float32": "f32", "torch.float64": "f64", "torch.bfloat16": "bf16", "torch.int32": "i32",
                       "torch.int64": "i64", "torch.int16": "i16", "torch.int8": "i8", "torch.uint8": "u8",
@@ -94,6 +95,12 @@ _lib.ftar_topo_choose.argtypes = [_int, _sz, ctypes.POINTER(Topo)]
 _lib.ftar_topo_candidates.argtypes = [_int, ctypes.POINTER(Topo), _int]
 _lib.ftar_topo_cost.argtypes = [ctypes.POINTER(Topo), _int, _sz]
 _lib.ftar_topo_cost.restype = ctypes.c_double
+_lib.ftar_cost_reference.argtypes = [ctypes.POINTER(_int), _int, _int, ctypes.c_double]
+_lib.ftar_cost_reference.restype = ctypes.c_double
+_lib.ftar_topo_choose_reference.argtypes = [_int, ctypes.c_double, ctypes.POINTER(Topo), ctypes.POINTER(_int)]
+_lib.ftar_cost_reference_candidates.argtypes = [_int, ctypes.POINTER(_int), _int, ctypes.POINTER(_int), _int]
+_lib.ftar_cost_set_params.argtypes = [ctypes.c_double] * 3
+_lib.ftar_cost_get_params.argtypes = [ctypes.POINTER(ctypes.c_double)] * 3
 _lib.ftar_topo_format.argtypes = [ctypes.POINTER(Topo), ctypes.c_char_p, _sz]
 _lib.ftar_get_unique_id.argtypes = [ctypes.POINTER(UniqueId)]
 _lib.ftar_comm_init_rank.argtypes = [ctypes.POINTER(_vp), _int, UniqueId, _int, _int]
@@ -268,6 +275,46 @@ def topo_candidates(nranks):
 
 def topo_cost(t, nranks, nbytes):
     return _lib.ftar_topo_cost(ctypes.byref(topo(t)), nranks, nbytes)
+
+
+def cost_reference(widths, nranks, chunk=100.0):
+    """The reference's CostModel score of one getWidth-style width list (cost_model/CostModel.h:1-120)."""
+    arr = (_int * len(widths))(*widths)
+    return _lib.ftar_cost_reference(arr, len(widths), nranks, chunk)
+
+
+def reference_candidates(nranks):
+    """getWidth(P) (cost_model/GetWidth.h:42-47) as lists, [1,P] and [P,1] included."""
+    n = _lib.ftar_cost_reference_candidates(nranks, None, 0, None, 0)
+    if n < 0:
+        raise FtarError(-n, "ftar_cost_reference_candidates")
+    lens = (_int * n)()
+    _lib.ftar_cost_reference_candidates(nranks, None, 0, lens, n)
+    tot = sum(lens)
+    ws = (_int * tot)()
+    _lib.ftar_cost_reference_candidates(nranks, ws, tot, lens, n)
+    out, at = [], 0
+    for ln in lens:
+        out.append(list(ws[at:at + ln]))
+        at += ln
+    return out
+
+
+def topo_choose_reference(nranks, chunk=100.0):
+    """The reference cost model's argmin (CostModel.h:82-120): (topology, index into reference_candidates)."""
+    t, i = Topo(), _int(0)
+    _check(_lib.ftar_topo_choose_reference(nranks, chunk, ctypes.byref(t), ctypes.byref(i)),
+           "ftar_topo_choose_reference")
+    return t, i.value
+
+
+def cost_params(alpha_us=None, link_gbps=None, hbm_gbps=None):
+    """Read, or set (process-wide; 0 restores the default), the xGMI cost model's constants."""
+    if alpha_us is not None or link_gbps is not None or hbm_gbps is not None:
+        _check(_lib.ftar_cost_set_params(alpha_us or 0.0, link_gbps or 0.0, hbm_gbps or 0.0), "ftar_cost_set_params")
+    v = [ctypes.c_double() for _ in range(3)]
+    _check(_lib.ftar_cost_get_params(*[ctypes.byref(x) for x in v]), "ftar_cost_get_params")
+    return {"alpha_us": v[0].value, "link_GBps": v[1].value, "hbm_GBps": v[2].value}
 
 
 def schedule_json(t, nranks, rank, count):

@@ -14,7 +14,15 @@
 // --dump PREFIX (every rank writes its final buffer to PREFIX.<rank>.bin, raw
 // fp32: the parity tests compare it with the reference's own output),
 // --warmup W (untimed calls first; the reference's first call pays one-time
-// setup), and one JSON summary line on rank 0.
+// setup), --no-register (host buffers: pageable copies instead of
+// MPI_Allreduce_FT_register), and one JSON summary line on rank 0.
+// Communicator lifecycle checks (after the timed calls):
+//   --comm-cycle C    C communicators created and freed in turn, duplicates of
+//                     MPI_COMM_WORLD alternating with singleton splits (MPI
+//                     recycles the handles), one exact integer-valued
+//                     MPI_Allreduce_FT on each;
+//   --comm-threads T  T duplicates driven at once from T threads
+//                     (MPI_THREAD_MULTIPLE), 3 exact calls each.
 // --check is two-sided here: the reference only flags results that are too
 // LARGE (benchmark.cpp:201), so NaN/zero results pass there.
 #include <hip/hip_runtime_api.h>
@@ -45,8 +53,8 @@ int main(int argc, char** argv) {
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
 
   size_t data_len = 35;
-  int repeat = 1, warmup = 0;
-  bool to_file = false, check = false, device = false;
+  int repeat = 1, warmup = 0, comm_cycle = 0, comm_threads = 0;
+  bool to_file = false, check = false, device = false, do_register = true;
   std::string tag, comm_type = "flextree", dump;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -63,6 +71,9 @@ int main(int argc, char** argv) {
     else if (a == "--check") check = true;
     else if (a == "--device") device = true;
     else if (a == "--dump") dump = next();
+    else if (a == "--no-register") do_register = false;
+    else if (a == "--comm-cycle") comm_cycle = atoi(next().c_str());
+    else if (a == "--comm-threads") comm_threads = atoi(next().c_str());
     else if (a == "--version") {
       if (rank == 0) printf("ftar_benchmark: %s\n", ftar_version());
       MPI_Finalize();
@@ -82,6 +93,9 @@ int main(int argc, char** argv) {
   char topo_s[128] = "?";
   if (have_topo) ftar_topo_format(&topo, topo_s, sizeof topo_s);
 
+  // the host buffer stays alive for the whole run: pin it once (RCCL-style user-buffer registration)
+  const bool registered = !device && comm_type == "flextree" && do_register && data_len &&
+                          MPI_Allreduce_FT_register(data.data(), data_len * sizeof(float)) == MPI_SUCCESS;
   float* dptr = nullptr;
   if (device) {
     ftar_comm_t fc;
@@ -170,7 +184,85 @@ int main(int argc, char** argv) {
   MPI_Allreduce(&min_time, &max_min, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
   MPI_Allreduce(&avg, &max_avg, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
 
+  // communicator lifecycle: state released by MPI_Comm_free, fresh state under recycled handles
+  int lifecycle_bad = 0;
+  if (comm_cycle > 0 && comm_type == "flextree") {
+    const size_t n = 4099;
+    std::vector<float> buf(n);
+    int reused = 0, bad_c = 0;
+    MPI_Comm prev = MPI_COMM_NULL;
+    for (int c = 0; c < comm_cycle; ++c) {
+      MPI_Comm cc;
+      const bool single = c % 2 == 1;
+      if (single) MPI_Comm_split(MPI_COMM_WORLD, rank, 0, &cc);
+      else MPI_Comm_dup(MPI_COMM_WORLD, &cc);
+      if (c > 0 && cc == prev) ++reused;
+      prev = cc;
+      for (size_t i = 0; i < n; ++i) buf[i] = (float)((rank + 1) * (int)(i % 1000) + c);
+      if (MPI_Allreduce_FT(MPI_IN_PLACE, buf.data(), (int)n, MPI_FLOAT, MPI_SUM, cc) != MPI_SUCCESS) ++bad_c;
+      const int ranks = single ? 1 : P;
+      for (size_t i = 0; i < n && !bad_c; ++i) {
+        const double want = single ? (double)((rank + 1) * (int)(i % 1000) + c)
+                                   : (double)P * (P + 1) / 2 * (int)(i % 1000) + (double)ranks * c;
+        if ((double)buf[i] != want) ++bad_c;
+      }
+      MPI_Comm_free(&cc);
+    }
+    for (int r = 0; r <= P; ++r) {
+      MPI_Barrier(MPI_COMM_WORLD);
+      if (r == rank + 1) {
+        printf("COMM_CYCLE %d: cycles=%d handles_reused=%d %s\n", rank, comm_cycle, reused, bad_c ? "FAILED" : "ok");
+        fflush(stdout);
+      }
+    }
+    lifecycle_bad += bad_c;
+  }
+  if (comm_threads > 0 && comm_type == "flextree") {
+    if (provided < MPI_THREAD_MULTIPLE) {
+      if (rank == 0) printf("COMM_THREADS skipped: MPI provides thread level %d\n", provided);
+    } else {
+      std::vector<MPI_Comm> comms(comm_threads);
+      for (auto& cc : comms) MPI_Comm_dup(MPI_COMM_WORLD, &cc);  // same order on every rank
+      std::vector<int> bad_t(comm_threads, 0);
+      std::vector<std::thread> th;
+      for (int t = 0; t < comm_threads; ++t)
+        th.emplace_back([&, t] {
+          const size_t n = 8192 + 64 * t;
+          std::vector<float> b(n);
+          for (int it = 0; it < 3; ++it) {
+            for (size_t i = 0; i < n; ++i) b[i] = (float)((rank + 1) * (t + 1) + (int)(i % 512) + it);
+            if (MPI_Allreduce_FT(MPI_IN_PLACE, b.data(), (int)n, MPI_FLOAT, MPI_SUM, comms[t]) != MPI_SUCCESS) {
+              ++bad_t[t];
+              return;
+            }
+            for (size_t i = 0; i < n; ++i) {
+              const double want = (double)(t + 1) * P * (P + 1) / 2 + (double)P * ((int)(i % 512) + it);
+              if ((double)b[i] != want) {
+                ++bad_t[t];
+                return;
+              }
+            }
+          }
+        });
+      for (auto& x : th) x.join();
+      for (auto& cc : comms) MPI_Comm_free(&cc);
+      int bad = 0;
+      for (int v : bad_t) bad += v;
+      for (int r = 0; r <= P; ++r) {
+        MPI_Barrier(MPI_COMM_WORLD);
+        if (r == rank + 1) {
+          printf("COMM_THREADS %d: threads=%d %s\n", rank, comm_threads, bad ? "FAILED" : "ok");
+          fflush(stdout);
+        }
+      }
+      lifecycle_bad += bad;
+    }
+  }
+  int lifecycle_bad_all = 0;
+  MPI_Allreduce(&lifecycle_bad, &lifecycle_bad_all, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
+
   if (device) (void)hipFree(dptr);
+  if (registered) MPI_Allreduce_FT_unregister(data.data());
   MPI_Allreduce_FT_finalize();
   MPI_Finalize();
 
@@ -203,5 +295,5 @@ int main(int argc, char** argv) {
            bytes / tmin / 1e9, P > 1 ? bytes / tmin / 1e9 * 2.0 * (P - 1) / P : bytes / tmin / 1e9,
            check ? (bad_all ? "FAILED" : "passed") : "off");
   }
-  return bad_all ? 2 : 0;
+  return bad_all || lifecycle_bad_all ? 2 : 0;
 }

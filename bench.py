@@ -443,6 +443,31 @@ def bench_distributed(a):
             reg["ids"] = [comm.register(reg["x"], bucket), comm.register(reg["y"], bucket)]
         return reg["x"], reg["y"]
 
+    def fit_cost_model(probe):
+        """The xGMI cost model's constants from this node: link = the probe's per-link,
+        per-direction rate; alpha = half the time of a 4 KiB direct-form AllReduce (two p2p rounds, no
+        bandwidth term to speak of).  Set process-wide (ftar_cost_set_params) on every rank alike, so the
+        C5 line item and every later choice use them; reported next to the defaults and to the reference
+        model's own choice (CostModel.h, chunk 100)."""
+        default = ftar.cost_params()
+        link = link_rate_from_probe(probe, world)
+        small = torch.zeros(1024, device=dev)
+        small_y = torch.empty_like(small)
+        comm.peer_direct, comm.allgather, comm.reduce_scatter = 0, "direct", "direct"
+        ms_small = timed(lambda: comm.allreduce(small, small_y, 1024, "f32", "sum", topo_=ftar.topo(str(world)),
+                                                stream=stream), 20, 3)
+        v = torch.tensor([link or 0.0, ms_small], dtype=torch.float64)
+        dist.broadcast(v, 0)  # one set of constants on every rank: identical choices everywhere
+        link, ms_small = (v[0].item() or None), v[1].item()
+        fitted = ftar.cost_params(alpha_us=ms_small * 1e3 / 2, link_gbps=link or 0.0)
+        t_ref, _ = ftar.topo_choose_reference(world)
+        return {"default": {k: round(x, 3) for k, x in default.items()},
+                "fitted": {k: round(x, 3) for k, x in fitted.items()},
+                "source": "link: ftar_xgmi_probe best per-link one-direction rate (rank 0); alpha: half a 4 KiB "
+                          "direct AllReduce" + ("" if link else "; probe gave no link rate: default link kept"),
+                "choice_fitted": str(ftar.topo_choose(world, bucket)),
+                "choice_reference_model": str(t_ref)}
+
     # correctness of y: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
     idx = sample_index(n, dev)
     xs = x[idx].float().cpu()
@@ -532,6 +557,9 @@ def bench_distributed(a):
                 "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
                 "check": "ok" if bool(flag.item()) else "MISMATCH",
                 "cost_model_s": round(ftar.topo_cost(t5, world, nb * 2), 6),
+                "cost_model_params": ftar.cost_params(),
+                "cost_model_choice_now": str(ftar.topo_choose(world, nb * 2)),
+                "reference_model_choice": str(ftar.topo_choose_reference(world)[0]),
                 "other_widths": widths}
 
     def measure_host():
@@ -631,9 +659,7 @@ def bench_distributed(a):
             continue
         seen.add(key)
         forms = ["direct"] + (["collective"] if (not t.ring and n % world == 0) else []) + ["stages"]
-        if a.host_comm and os.environ.get("FTAR_HOST_P2P", "0") in ("", "0"):
-            # the host transport's p2p is an experimental host-synchronous bounce-buffer fallback (FTAR_HOST_P2P=1,
-            # DESIGN §4), not a data path to time: without it, the peer forms only
+        if a.host_comm:  # the host-bootstrapped communicator has no p2p transfers: the peer forms only
             forms = []
         for form in forms:
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
@@ -677,6 +703,10 @@ def bench_distributed(a):
                 state["line"]["xgmi_probe_GBps"]["by_workgroups_per_peer"] = by_cap
             except Exception as e:  # noqa: BLE001
                 state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
+            try:
+                state["line"]["cost_model_fit"] = fit_cost_model(state["line"].get("xgmi_probe_GBps"))
+            except Exception as e:  # noqa: BLE001
+                state["line"]["cost_model_fit"] = {"error": str(e)[:200]}
         stop = torch.tensor([1 if time.time() - sweep_t0 > sweep_budget else 0], dtype=torch.int32)
         dist.broadcast(stop, 0)  # every rank takes the same decision
         if stop.item():
@@ -705,7 +735,7 @@ def bench_distributed(a):
         ms = timed(fn_best, a.steps, a.warmup)
         ok, _ = check_y(fn_best)
         if ok and ms < ms_default:
-            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps",) if k in state["line"]}
+            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps", "cost_model_fit") if k in state["line"]}
             state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,
                                         {"config_selection": "best validated configuration of the sweep",
                                          "default_config": default_info, "sweep": sweep, **carry})

@@ -68,7 +68,8 @@ typedef enum {
   FTAR_ERR_HIP = 4,
   FTAR_ERR_RCCL = 5,
   FTAR_ERR_INTERNAL = 6,
-  FTAR_ERR_TIMEOUT = 7
+  FTAR_ERR_TIMEOUT = 7,
+  FTAR_ERR_NO_MEMORY = 8      /* a device allocation (scratch, staging, exchange buffer) failed */
 } ftar_status_t;
 
 /* Topology = FT_TOPO stage widths (bottom-up) + FT_LONELY count.  ring != 0
@@ -126,6 +127,30 @@ ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out);
 int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out);
 /* Model cost (seconds) of one topology for a bucket of `bytes`. */
 double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes);
+/* Constants of that (xGMI) model: alpha = one p2p round's latency (us), link =
+ * one peer's one-direction bandwidth (GB/s), hbm = the reduce kernel's rate
+ * (GB/s).  Process-wide; a value <= 0 restores the default; the environment
+ * (FTAR_COST_ALPHA_US / _LINK_GBPS / _HBM_GBPS) overrides both.  bench.py sets
+ * them from ftar_xgmi_probe. */
+ftar_status_t ftar_cost_set_params(double alpha_us, double link_gbps, double hbm_gbps);
+ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* hbm_gbps);
+
+/* The reference's own cost model, restated bit for bit
+ * (cost_model/CostModel.h:1-120; tests/golden/costmodel.jsonl holds its
+ * output).  ftar_topo_choose uses it instead of the xGMI model when
+ * FTAR_COST_MODEL=reference (chunk = FTAR_COST_REF_CHUNK, default 100 as in
+ * cost_model/main.cpp:23).
+ *   ftar_cost_reference       score of one getWidth-style width list (a width
+ *                             1 = the ring's [1,P]/[P,1]); < 0 where the
+ *                             reference has no case (height 0 or > 9)
+ *   ftar_topo_choose_reference its argmin over getWidth(P), first minimum wins
+ *                             (CostModel.h:97); *index = position in that list
+ *   ftar_cost_reference_candidates getWidth(P) (GetWidth.h:42-47) flattened:
+ *                             returns the number of lists, their lengths in
+ *                             lengths[], their widths concatenated in widths[] */
+double ftar_cost_reference(const int* widths, int nwidths, int nranks, double chunk);
+ftar_status_t ftar_topo_choose_reference(int nranks, double chunk, ftar_topo_t* out, int* index);
+int ftar_cost_reference_candidates(int nranks, int* widths, int max_widths, int* lengths, int max_lists);
 /* Writes "w0,w1,..+L" / "ring" into buf; returns needed length. */
 int ftar_topo_format(const ftar_topo_t* topo, char* buf, size_t buflen);
 

@@ -45,8 +45,22 @@ int MPI_Allreduce_FT_device(const void* sendbuf, void* recvbuf, int count, MPI_D
 /* The ftar communicator bound to an MPI communicator (created on first use). */
 int MPI_Allreduce_FT_comm(MPI_Comm comm, ftar_comm_t* out);
 
+/* Pin a host buffer for the copies of MPI_Allreduce_FT (hipHostRegister),
+ * until MPI_Allreduce_FT_unregister; the caller keeps it alive meanwhile.
+ * Calls on unregistered buffers copy pageable, unless FTAR_MPI_REGISTER=1
+ * (pin every buffer passed in, at most FTAR_MPI_REGISTER_MAX = 4 kept, least
+ * recently used evicted: the caller must not free such a buffer while it may
+ * be cached).  unregister returns MPI_ERR_ARG for an unknown pointer and
+ * MPI_ERR_PENDING while a call copies through it. */
+int MPI_Allreduce_FT_register(const void* buf, size_t bytes);
+int MPI_Allreduce_FT_unregister(const void* buf);
+
 /* Release every cached communicator, device buffer and host registration.
- * Call before MPI_Finalize (the reference leaks its buffer, mpi_mod.hpp:1489). */
+ * Optional: each communicator's state is also released by MPI_Comm_free (an
+ * MPI attribute with a delete callback; MPI_Finalize for MPI_COMM_WORLD), and
+ * a communicator created later under the same handle starts fresh.  (The
+ * reference leaks its buffer, mpi_mod.hpp:1489, and a communicator per call,
+ * :1541-1548.) */
 int MPI_Allreduce_FT_finalize(void);
 
 /* Map an MPI datatype / op of the reference (mpi_mod.hpp:1363-1412) to ftar. */

@@ -14,11 +14,16 @@ fixtures:
   tests/golden/schedules.jsonl FMA-level send/recv schedules per rank
   tests/golden/inputs.json     first draws of the input generator (pins it)
   tests/golden/getwidth.json   the cost model's candidate width lists, P = 1..24
+  tests/golden/costmodel.jsonl the cost model's per-candidate scores and argmin
+                               (CostModel.h:1-120) for P = 2..48 and a few
+                               larger P, chunk = 100 (main.cpp:23), 1 and 1000
+                               (oracle/_ref/ref_costmodel, -O0)
 
 Inputs are not stored: they are regenerated from (seed, rank) with
 include/ftar_inputs.h / tests/ftar_inputs.py, which inputs.json pins.
 
-Usage:  python oracle/gen_golden.py   (needs /root/reference, MPICH, ~2 min)
+Usage:  python oracle/gen_golden.py              (needs /root/reference, MPICH, ~2 min)
+        python oracle/gen_golden.py costmodel    (only costmodel.jsonl)
 """
 import hashlib
 import itertools
@@ -71,6 +76,20 @@ def run_allreduce(P, topo, lonely, dtype, op, n, seed, oop=False, repeat=1, init
             with open(f"{prefix}.{r}.bin", "rb") as f:
                 outs.append(f.read())
     return outs
+
+
+COSTMODEL_P = list(range(2, 49)) + [60, 64, 72, 96, 128, 256, 512]
+COSTMODEL_CHUNKS = ["100", "1", "1000"]
+
+
+def gen_costmodel():
+    """The reference's CostModel(getWidth(P), P, chunk) as its own build prints it (oracle/ref_costmodel.cpp)."""
+    exe = os.path.join(HERE, "_ref", "ref_costmodel")
+    with open(os.path.join(OUT, "costmodel.jsonl"), "w") as f:
+        for P in COSTMODEL_P:
+            out = subprocess.run([exe, str(P), str(P)] + COSTMODEL_CHUNKS, check=True, capture_output=True,
+                                 text=True).stdout
+            f.write(out)
 
 
 def main():
@@ -167,4 +186,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["costmodel"]:
+        gen_costmodel()
+    else:
+        main()
+        gen_costmodel()

@@ -157,3 +157,75 @@ def test_header_is_plain_c99(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, (out.returncode, out.stdout, out.stderr)
     assert "c99 ok" in out.stdout
+
+
+def _costmodel_golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "costmodel.jsonl")) as f:
+        return [json.loads(line) for line in f]
+
+
+def test_reference_cost_model_matches_reference_output():
+    """The reference's cost model restated in libftar (ftar_cost_reference, ftar_topo_choose_reference) against
+    what the reference itself prints (tests/golden/costmodel.jsonl, oracle/ref_costmodel.cpp around the
+    unmodified cost_model/CostModel.h + GetWidth.h): every candidate list in getWidth's order, every
+    candidate's score to the last bit (printed at 17 digits), and the argmin, for P = 2..48, 60, 64, 72, 96,
+    128, 256, 512 and chunk 100 (cost_model/main.cpp:23), 1 and 1000."""
+    import ftar
+    rows = _costmodel_golden()
+    assert len(rows) >= 150
+    for d in rows:
+        P, ch = d["P"], d["chunk"]
+        cands = ftar.reference_candidates(P)
+        assert cands == d["candidates"], P
+        for w, c in zip(cands, d["costs"]):
+            assert ftar.cost_reference(w, P, ch) == float(c), (P, ch, w)
+        t, idx = ftar.topo_choose_reference(P, ch)
+        assert "*".join(map(str, cands[idx])) == d["chosen"], (P, ch, cands[idx], d["chosen"])
+        assert ftar.cost_reference(cands[idx], P, ch) == float(d["cost"])
+        want = "ring" if 1 in cands[idx] else ",".join(map(str, cands[idx]))
+        assert str(t) == want, (P, str(t), want)
+
+
+def test_reference_cost_model_picks_the_ring_at_2_4_8():
+    """with chunk 100 the reference's model chooses 1*2, 1*4, 1*8 -- the ring."""
+    import ftar
+    for P in (2, 4, 8):
+        t, idx = ftar.topo_choose_reference(P)
+        assert str(t) == "ring" and ftar.reference_candidates(P)[idx] == [1, P]
+
+
+def test_cost_model_selector(monkeypatch):
+    """FTAR_COST_MODEL=reference makes ftar_topo_choose (and so FT_TOPO-less communicators) take the
+    reference's argmin; the default stays the xGMI model (width 8 at P = 8); anything else is refused."""
+    import ftar
+    monkeypatch.delenv("FT_TOPO", raising=False)
+    monkeypatch.setenv("FTAR_COST_MODEL", "reference")
+    assert str(ftar.topo_choose(8, 1 << 30)) == "ring"
+    monkeypatch.setenv("FTAR_COST_REF_CHUNK", "100")
+    assert str(ftar.topo_choose(12, 1 << 30)) == "2,6"
+    monkeypatch.setenv("FTAR_COST_MODEL", "xgmi")
+    assert str(ftar.topo_choose(8, 1 << 30)) == "8"
+    monkeypatch.setenv("FTAR_COST_MODEL", "bogus")
+    with pytest.raises(ftar.FtarError):
+        ftar.topo_choose(8, 1 << 30)
+
+
+def test_cost_params_set_and_restore(monkeypatch):
+    """ftar_cost_set_params (bench.py fits it from the xGMI probe) changes the xGMI model's constants and
+    its costs; 0 restores the defaults; the environment still overrides."""
+    import ftar
+    for k in ("FTAR_COST_ALPHA_US", "FTAR_COST_LINK_GBPS", "FTAR_COST_HBM_GBPS"):
+        monkeypatch.delenv(k, raising=False)
+    base = ftar.cost_params()
+    c0 = ftar.topo_cost("8", 8, 1 << 30)
+    try:
+        p = ftar.cost_params(alpha_us=5.0, link_gbps=2 * base["link_GBps"])
+        assert p["alpha_us"] == pytest.approx(5.0) and p["link_GBps"] == pytest.approx(2 * base["link_GBps"])
+        assert ftar.topo_cost("8", 8, 1 << 30) < c0
+        monkeypatch.setenv("FTAR_COST_LINK_GBPS", "10")
+        assert ftar.cost_params()["link_GBps"] == pytest.approx(10.0)
+    finally:
+        ftar.cost_params(0.0, 0.0, 0.0)
+    monkeypatch.delenv("FTAR_COST_LINK_GBPS")
+    assert ftar.cost_params() == base and ftar.topo_cost("8", 8, 1 << 30) == c0

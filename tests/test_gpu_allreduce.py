@@ -346,3 +346,55 @@ def test_random_soak_all_forms(seed):
         for r in range(c["P"]):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"],
                                                                 rs, ag, peer, r)
+
+
+@pytest.mark.parametrize("host", [False, True], ids=["device", "host"])
+def test_calls_on_alternating_streams_without_sync(host):
+    """Consecutive calls on one communicator share its scratch (and, for host buffers, its staging buffer).
+    Call i+1 issued on ANOTHER stream than call i, with no synchronisation in between, must not overwrite
+    scratch call i's reduces are still reading: the entry waits for the previous call's completion marker
+    (engine.cpp allreduce).  P = 2 ring, direct forms, 1 MiB pieces of a 64 MiB bucket, 6 calls alternating
+    between two streams on every rank; every output is x0 + x1 exactly (fp32 addition commutes)."""
+    import threading
+
+    import torch
+    import ftar
+    P, n, calls = 2, 1 << 24, 6
+    comms = ftar.Comm.init_local(P)
+    try:
+        comms.set_chunk_bytes(1 << 20)
+        comms.set_allgather("direct")
+        comms.set_reduce_scatter("direct")
+        gen = torch.Generator().manual_seed(7)
+        xs = [[torch.rand(n, generator=gen) * 2 - 1 for _ in range(P)] for _ in range(calls)]
+        expect = [x[0] + x[1] for x in xs]
+        if host:
+            ins = [[x.pin_memory() for x in xc] for xc in xs]
+            outs = [[torch.empty(n).pin_memory() for _ in range(P)] for _ in range(calls)]
+        else:
+            ins = [[x.cuda() for x in xc] for xc in xs]
+            outs = [[torch.empty(n, device="cuda") for _ in range(P)] for _ in range(calls)]
+        streams = [[torch.cuda.Stream() for _ in range(2)] for _ in range(P)]
+        torch.cuda.synchronize()
+        errs = []
+
+        def rank(r):
+            try:
+                c = comms.comms[r]
+                for i in range(calls):
+                    fn = c.allreduce_host if host else c.allreduce
+                    fn(ins[i][r], outs[i][r], n, "f32", "sum", topo_="1", stream=streams[r][i % 2])
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+        th = [threading.Thread(target=rank, args=(r,)) for r in range(P)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs, errs
+        for i in range(calls):
+            for r in range(P):
+                assert torch.equal(outs[i][r].cpu(), expect[i]), (i, r)
+    finally:
+        comms.destroy()

@@ -11,8 +11,7 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-# (topo, lonely, reduce-scatter form, all-gather form, chunk bytes) for the bounce-buffer p2p path
-P2P_CASES = {2: [("1", 0, "stages", "stages", 1 << 16), ("2", 0, "direct", "collective", 0),
+CASES = {2: [("1", 0, "stages", "stages", 1 << 16), ("2", 0, "direct", "collective", 0),
                  ("1", 0, "direct", "direct", 4096)],
              4: [("2,2", 0, "stages", "stages", 1 << 16), ("1", 0, "stages", "stages", 0),
                  ("2,2", 0, "direct", "collective", 1 << 15), ("4", 0, "direct", "direct", 0)],
@@ -32,7 +31,7 @@ def _worker(rank, world, port, n, q):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FTAR_HOST_P2P="1")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch
     import torch.distributed as dist
     import ftar
@@ -61,21 +60,18 @@ def _worker(rank, world, port, n, q):
                         for r in regs:
                             comm.deregister(r)
                         dist.barrier()
-        # point-to-point through the bounce buffers (host-synchronous): every other form, lonely plans,
-        # host buffers (pipelined path), all across the process boundary
+        # plans that need point-to-point transfers (staged forms, lonely ranks) are refused alike on every
+        # rank before anything moves: the host-bootstrapped communicator has the peer forms only
         comm.peer_direct = 0
-        for topo, lonely, rs, ag, chunk in P2P_CASES[world]:
-            x = fi.fill("f32", 23, rank, n)
-            xt = torch.from_numpy(x.copy()).cuda()
-            comm.reduce_scatter, comm.allgather, comm.chunk_bytes = rs, ag, chunk
-            comm.allreduce(None, xt, n, "f32", "sum", topo_=topo, lonely=lonely)
-            torch.cuda.synchronize()
-            out[("p2p", topo, lonely, rs, ag)] = xt.cpu().numpy().tobytes()
-        hx = torch.from_numpy(fi.fill("f32", 23, rank, n).copy()).pin_memory()
-        comm.reduce_scatter, comm.allgather, comm.chunk_bytes = "direct", "direct", 1 << 16
-        comm.allreduce_host(None, hx, n, "f32", "sum", topo_=P2P_CASES[world][0][0], lonely=P2P_CASES[world][0][1])
-        torch.cuda.synchronize()
-        out["host"] = hx.numpy().tobytes()
+        xt = torch.from_numpy(fi.fill("f32", 23, rank, n).copy()).cuda()
+        comm.reduce_scatter, comm.allgather = "stages", "stages"
+        try:
+            comm.allreduce(None, xt, n, "f32", "sum", topo_="1")
+            out["p2p"] = "ran"
+        except ftar.FtarError as e:
+            out["p2p"] = e.status
+        comm.reduce_scatter, comm.allgather = "direct", "direct"
+        dist.barrier()
         comm.destroy()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001  report, don't hang the parent
@@ -107,13 +103,7 @@ def test_peer_forms_across_processes(world):
         for key in keys:
             for r in range(world):
                 assert res[r][key] == ref[r].tobytes(), (world, key, r)
-    ins = [fi.fill("f32", 23, r, n) for r in range(world)]
-    for topo, lonely, rs, ag, _ in P2P_CASES[world]:
-        ref = oracle_lib.allreduce(ins, topo, lonely)
-        for r in range(world):
-            assert res[r][("p2p", topo, lonely, rs, ag)] == ref[r].tobytes(), (world, topo, lonely, rs, ag, r)
-    ref = oracle_lib.allreduce(ins, P2P_CASES[world][0][0], P2P_CASES[world][0][1])
-    assert all(res[r]["host"] == ref[r].tobytes() for r in range(world))
+    assert all(res[r]["p2p"] == 2 for r in range(world)), [res[r]["p2p"] for r in range(world)]  # UNSUPPORTED
 
 
 def _big_worker(rank, world, port, n, q):

@@ -100,3 +100,32 @@ def test_harness_reproduces_reference_benchmark_output(tmp_path, case_id, device
 def test_harness_rccl_only_fails_cleanly_on_a_shared_gpu(tmp_path):
     rc, out = run(2, ["--size", "4096", "--repeat", "1"], tmp_path, {"FT_TOPO": "2", "FTAR_MPI_TRANSPORT": "rccl"})
     assert rc != 0, out
+
+
+@needs
+def test_harness_communicator_lifecycle_single_rank(tmp_path):
+    """MPI_Allreduce_FT state hangs on the communicator as an MPI attribute: freeing it releases the state
+    (delete callback) and a communicator created later under the recycled handle starts fresh; threads on
+    different communicators run at once (MPI_THREAD_MULTIPLE, benchmark.cpp:50)."""
+    rc, out = run(1, ["--size", "1000", "--check", "--comm-cycle", "6", "--comm-threads", "3"], tmp_path)
+    assert rc == 0, out
+    m = re.search(r"COMM_CYCLE 0: cycles=6 handles_reused=(\d+) ok", out)
+    assert m, out
+    assert "COMM_THREADS 0: threads=3 ok" in out or "COMM_THREADS skipped" in out, out
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--no-register"]], ids=["registered", "pageable"])
+def test_harness_communicator_lifecycle_two_ranks(tmp_path, extra):
+    """Two ranks: duplicates of MPI_COMM_WORLD (a 2-rank AllReduce) alternate with singleton splits (the
+    reference's P <= 1 copy, mpi_mod.hpp:1739) under handles MPICH recycles; with a raw-handle cache the
+    singleton would reuse the freed 2-rank state.  Then 2 threads drive 2 communicators at once.  Exact
+    integer-valued sums."""
+    rc, out = run(2, ["--size", "65536", "--repeat", "2", "--check", "--comm-cycle", "6", "--comm-threads", "2"]
+                  + extra, tmp_path, {"FT_TOPO": "2"})
+    assert rc == 0, out
+    assert out.count("(test passed)") == 2, out
+    for r in range(2):
+        assert re.search(rf"COMM_CYCLE {r}: cycles=6 handles_reused=\d+ ok", out), out
+        assert f"COMM_THREADS {r}: threads=2 ok" in out or "COMM_THREADS skipped" in out, out
