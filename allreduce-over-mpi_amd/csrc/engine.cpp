@@ -80,6 +80,10 @@ struct ftar_comm {
   hipEvent_t done_ev = nullptr;
   hipStream_t done_stream = nullptr;
   bool done_recorded = false;
+  bool capturing = false;  // the current call's stream is being captured: no allocation, no host sync
+  // events handed to captured calls: each captured call records a fresh set
+  // (an event is never re-recorded inside one capture), kept until teardown
+  std::vector<hipEvent_t> captured_events;
   std::mutex mu;
 };
 
@@ -110,6 +114,10 @@ ftar_status_t mark(ftar_comm* c, const std::string& name, hipStream_t s) {
 }
 
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
+  if (c->capturing) {  // a fresh set for this captured call; the uncaptured set stays as it is
+    for (hipEvent_t e : c->events) c->captured_events.push_back(e);
+    c->events.clear();
+  }
   while (c->events.size() < n) {
     hipEvent_t e;
     FTAR_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -171,6 +179,7 @@ void comm_teardown(ftar_comm* c) {
   if (c->dma_fork) hip_ignore(hipEventDestroy(c->dma_fork));
   if (c->done_ev) hip_ignore(hipEventDestroy(c->done_ev));
   for (auto e : c->events) hip_ignore(hipEventDestroy(e));
+  for (auto e : c->captured_events) hip_ignore(hipEventDestroy(e));
   for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
   if (c->scratch) hip_ignore(hipFree(c->scratch));
   if (c->staging) hip_ignore(hipFree(c->staging));
@@ -229,8 +238,17 @@ namespace {
 // owner's stamped token).  Nothing here returns before map_peers: every rank
 // must reach the exchange; a failed rank publishes an invalid reference and
 // all ranks fail, and retry, together.
+ftar_status_t refuse_growth_under_capture(const ftar_comm* c, const char* what) {
+  if (!c->capturing) return FTAR_SUCCESS;
+  set_error(std::string(what) + " would grow during stream capture: make one call of the same shape before "
+                                "capturing (growth allocates and synchronises)",
+            __FILE__, __LINE__);
+  return FTAR_ERR_UNSUPPORTED;
+}
+
 ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   if (bytes <= c->xbuf_bytes && !c->xpeers.empty()) return FTAR_SUCCESS;
+  FTAR_RETURN_IF(refuse_growth_under_capture(c, "the exchange buffer"));
   Transport* tp = c->tp.get();
   FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));  // the last barrier: no peer still touches the old X
   FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
@@ -649,7 +667,9 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   const bool capturing = cs != hipStreamCaptureStatusNone;
   if (!capturing && c->done_recorded && c->done_stream != stream)
     FTAR_CHECK_HIP(hipStreamWaitEvent(stream, c->done_ev, 0));
+  c->capturing = capturing;
   const ftar_status_t st = allreduce_locked(sendbuf, recvbuf, count, dt, op, topo, c, stream, host);
+  c->capturing = false;
   if (st == FTAR_SUCCESS && !capturing) {
     FTAR_CHECK_HIP(hipEventRecord(c->done_ev, stream));
     c->done_stream = stream;
@@ -692,6 +712,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     // pipelined piece by piece like the p2p path below (which transports with
     // stream-ordered p2p keep using for host buffers even in peer-direct mode)
     const size_t bytes = count * esz;
+    if (bytes > c->staging_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the staging buffer"));
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     FTAR_CHECK_HIP(hipMemcpyAsync(c->staging, host->src, bytes, hipMemcpyHostToDevice, stream));
     FTAR_RETURN_IF(grow_events(c, 5));
@@ -716,6 +737,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   size_t chunk_bytes = c->chunk_bytes;
   if (host) {
     chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
+    if (count * esz > c->staging_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the staging buffer"));
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, count * esz, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     sendbuf = nullptr;
     recvbuf = c->staging;
@@ -734,6 +756,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   const bool skew = host != nullptr;
   std::vector<long> delta(nst, 0);
   const size_t scratch_elems = skew ? per_stage_scratch(plan, &delta) : 2 * plan.scratch_half;
+  if (scratch_elems * esz > c->scratch_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the scratch buffer"));
   FTAR_RETURN_IF(ensure_buffer(&c->scratch, &c->scratch_bytes, scratch_elems * esz, {c->comm_s, c->red_s}));
   const std::vector<std::pair<size_t, size_t>> order = step_order(nst, nchunks, skew);
 
@@ -1165,20 +1188,37 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
                         void* const* streams, bool host) {
   if (!recvbufs || !comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
   std::vector<ftar_status_t> st(nranks, FTAR_SUCCESS);
+  std::vector<std::string> why(nranks);
   std::vector<std::thread> th;
+  // Capturing streams (the caller forked every rank's stream from one capture):
+  // the ranks' threads take turns issuing (Transport::capture_enter), and nobody
+  // synchronises; the caller joins the streams back and ends the capture.
+  bool capturing = false;
+  if (streams && streams[0]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    FTAR_CHECK_HIP(hipSetDevice(comms[0]->device));
+    FTAR_CHECK_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(streams[0]), &cs));
+    capturing = cs != hipStreamCaptureStatusNone;
+  }
   for (int r = 0; r < nranks; ++r)
     th.emplace_back([&, r] {
       hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;
       const void* sb = sendbufs ? sendbufs[r] : nullptr;
+      if (capturing) comms[r]->tp->capture_enter();
       st[r] = host ? ftar_allreduce_host(sb, recvbufs[r], count, dtype, op, topo, comms[r], s)
                    : ftar::allreduce(sb, recvbufs[r], count, dtype, op, topo, comms[r], s);
-      if (st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
+      if (capturing) comms[r]->tp->capture_leave();
+      if (!capturing && st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
           hipStreamSynchronize(s) != hipSuccess)
         st[r] = FTAR_ERR_HIP;
+      if (st[r] != FTAR_SUCCESS) why[r] = ftar::last_error();  // the error text is per thread
     });
   for (auto& t : th) t.join();
   for (int r = 0; r < nranks; ++r)
-    if (st[r] != FTAR_SUCCESS) return st[r];
+    if (st[r] != FTAR_SUCCESS) {
+      ftar::set_error("rank " + std::to_string(r) + ": " + why[r], __FILE__, __LINE__);  // to the caller's thread
+      return st[r];
+    }
   return FTAR_SUCCESS;
 }
 }  // namespace

@@ -184,6 +184,12 @@ class Transport {
   // matching operation (RCCL, local).  false: the host transport, which has
   // no point-to-point transfers (peer-direct forms only).
   virtual bool async_p2p() const { return true; }
+  // Stream capture of an in-process group (ftar_allreduce_group on capturing
+  // streams): between enter and leave this thread issues its HIP calls only
+  // while it holds the group's issue lock (released while it waits for a
+  // peer), so the one capture graph is built by one host thread at a time.
+  virtual void capture_enter() {}
+  virtual void capture_leave() {}
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {

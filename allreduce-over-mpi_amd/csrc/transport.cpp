@@ -406,18 +406,70 @@ std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_
 // ---------------------------------------------------------------------------
 // in-process ranks
 // ---------------------------------------------------------------------------
+namespace {
+thread_local bool t_issue_held = false;  // this thread holds its group's issue lock (capture)
+}
+
 struct LocalHub {
+  // Per-message and barrier events are recycled through a pool, never
+  // destroyed before the hub: a stream capture may still refer to an event
+  // after both sides dropped the message.
   struct Posted {
+    LocalHub* hub = nullptr;
     const void* buf;
     size_t bytes;
     hipEvent_t ready = nullptr;  // sender-side data ready
     hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
     bool taken = false;
     ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
-      if (ready) hip_ignore(hipEventDestroy(ready));
-      if (done) hip_ignore(hipEventDestroy(done));
+      if (ready) hub->give_event(ready);
+      if (done) hub->give_event(done);
     }
   };
+  // During a capture (this thread holds the issue lock) every record gets a
+  // fresh event and used ones retire until the next uncaptured use: an event
+  // re-recorded inside one capture -- on another rank's stream after a peer
+  // waited on it -- made hipStreamEndCapture recurse without end
+  // (tools/capture/, profiles/r02/capture/).
+  ftar_status_t take_event(hipEvent_t* e) {
+    {
+      std::lock_guard<std::mutex> g(pool_mu);
+      if (!t_issue_held && !retired.empty()) {
+        pool.insert(pool.end(), retired.begin(), retired.end());
+        retired.clear();
+      }
+      if (!t_issue_held && !pool.empty()) {
+        *e = pool.back();
+        pool.pop_back();
+        return FTAR_SUCCESS;
+      }
+    }
+    FTAR_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return FTAR_SUCCESS;
+  }
+  void give_event(hipEvent_t e) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    (t_issue_held ? retired : pool).push_back(e);
+  }
+  ~LocalHub() {
+    for (hipEvent_t e : pool) hip_ignore(hipEventDestroy(e));
+    for (hipEvent_t e : retired) hip_ignore(hipEventDestroy(e));
+  }
+  // cv wait that lets the other ranks' threads issue meanwhile when this one
+  // holds the issue lock (lock order: issue before mu)
+  template <class Pred>
+  bool wait(std::unique_lock<std::mutex>& g, Pred pred) {
+    if (!t_issue_held) return cv.wait_for(g, std::chrono::seconds(120), pred);
+    if (pred()) return true;
+    g.unlock();
+    issue.unlock();
+    g.lock();
+    const bool ok = cv.wait_for(g, std::chrono::seconds(120), pred);
+    g.unlock();
+    issue.lock();
+    g.lock();
+    return ok;
+  }
   // every rank's value of one rendezvous (barriers, peer pointers)
   struct Round {
     std::vector<const void*> ptr;
@@ -443,7 +495,7 @@ struct LocalHub {
       arrived = 0;
       ++gen;
       cv.notify_all();
-    } else if (!cv.wait_for(g, std::chrono::seconds(120), [&] { return gen != my_gen; })) {
+    } else if (!wait(g, [&] { return gen != my_gen; })) {
       set_error("local transport: rendezvous timed out", __FILE__, __LINE__);
       return FTAR_ERR_TIMEOUT;
     }
@@ -457,6 +509,9 @@ struct LocalHub {
   std::shared_ptr<Round> pending, done;
   int arrived = 0;
   long gen = 0;
+  std::mutex issue;  // capture of the group: one issuing thread at a time
+  std::mutex pool_mu;
+  std::vector<hipEvent_t> pool, retired;
 };
 
 std::shared_ptr<LocalHub> make_local_hub(int nranks) { return std::make_shared<LocalHub>(nranks); }
@@ -492,13 +547,22 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "local"; }
+  void capture_enter() override {
+    hub_->issue.lock();
+    t_issue_held = true;
+  }
+  void capture_leave() override {
+    t_issue_held = false;
+    hub_->issue.unlock();
+  }
   // each rank's stream waits for every other rank's event recorded at the barrier
   ftar_status_t barrier(hipStream_t s) override {
-    auto e = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [](hipEvent_t* p) {
-      if (*p) hip_ignore(hipEventDestroy(*p));
+    LocalHub* hub = hub_.get();
+    auto e = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [hub](hipEvent_t* p) {
+      if (*p) hub->give_event(*p);
       delete p;
     });
-    FTAR_RETURN_IF(event(e.get()));
+    FTAR_RETURN_IF(hub_->take_event(e.get()));
     FTAR_CHECK_HIP(hipEventRecord(*e, s));
     std::shared_ptr<LocalHub::Round> r;
     FTAR_RETURN_IF(hub_->rendezvous(rank_, nullptr, e, &r));
@@ -517,10 +581,6 @@ class LocalTransport final : public Transport {
   }
 
  private:
-  static ftar_status_t event(hipEvent_t* e) {
-    FTAR_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    return FTAR_SUCCESS;
-  }
 
   ftar_status_t flush() {
     std::vector<Op> ops;
@@ -531,10 +591,11 @@ class LocalTransport final : public Transport {
       if (!o.is_send) continue;
       if (o.peer == rank_ || o.peer < 0 || o.peer >= hub_->nranks) return FTAR_ERR_INVALID_ARG;
       auto p = std::make_shared<LocalHub::Posted>();
+      p->hub = hub_.get();
       p->buf = o.buf;
       p->bytes = o.bytes;
       p->ready = nullptr;
-      FTAR_RETURN_IF(event(&p->ready));
+      FTAR_RETURN_IF(hub_->take_event(&p->ready));
       FTAR_CHECK_HIP(hipEventRecord(p->ready, o.s));
       mine.push_back(p);
       std::lock_guard<std::mutex> g(hub_->mu);
@@ -548,7 +609,7 @@ class LocalTransport final : public Transport {
       {
         std::unique_lock<std::mutex> g(hub_->mu);
         auto& q = hub_->wire[{o.peer, rank_}];
-        if (!hub_->cv.wait_for(g, std::chrono::seconds(120), [&] { return !q.empty(); })) {
+        if (!hub_->wait(g, [&] { return !q.empty(); })) {
           set_error("local transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
           return FTAR_ERR_TIMEOUT;
         }
@@ -562,9 +623,9 @@ class LocalTransport final : public Transport {
       FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
       if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
       hipEvent_t done = nullptr;
-      FTAR_RETURN_IF(event(&done));
+      FTAR_RETURN_IF(hub_->take_event(&done));
       if (hipEventRecord(done, o.s) != hipSuccess) {
-        hip_ignore(hipEventDestroy(done));
+        hub_->give_event(done);
         set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
         return FTAR_ERR_HIP;
       }
@@ -583,7 +644,7 @@ class LocalTransport final : public Transport {
       hipEvent_t done;
       {
         std::unique_lock<std::mutex> g(hub_->mu);
-        if (!hub_->cv.wait_for(g, std::chrono::seconds(120), [&] { return p->taken; })) {
+        if (!hub_->wait(g, [&] { return p->taken; })) {
           set_error("local transport: send to rank " + std::to_string(o.peer) + " never received", __FILE__,
                     __LINE__);
           return FTAR_ERR_TIMEOUT;

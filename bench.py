@@ -453,7 +453,9 @@ def bench_distributed(a):
         link = link_rate_from_probe(probe, world)
         small = torch.zeros(1024, device=dev)
         small_y = torch.empty_like(small)
-        comm.peer_direct, comm.allgather, comm.reduce_scatter = 0, "direct", "direct"
+        comm.peer_tuning()
+        comm.peer_direct = "read" if base_form.startswith("peer-") else 0   # host-bootstrapped: peer forms only
+        comm.allgather, comm.reduce_scatter = "direct", "direct"
         ms_small = timed(lambda: comm.allreduce(small, small_y, 1024, "f32", "sum", topo_=ftar.topo(str(world)),
                                                 stream=stream), 20, 3)
         v = torch.tensor([link or 0.0, ms_small], dtype=torch.float64)

@@ -12,6 +12,8 @@ only the byte mover differs from the multi-GPU RCCL path.
     against the pinned oracle;
   * an RCCL communicator of one rank (the 1-GPU box cannot host more).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -398,3 +400,63 @@ def test_calls_on_alternating_streams_without_sync(host):
                 assert torch.equal(outs[i][r].cpu(), expect[i]), (i, r)
     finally:
         comms.destroy()
+
+
+@pytest.mark.parametrize("P,topo,rs,ag,chunk", [(2, "1", "direct", "direct", 4096), (4, "2,2", "stages", "stages", 4096),
+                                                (4, "4", "direct", "direct", 1 << 20), (3, "1", "stages", "stages", 0)])
+def test_allreduce_group_captures_into_a_hip_graph(tmp_path, P, topo, rs, ag, chunk):
+    """A whole in-process group AllReduce captured into ONE HIP graph (relaxed mode; every rank's stream forked
+    from the capture stream and joined back) and replayed on new inputs: bit-exact against the oracle on every
+    replay.  The ranks' host threads take turns issuing during capture (Transport::capture_enter); scratch and
+    events exist from a warm-up call, so nothing allocates or synchronises under capture.  Runs in a child
+    process (tests/capture_child.py): a runtime abort fails the test instead of ending the run."""
+    import subprocess
+    import sys
+    import ftar_inputs as fi
+    n, replays = 10007, 3
+    out = str(tmp_path / "cap.npz")
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "capture_child.py")
+    p = subprocess.run([sys.executable, child, out, str(P), topo, str(n), str(chunk), rs, ag, str(replays)],
+                       capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0 and "capture ok" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
+    got = np.load(out)
+    for it in range(replays):
+        ins = [fi.fill("f32", 1000 + it, r, n) for r in range(P)]
+        ref = oracle_lib.allreduce(ins, topo)
+        for r in range(P):
+            assert got[f"it{it}_r{r}"].tobytes() == ref[r].tobytes(), (it, r)
+
+
+def test_growth_under_capture_is_refused():
+    """A call whose scratch would have to grow inside a capture returns FTAR_ERR_UNSUPPORTED (growth allocates
+    and synchronises) instead of breaking the capture; the same call outside capture then works."""
+    import torch
+    import ftar
+    g = ftar.Comm.init_local(2)
+    try:
+        n = 1 << 16
+        xs = [torch.ones(n, device="cuda") for _ in range(2)]
+        s0 = torch.cuda.Stream()
+        rank_streams = [torch.cuda.Stream() for _ in range(2)]
+        graph = torch.cuda.CUDAGraph()
+        err = None
+        with torch.cuda.stream(s0):
+            try:
+                with torch.cuda.graph(graph, stream=s0, capture_error_mode="relaxed"):
+                    for s in rank_streams:
+                        s.wait_stream(s0)
+                    try:
+                        g.allreduce(None, xs, n, "f32", "sum", topo_="2", streams=rank_streams)
+                    except ftar.FtarError as e:
+                        err = e
+                    for s in rank_streams:
+                        s0.wait_stream(s)
+            except RuntimeError:
+                pass   # an empty or partial capture may be rejected at its end; the status is what matters
+        torch.cuda.synchronize()
+        assert err is not None and err.status == 2 and "capture" in str(err), err
+        g.allreduce(None, xs, n, "f32", "sum", topo_="2")
+        torch.cuda.synchronize()
+        assert bool((xs[0] == 2).all()) and bool((xs[1] == 2).all())
+    finally:
+        g.destroy()
