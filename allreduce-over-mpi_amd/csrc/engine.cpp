@@ -80,6 +80,7 @@ struct ftar_comm {
   hipEvent_t done_ev = nullptr;
   hipStream_t done_stream = nullptr;
   bool done_recorded = false;
+  int reduce_cus = 0;      // CUs the reduce stream may use (0 = all; ftar_comm_set_reduce_cus)
   bool capturing = false;  // the current call's stream is being captured: no allocation, no host sync
   // events handed to captured calls: each captured call records a fresh set
   // (an event is never re-recorded inside one capture), kept until teardown
@@ -113,6 +114,38 @@ ftar_status_t mark(ftar_comm* c, const std::string& name, hipStream_t s) {
   return FTAR_SUCCESS;
 }
 
+// The reduce stream on `cus` of the device's CUs (0 or >= all: every CU), so
+// the transport's own kernels on the comm stream (RCCL's p2p kernels, the
+// local transport's copies) always find free CUs while a piece's fold runs:
+// the one-shot reduce grids otherwise fill every CU.  The CUs kept are spread
+// evenly over the mask (CU i is kept iff floor((i+1)*cus/N) > floor(i*cus/N)),
+// so every XCD keeps its share whichever way the mask bits map to XCDs.
+// hipExtStreamCreateWithCUMask makes a blocking stream (it synchronises with
+// the legacy NULL stream), the price of the knob.
+ftar_status_t set_reduce_cus(ftar_comm* c, int cus) {
+  int total = 0;
+  FTAR_CHECK_HIP(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, c->device));
+  if (cus <= 0 || cus >= total) cus = 0;
+  if (cus == c->reduce_cus && c->red_s) return FTAR_SUCCESS;
+  hipStream_t fresh = nullptr;
+  if (cus == 0) {
+    FTAR_CHECK_HIP(hipStreamCreateWithFlags(&fresh, hipStreamNonBlocking));
+  } else {
+    std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+    for (int i = 0; i < total; ++i)
+      if ((long)(i + 1) * cus / total > (long)i * cus / total) mask[(size_t)i / 32] |= 1u << (i % 32);
+    FTAR_CHECK_HIP(hipExtStreamCreateWithCUMask(&fresh, (uint32_t)mask.size(), mask.data()));
+  }
+  if (c->red_s) {
+    hip_ignore(hipStreamSynchronize(c->red_s));
+    hip_ignore(hipStreamDestroy(c->red_s));
+  }
+  c->red_s = fresh;
+  c->reduce_cus = cus;
+  trace("rank %d: reduce stream on %d of %d CUs", c->rank, cus ? cus : total, total);
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
   if (c->capturing) {  // a fresh set for this captured call; the uncaptured set stays as it is
     for (hipEvent_t e : c->events) c->captured_events.push_back(e);
@@ -130,7 +163,8 @@ ftar_status_t grow_events(ftar_comm* c, size_t n) {
 ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
-  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
+  if (const char* rc = getenv("FTAR_REDUCE_CUS")) FTAR_RETURN_IF(set_reduce_cus(c, atoi(rc)));
+  else FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
   FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
@@ -447,6 +481,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
       FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
     }
   }
+  FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
   return FTAR_SUCCESS;
@@ -868,6 +903,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
                                  c->rank, c->nranks, c->comm_s));
   }
   if (plan.allgather == FTAR_AG_COLLECTIVE) FTAR_RETURN_IF(mark(c, "collective all-gather", c->comm_s));
+  FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
   FTAR_CHECK_HIP(hipEventRecord(ev[2], c->red_s));
   FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[1], 0));
@@ -1158,6 +1194,19 @@ ftar_status_t ftar_debug_xgmi_probe_cap(ftar_comm_t comm, size_t bytes_per_peer,
   std::lock_guard<std::mutex> g(comm->mu);
   FTAR_CHECK_HIP(hipSetDevice(comm->device));
   return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n, wg_per_peer);
+}
+
+ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  FTAR_CHECK_HIP(hipSetDevice(comm->device));
+  return ftar::set_reduce_cus(comm, cus);
+}
+
+ftar_status_t ftar_comm_get_reduce_cus(ftar_comm_t comm, int* cus) {
+  if (!comm || !cus) return FTAR_ERR_INVALID_ARG;
+  *cus = comm->reduce_cus;
+  return FTAR_SUCCESS;
 }
 
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {

@@ -190,6 +190,13 @@ class Transport {
   // peer), so the one capture graph is built by one host thread at a time.
   virtual void capture_enter() {}
   virtual void capture_leave() {}
+  // Called by every rank before it joins its internal streams back into the
+  // caller's stream.  Under capture the local transport makes the ranks meet
+  // here first: HIP's capture breaks (hipStreamEndCapture recurses without
+  // end, tools/capture/) when a stream waits on an event of a stream that was
+  // already joined back into its parent -- a peer's last wait on my "copied"
+  // event must come before my join.
+  virtual ftar_status_t before_join() { return FTAR_SUCCESS; }
   // The transport library's own collective, for comparison (RCCL only).
   virtual ftar_status_t native_allreduce(const void* send, void* recv, size_t count, ftar_dtype_t dt, ftar_op_t op,
                                          hipStream_t s) {

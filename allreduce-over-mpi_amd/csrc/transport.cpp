@@ -555,6 +555,11 @@ class LocalTransport final : public Transport {
     t_issue_held = false;
     hub_->issue.unlock();
   }
+  ftar_status_t before_join() override {
+    if (!t_issue_held) return FTAR_SUCCESS;
+    std::shared_ptr<LocalHub::Round> r;
+    return hub_->rendezvous(rank_, nullptr, nullptr, &r);
+  }
   // each rank's stream waits for every other rank's event recorded at the barrier
   ftar_status_t barrier(hipStream_t s) override {
     LocalHub* hub = hub_.get();

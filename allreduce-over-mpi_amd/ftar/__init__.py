@@ -137,6 +137,8 @@ def _peer_mode(mode):
     if mode is True or mode is False:
         return int(mode)
     return int(mode)
+_lib.ftar_comm_set_reduce_cus.argtypes = [_vp, _int]
+_lib.ftar_comm_get_reduce_cus.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_comm_set_host_chunk_bytes.argtypes = [_vp, _sz]
 _lib.ftar_comm_get_host_chunk_bytes.argtypes = [_vp, ctypes.POINTER(_sz)]
 _lib.ftar_schedule_json.argtypes = [ctypes.POINTER(Topo), _int, _int, _sz, ctypes.c_char_p, _sz]
@@ -470,6 +472,17 @@ class Comm:
                          "dma_read_all_peers", "dma_write_all_peers"), (round(v, 2) for v in out)))
 
     @property
+    def reduce_cus(self):
+        """CUs the reduce stream may use (0 = all): leaves the rest to the transport's kernels."""
+        v = _int()
+        _check(_lib.ftar_comm_get_reduce_cus(self.handle, ctypes.byref(v)), "reduce_cus")
+        return v.value
+
+    @reduce_cus.setter
+    def reduce_cus(self, n):
+        _check(_lib.ftar_comm_set_reduce_cus(self.handle, int(n)), "reduce_cus")
+
+    @property
     def host_chunk_bytes(self):
         v = _sz()
         _check(_lib.ftar_comm_get_host_chunk_bytes(self.handle, ctypes.byref(v)), "host_chunk_bytes")
@@ -561,6 +574,10 @@ class LocalGroup:
     def set_reduce_scatter(self, mode):
         for c in self.comms:
             c.reduce_scatter = mode
+
+    def set_reduce_cus(self, n):
+        for c in self.comms:
+            c.reduce_cus = n
 
     def register(self, bufs, nbytes):
         """Register one buffer per rank (collective: one host thread per rank); returns the ids."""

@@ -271,6 +271,12 @@ ftar_status_t ftar_allreduce_host(const void* sendbuf, void* recvbuf, size_t cou
 ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
                                         ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo,
                                         ftar_comm_t* comms, int nranks, void* const* streams);
+/* Co-scheduling of the fold with the transport: the reduce stream runs on
+ * `cus` of the device's CUs (spread evenly; 0 = all, the default), so the
+ * comm stream's kernels (RCCL p2p, copies) always find free CUs while a
+ * piece's fold runs (FTAR_REDUCE_CUS at init).  Same bits either way. */
+ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus);
+ftar_status_t ftar_comm_get_reduce_cus(ftar_comm_t comm, int* cus);
 /* Host-mode piece size per block (bytes, rounded to 256 B); 0 = auto: 16 MiB,
  * at least 1/64 of a block (FTAR_HOST_CHUNK_BYTES at init). */
 ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes);

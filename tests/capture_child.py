@@ -6,7 +6,8 @@ the group call captured into one HIP graph -- torch.cuda.graph in relaxed mode o
 stream forked from s0 and joined back -- then replayed on fresh inputs written in place.  Writes every
 replay's per-rank outputs to OUT.npz.
 
-usage: capture_child.py OUT P TOPO N CHUNK RS AG REPLAYS
+usage: capture_child.py OUT P TOPO N CHUNK RS AG REPLAYS   (CAPTURE_SHARED=1: every rank's call on the
+capture stream itself instead of a stream forked per rank)
 """
 import os
 import sys
@@ -110,17 +111,20 @@ def raw_capture(g, xs, ys, n, topo, P):
 def torch_capture(g, xs, ys, n, topo, P):
     import torch
     s0 = torch.cuda.Stream()
-    rank_streams = [torch.cuda.Stream() for _ in range(P)]
+    shared = bool(os.environ.get("CAPTURE_SHARED"))
+    rank_streams = [s0] * P if shared else [torch.cuda.Stream() for _ in range(P)]
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s0):
         with torch.cuda.graph(graph, stream=s0, capture_error_mode="relaxed"):
             step("capture begun")
             for s in rank_streams:
-                s.wait_stream(s0)
+                if s is not s0:
+                    s.wait_stream(s0)
             g.allreduce(xs, ys, n, "f32", "sum", topo_=topo, streams=rank_streams)
             step("group call issued")
             for s in rank_streams:
-                s0.wait_stream(s)
+                if s is not s0:
+                    s0.wait_stream(s)
     step("capture ended")
     torch.cuda.synchronize()
     return graph.replay

@@ -3,7 +3,8 @@
 // without torch: decides whether a crash in hipStreamEndCapture belongs to the
 // HIP runtime torch bundles (7.0) or to ftar.  Replays on fresh inputs and
 // compares every rank's output with an uncaptured call on the same inputs.
-//   group_capture P TOPO N CHUNK  (TOPO "1" = ring, else stage widths)
+//   group_capture P TOPO N CHUNK [shared]  (TOPO "1" = ring, else stage widths;
+//   shared: every rank's call on the capture stream itself, no per-rank fork)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -36,13 +37,14 @@ int main(int argc, char** argv) {
   const char* ts = argc > 2 ? argv[2] : "1";
   const size_t n = argc > 3 ? strtoull(argv[3], nullptr, 0) : 10007;
   const size_t chunk = argc > 4 ? strtoull(argv[4], nullptr, 0) : 0;
+  const bool shared = argc > 5 && !strcmp(argv[5], "shared");
   int dv = 0;
   CK(hipRuntimeGetVersion(&dv));
   fprintf(stderr, "HIP runtime %d\n", dv);
   std::vector<ftar_comm_t> comms(P);
   FT(ftar_comm_init_local(comms.data(), P, nullptr));
   ftar_topo_t topo;
-  FT(ftar_topo_parse(ts, "0", P, &topo));
+  FT(ftar_topo_parse(ts, argc > 6 ? argv[6] : "0", P, &topo));
   for (auto c : comms) {
     if (chunk) FT(ftar_comm_set_chunk_bytes(c, chunk));
   }
@@ -79,14 +81,15 @@ int main(int argc, char** argv) {
   for (int r = 0; r < P; ++r) {
     CK(hipStreamCreateWithFlags(&rs[r], hipStreamNonBlocking));
     CK(hipEventCreateWithFlags(&join[r], hipEventDisableTiming));
-    rsv[r] = rs[r];
+    rsv[r] = shared ? (void*)s0 : (void*)rs[r];
   }
   CK(hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed));
   CK(hipEventRecord(fork, s0));
-  for (auto s : rs) CK(hipStreamWaitEvent(s, fork, 0));
+  if (!shared)
+    for (auto s : rs) CK(hipStreamWaitEvent(s, fork, 0));
   FT(ftar_allreduce_group(xc.data(), yv.data(), n, FTAR_FLOAT32, FTAR_SUM, &topo, comms.data(), P, rsv.data()));
   fprintf(stderr, "group call issued\n");
-  for (int r = 0; r < P; ++r) {
+  for (int r = 0; r < P && !shared; ++r) {
     CK(hipEventRecord(join[r], rs[r]));
     CK(hipStreamWaitEvent(s0, join[r], 0));
   }
