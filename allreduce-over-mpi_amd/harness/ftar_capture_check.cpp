@@ -1,9 +1,9 @@
-// group_capture — the in-process group AllReduce (ftar_allreduce_group on a
+// ftar_capture_check — the in-process group AllReduce (ftar_allreduce_group on a
 // ftar_comm_init_local group) captured into one HIP graph from plain C++,
 // without torch: decides whether a crash in hipStreamEndCapture belongs to the
 // HIP runtime torch bundles (7.0) or to ftar.  Replays on fresh inputs and
 // compares every rank's output with an uncaptured call on the same inputs.
-//   group_capture P TOPO N CHUNK [shared]  (TOPO "1" = ring, else stage widths;
+//   ftar_capture_check P TOPO N CHUNK [shared [LONELY]]  (TOPO "1" = ring, else stage widths;
 //   shared: every rank's call on the capture stream itself, no per-rank fork)
 #include <hip/hip_runtime.h>
 
