@@ -416,6 +416,8 @@ def bench_distributed(a):
         # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
         comm.peer_tuning(nt=tune != "plain", lds=tune != "vec", dma=tune == "dma")
+        # ":cusN": the reduce stream on N CUs, the rest left to RCCL's p2p kernels (DESIGN §4 co-scheduling)
+        comm.reduce_cus = int(tune[3:]) if tune.startswith("cus") else 0
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
         rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
         kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
@@ -667,6 +669,7 @@ def bench_distributed(a):
             chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
+                plan.append((t, default_chunk, "direct:cus224"))
             if form == "stages" and t.ring:
                 chunks = {default_chunk}  # the reference's ring rounds: one point is enough
             plan += [(t, chunk, form) for chunk in sorted(chunks)]
