@@ -318,9 +318,10 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   ftar_topo_t t{};
   if (ft_lonely && *ft_lonely) t.lonely = atoi(ft_lonely);
   if (!ft_topo || !*ft_topo) {
-    if (nranks == 1) {
+    if (nranks == 1) {  // one rank: a copy (mpi_mod.hpp:1739-1746); reported as the ring, like any width 1
       t.nstages = 1;
       t.stages[0] = 1;
+      t.ring = 1;
       *out = t;
       return FTAR_SUCCESS;
     }
