@@ -62,11 +62,15 @@ constexpr bool kNtLoads = true, kNtStores = true;
 // x {f32, bf16} on MI355X (tools/kbench_cold.py variants 40-53,
 // profiles/r02/kbench_cold_prog_shapes.log).  Up to k = 4 deep per-wave
 // queues win (U = 3-4); from k = 5 on, two workgroups per CU of 2-6 waves.
+// Round 2 added one-wave and two-wave workgroups of 1-4 tiles (variants 54-59,
+// profiles/r02/kbench_cold_small_wg.log, kbench_k2_shape_ab.log): for 4-byte
+// k = 2, U = 1 x W = 2 (4 KiB of LDS, up to 16 workgroups per CU) measured
+// +0.6 / +1.3 / +1.8 % over U = 4 x W = 4 in three runs; elsewhere the table held.
 template <class Tr, int K>
-constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 4 : K <= 4 ? 3 : K <= 6 ? 2 : K <= 10 ? 4 : 2)
+constexpr int kLdsTiles = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 1 : K <= 4 ? 3 : K <= 6 ? 2 : K <= 10 ? 4 : 2)
                                                      : (K <= 4 ? 4 : K == 5 ? 2 : K == 6 ? 5 : K <= 10 ? 4 : 2);
 template <class Tr, int K>
-constexpr int kLdsWaves = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 4 : K <= 6 ? 6 : K <= 10 ? 2 : 4)
+constexpr int kLdsWaves = sizeof(typename Tr::S) >= 4 ? (K == 2 ? 2 : K <= 6 ? 6 : K <= 10 ? 2 : 4)
                                                      : (K <= 4 ? 4 : K == 5 ? 5 : K <= 10 ? 2 : 4);
 // LDS per workgroup = W waves x K x U x 1 KiB (<= 160 KiB): k = 16 at U = 2 stages 128 KiB
 
@@ -859,6 +863,13 @@ hipError_t variant_prog(int v, const void* const* srcs, void* dst, size_t nvec, 
     case 51: return launch_lds<Tr, K, 1, 4>(srcs, dst, nvec, s);
     case 52: return launch_lds<Tr, K, 5, 2>(srcs, dst, nvec, s);
     case 53: return launch_lds<Tr, K, 2, 5>(srcs, dst, nvec, s);
+    // small workgroups, many per CU (round 2: tools/kexp/k8_exp.hip found U1 W2 / U2 W1 ahead at k = 2..9)
+    case 54: return launch_lds<Tr, K, 1, 2>(srcs, dst, nvec, s);
+    case 55: return launch_lds<Tr, K, 1, 1>(srcs, dst, nvec, s);
+    case 56: return launch_lds<Tr, K, 2, 1>(srcs, dst, nvec, s);
+    case 57: return launch_lds<Tr, K, 1, 3>(srcs, dst, nvec, s);
+    case 58: return launch_lds<Tr, K, 3, 1>(srcs, dst, nvec, s);
+    case 59: return launch_lds<Tr, K, 4, 1>(srcs, dst, nvec, s);
   }
   return hipErrorInvalidValue;
 }

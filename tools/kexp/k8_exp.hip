@@ -186,7 +186,14 @@ __device__ __forceinline__ void st_pol(f32x4* p, f32x4 v) {
   else asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
 }
 
-template <int K, int U, int W, int SW = 0, bool RO = false, int ST = 0>
+// issue order of the K sources (the fold still reads them 0..K-1 from LDS):
+//   ORD 0 ascending (production); 1 wave parity: odd waves descending; 2 block parity: odd blocks
+//   descending; 3 rotated by blockIdx % K (every source is somebody's first at any moment)
+// BURST: fold every tile as it lands but keep the results in registers and store all U tiles at the end
+template <int K, int R>
+__device__ __forceinline__ constexpr int rot(int j) { return (j + R) % K; }
+
+template <int K, int U, int W, int SW = 0, bool RO = false, int ST = 0, int ORD = 0, bool BURST = false>
 __global__ void __launch_bounds__(W * 64) k_prog(Srcs<K> src, f32x4* dst, size_t nvec) {
   __shared__ f32x4 lds[W][U][K][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -200,15 +207,35 @@ __global__ void __launch_bounds__(W * 64) k_prog(Srcs<K> src, f32x4* dst, size_t
   }
   const size_t base = (b * W + wave) * (U * 64);
   if (base + U * 64 > nvec) return;
+  auto issue = [&](auto rc, auto dc) {
+    constexpr int R = decltype(rc)::value;
+    constexpr bool desc = decltype(dc)::value;
 #pragma unroll
-  for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-      __builtin_amdgcn_global_load_lds(GPTR(src.p[j] + base + u * 64 + lane), LPTR(&lds[wave][u][j][0]), 16, 0, 2);
+      for (int jj = 0; jj < K; ++jj) {
+        const int j = desc ? K - 1 - jj : (jj + R) % K;
+        __builtin_amdgcn_global_load_lds(GPTR(src.p[j] + base + u * 64 + lane), LPTR(&lds[wave][u][j][0]), 16, 0,
+                                         2);
+      }
+  };
+  if constexpr (ORD == 0) {
+    issue(std::integral_constant<int, 0>{}, std::false_type{});
+  } else if constexpr (ORD == 1 || ORD == 2) {
+    const bool odd = ORD == 1 ? (wave & 1) : (blockIdx.x & 1);
+    if (odd) issue(std::integral_constant<int, 0>{}, std::true_type{});
+    else issue(std::integral_constant<int, 0>{}, std::false_type{});
+  } else {
+    const int r = (int)(blockIdx.x % K);
+    [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+      ((r == Rs ? (issue(std::integral_constant<int, Rs>{}, std::false_type{}), 0) : 0), ...);
+    }(std::make_integer_sequence<int, K>{});
+  }
   if constexpr (RO) {  // read-only ceiling: the loads land in LDS, nothing is folded or stored
     wait_vm<0>();
     return;
   }
+  f32x4 res[U];
   auto tile = [&](auto uc) {
     constexpr int u = decltype(uc)::value;
     wait_vm<((U - 1 - u) * K > 63 ? 63 : (U - 1 - u) * K)>();
@@ -216,10 +243,15 @@ __global__ void __launch_bounds__(W * 64) k_prog(Srcs<K> src, f32x4* dst, size_t
     f32x4 a = lds[wave][u][0][lane];
 #pragma unroll
     for (int j = 1; j < K; ++j) a += lds[wave][u][j][lane];
-    st_pol<ST>(dst + base + u * 64 + lane, a);
+    if constexpr (BURST) res[u] = a;
+    else st_pol<ST>(dst + base + u * 64 + lane, a);
   };
   [&]<int... J>(std::integer_sequence<int, J...>) { (tile(std::integral_constant<int, J>{}), ...); }
   (std::make_integer_sequence<int, U>{});
+  if constexpr (BURST) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) st_pol<ST>(dst + base + u * 64 + lane, res[u]);
+  }
 }
 
 struct Var {
@@ -241,11 +273,11 @@ void L_lds(const void* const* p, void* d, size_t nvec, dim3 g, dim3 b, hipStream
   for (int j = 0; j < K; ++j) a.p[j] = static_cast<const f32x4*>(p[j]);
   hipLaunchKernelGGL((k_lds<K, U, W>), g, b, 0, s, a, static_cast<f32x4*>(d), nvec);
 }
-template <int K, int U, int W, int SW = 0, bool RO = false, int ST = 0>
+template <int K, int U, int W, int SW = 0, bool RO = false, int ST = 0, int ORD = 0, bool BURST = false>
 void L_prog(const void* const* p, void* d, size_t nvec, dim3 g, dim3 b, hipStream_t s) {
   Srcs<K> a;
   for (int j = 0; j < K; ++j) a.p[j] = static_cast<const f32x4*>(p[j]);
-  hipLaunchKernelGGL((k_prog<K, U, W, SW, RO, ST>), g, b, 0, s, a, static_cast<f32x4*>(d), nvec);
+  hipLaunchKernelGGL((k_prog<K, U, W, SW, RO, ST, ORD, BURST>), g, b, 0, s, a, static_cast<f32x4*>(d), nvec);
 }
 template <int K, int U, int D, int W>
 void L_ring(const void* const* p, void* d, size_t nvec, dim3 g, dim3 b, hipStream_t s) {
@@ -269,15 +301,15 @@ void L_reg(const void* const* p, void* d, size_t nvec, dim3 g, dim3 b, hipStream
 template <int K>
 std::vector<Var> variants() {
   std::vector<Var> v;
+  v.push_back({"prog U4 W2 (production k8)", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2>});
+  // one-wave workgroups: LDS per WG = U x K KiB, so up to 160 / (U K) workgroups per CU
+  v.push_back({"prog U2 W1", 64, 1 * 2 * 64, 0, L_prog<K, 2, 1>});
+  v.push_back({"prog U1 W1", 64, 1 * 1 * 64, 0, L_prog<K, 1, 1>});
+  v.push_back({"prog U3 W1", 64, 1 * 3 * 64, 0, L_prog<K, 3, 1>});
+  v.push_back({"prog U2 W1 burst", 64, 1 * 2 * 64, 0, L_prog<K, 2, 1, 0, false, 0, 0, true>});
+  v.push_back({"prog U2 W1 plain st", 64, 1 * 2 * 64, 0, L_prog<K, 2, 1, 0, false, 1>});
+  v.push_back({"prog U1 W2", 128, 2 * 1 * 64, 0, L_prog<K, 1, 2>});
   v.push_back({"prog U4 W4", 256, 4 * 4 * 64, 0, L_prog<K, 4, 4>});
-  v.push_back({"prog U4 W2", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2>});
-  v.push_back({"prog U4 W2 plain st", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 0, false, 1>});
-  v.push_back({"prog U4 W2 sc1 st", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 0, false, 2>});
-  v.push_back({"prog U4 W2 sc0sc1 st", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 0, false, 3>});
-  v.push_back({"prog U4 W2 sc1nt st", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 0, false, 4>});
-  v.push_back({"prog U4 W4 plain st", 256, 4 * 4 * 64, 0, L_prog<K, 4, 4, 0, false, 1>});
-  v.push_back({"prog U4 W4 sc1 st", 256, 4 * 4 * 64, 0, L_prog<K, 4, 4, 0, false, 2>});
-  v.push_back({"prog U4 W4 sc1nt st", 256, 4 * 4 * 64, 0, L_prog<K, 4, 4, 0, false, 4>});
   return v;
 }
 
