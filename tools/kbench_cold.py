@@ -29,6 +29,7 @@ ap.add_argument("--variants", default="0,1,2,4,12,13,14,15,16,17,18")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=12)
 ap.add_argument("--dtypes", default="f32")
+ap.add_argument("--inplace", action="store_true", help="dst = source 0 (the in-place fold of an MPI_IN_PLACE AllReduce)")
 ap.add_argument("--shapes", default="", help='nested folds instead of flat variants, e.g. "2,4;4,2;2,2,2": variant 1 '
                                              '= LDS-staged (production), 0 = register kernel (round 1)')
 a = ap.parse_args()
@@ -65,8 +66,9 @@ for r in range(a.rounds):
                         if sh:
                             return lib.ftar_debug_reduce_nested_lds(v, arrs[i % sets], k, bufs[i % sets][K].data_ptr(),
                                                                     m, ftar.DTYPE[d], sh_c, len(sh), stream.cuda_stream)
-                        return lib.ftar_debug_reduce_variant(v, ftar.DTYPE[d], arrs[i % sets], k,
-                                                             bufs[i % sets][K].data_ptr(), m, stream.cuda_stream)
+                        dst = bufs[i % sets][0 if a.inplace else K].data_ptr()
+                        return lib.ftar_debug_reduce_variant(v, ftar.DTYPE[d], arrs[i % sets], k, dst, m,
+                                                             stream.cuda_stream)
                     if launch(0) != 0:  # variant not built for this k (or its LDS would exceed 160 KiB)
                         continue
                     for i in range(1, sets):
@@ -83,5 +85,6 @@ for (d, sets, k, v), ts in sorted(res.items(), key=lambda kv: str(kv[0])):
     med = statistics.median(ts)
     kk = __import__("math").prod(int(w) for w in str(k).split(","))
     byts = (kk + 1) * n * 4
-    print(json.dumps({"dtype": d, "sets": sets, "k": k, "variant": v, "bytes_per_buffer": n * 4, "ms_med": round(med, 4),
+    print(json.dumps({"dtype": d, "sets": sets, "k": k, "variant": v, "inplace": a.inplace, "bytes_per_buffer": n * 4,
+                      "ms_med": round(med, 4),
                       "GBps_med": round(byts / med / 1e6, 1), "GBps_max": round(byts / min(ts) / 1e6, 1)}), flush=True)
