@@ -217,6 +217,29 @@ def bench_single(a):
     print(json.dumps(res), flush=True)
 
 
+def reference_mpi_path(world, n=1 << 24, repeat=5, seconds=120):
+    """The reference's MPI_Allreduce_FT (ring, FT_TOPO=1: its own cost model's choice at P = 2, 4, 8) with
+    `world` MPI ranks on this host, fp32 bucket of n elements (a bounded sample of the 1 GiB workload),
+    built from the unmodified header into oracle/_ref/ref_golden.  None when the binary or MPICH is absent."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
+    mpiexec = "/opt/conda/bin/mpiexec"
+    if not (os.path.exists(ref) and os.path.exists(mpiexec)):
+        return None
+    env = dict(os.environ, FT_TOPO="1")
+    for k in list(env):   # a clean MPI job: not the torchrun rank's rendezvous variables
+        if k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK") or k.startswith("TORCHELASTIC"):
+            env.pop(k)
+    try:
+        p = subprocess.run([mpiexec, "-n", str(world), ref, "arbench", "--n", str(n), "--repeat", str(repeat)],
+                           capture_output=True, text=True, timeout=seconds, env=env)
+        d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+        d["sample"] = (f"{world} MPI ranks on the host, ring (FT_TOPO=1), {n} fp32 per rank, best of {repeat} "
+                       "timed calls (benchmark.cpp timing: Barrier + Wtime, max over ranks)")
+        return d
+    except Exception as e:  # noqa: BLE001  a baseline must not cost the run its line
+        return {"error": str(e)[:200]}
+
+
 def sample_index(n, dev, m=4096):
     """m element indices spread over [0, n), computed in int64.  (A float32 linspace rounds n - 1 up to n
     once n > 2^24 -- at 2^28 elements it indexes one past the end of the bucket.)"""
@@ -824,6 +847,14 @@ def bench_distributed(a):
             state["line"]["host_e2e"] = measure_host()
         except Exception as e:  # noqa: BLE001
             state["line"]["host_e2e"] = {"error": str(e)[:200]}
+
+    # 7. the reference's own CPU/MPI path on this node's host cores, in the same run (north_star): its ring
+    # over MPICH with P ranks (oracle/_ref/ref_golden arbench: mpi_mod.hpp's MPI_Allreduce_FT, 14 OpenMP
+    # threads per rank), on a bounded sample, rank 0 only while the other ranks wait
+    phase("reference cpu/mpi")
+    if rank == 0 and not a.no_cpu_baseline:
+        state["line"]["reference_cpu_mpi"] = reference_mpi_path(world)
+    dist.barrier()
 
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
