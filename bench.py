@@ -200,16 +200,26 @@ def bench_single(a):
         for i in range(2):
             ftar.reduce(pp[i], sd[i].data_ptr(), n, a.dtype, "sum", stream=stream)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for i in range(6):
-            ftar.reduce(pp[i % 2], sd[i % 2].data_ptr(), n, a.dtype, "sum", stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        t = e0.elapsed_time(e1) / 6
+        reps = 6 if a.sweep else 20
+
+        def timed_k(dst_of):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(reps):
+                ftar.reduce(pp[i % 2], dst_of(i % 2), n, a.dtype, "sum", stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / reps
+        t = timed_k(lambda i: sd[i].data_ptr())
         bw = (kk + 1) * n * esz / (t * 1e-3) / 1e9
         sweep[kk] = {"ms": round(t, 4), "GBps": round(bw, 1), "frac": round(bw / HBM_PEAK_GBPS, 4),
                      "traffic": pmc_traffic(f"reduce_k{kk}_{a.dtype}_n{n}")}
+        if kk == 8 and not a.sweep:
+            # in place (destination = source 0): the width-8 tree's fold in an MPI_IN_PLACE AllReduce, whose own
+            # block is operand and result; same bytes, (k+1) x n x 4 (the values grow; timing only)
+            ti = timed_k(lambda i: pp[i][0])
+            bwi = (kk + 1) * n * esz / (ti * 1e-3) / 1e9
+            sweep[kk]["in_place"] = {"ms": round(ti, 4), "GBps": round(bwi, 1), "frac": round(bwi / HBM_PEAK_GBPS, 4)}
         del sw, sd
     res["k_sweep" if a.sweep else "k8"] = sweep if a.sweep else sweep[8]
     if not a.no_cpu_baseline:
@@ -223,8 +233,8 @@ def reference_mpi_path(world, n=1 << 24, repeat=5, seconds=120):
     built from the unmodified header into oracle/_ref/ref_golden.  None when the binary or MPICH is absent."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
     mpiexec = "/opt/conda/bin/mpiexec"
-    if not (os.path.exists(ref) and os.path.exists(mpiexec)):
-        return None
+    if world < 2 or not (os.path.exists(ref) and os.path.exists(mpiexec)):
+        return None   # P = 1 is the reference's memcpy (mpi_mod.hpp:1739), nothing to time
     env = dict(os.environ, FT_TOPO="1")
     for k in list(env):   # a clean MPI job: not the torchrun rank's rendezvous variables
         if k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK") or k.startswith("TORCHELASTIC"):
