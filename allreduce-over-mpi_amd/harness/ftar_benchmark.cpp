@@ -22,7 +22,9 @@
 //                     recycles the handles), one exact integer-valued
 //                     MPI_Allreduce_FT on each;
 //   --comm-threads T  T duplicates driven at once from T threads
-//                     (MPI_THREAD_MULTIPLE), 3 exact calls each.
+//                     (MPI_THREAD_MULTIPLE), 3 exact calls each;
+//   --register-check  MPI_Allreduce_FT_register / _unregister semantics on a
+//                     scratch buffer (needs a GPU: hipHostRegister).
 // --check is two-sided here: the reference only flags results that are too
 // LARGE (benchmark.cpp:201), so NaN/zero results pass there.
 #include <hip/hip_runtime_api.h>
@@ -54,7 +56,7 @@ int main(int argc, char** argv) {
 
   size_t data_len = 35;
   int repeat = 1, warmup = 0, comm_cycle = 0, comm_threads = 0;
-  bool to_file = false, check = false, device = false, do_register = true;
+  bool to_file = false, check = false, device = false, do_register = true, register_check = false;
   std::string tag, comm_type = "flextree", dump;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -74,6 +76,7 @@ int main(int argc, char** argv) {
     else if (a == "--no-register") do_register = false;
     else if (a == "--comm-cycle") comm_cycle = atoi(next().c_str());
     else if (a == "--comm-threads") comm_threads = atoi(next().c_str());
+    else if (a == "--register-check") register_check = true;
     else if (a == "--version") {
       if (rank == 0) printf("ftar_benchmark: %s\n", ftar_version());
       MPI_Finalize();
@@ -257,6 +260,23 @@ int main(int argc, char** argv) {
       }
       lifecycle_bad += bad;
     }
+  }
+  if (register_check) {
+    std::vector<float> buf(1 << 20, 1.0f);
+    const size_t bytes = buf.size() * sizeof(float);
+    int bad_r = 0;
+    bad_r += MPI_Allreduce_FT_register(buf.data(), bytes) != MPI_SUCCESS;
+    bad_r += MPI_Allreduce_FT_register(buf.data() + 16, 1024) != MPI_SUCCESS;  // inside a registration: no-op
+    bad_r += MPI_Allreduce_FT_unregister(buf.data() + 16) != MPI_ERR_ARG;      // not a registration's start
+    bad_r += MPI_Allreduce_FT(MPI_IN_PLACE, buf.data(), (int)buf.size(), MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) !=
+             MPI_SUCCESS;
+    for (size_t i = 0; i < buf.size() && !bad_r; ++i) bad_r += buf[i] != (float)P;
+    bad_r += MPI_Allreduce_FT_unregister(buf.data()) != MPI_SUCCESS;
+    bad_r += MPI_Allreduce_FT_unregister(buf.data()) != MPI_ERR_ARG;           // already gone
+    bad_r += MPI_Allreduce_FT_register(nullptr, 16) != MPI_ERR_ARG;
+    printf("REGISTER_CHECK %d: %s\n", rank, bad_r ? "FAILED" : "ok");
+    fflush(stdout);
+    lifecycle_bad += bad_r;
   }
   int lifecycle_bad_all = 0;
   MPI_Allreduce(&lifecycle_bad, &lifecycle_bad_all, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);

@@ -129,3 +129,16 @@ def test_harness_communicator_lifecycle_two_ranks(tmp_path, extra):
     for r in range(2):
         assert re.search(rf"COMM_CYCLE {r}: cycles=6 handles_reused=\d+ ok", out), out
         assert f"COMM_THREADS {r}: threads=2 ok" in out or "COMM_THREADS skipped" in out, out
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_harness_host_buffer_registration(tmp_path, ranks):
+    """MPI_Allreduce_FT_register / _unregister (RCCL-style user-buffer registration of host buffers): a range
+    inside a registration is already pinned, only a registration's start unregisters, a second unregister and a
+    null buffer are MPI_ERR_ARG, and a call on the registered buffer sums exactly."""
+    rc, out = run(ranks, ["--size", "4096", "--register-check"], tmp_path, {"FT_TOPO": "1"})
+    assert rc == 0, out
+    for r in range(ranks):
+        assert f"REGISTER_CHECK {r}: ok" in out, out
