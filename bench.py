@@ -227,7 +227,7 @@ def bench_single(a):
     print(json.dumps(res), flush=True)
 
 
-def reference_mpi_path(world, n=1 << 24, repeat=5, seconds=120):
+def reference_mpi_path(world, n=1 << 24, repeat=20, seconds=150):
     """The reference's MPI_Allreduce_FT (ring, FT_TOPO=1: its own cost model's choice at P = 2, 4, 8) with
     `world` MPI ranks on this host, fp32 bucket of n elements (a bounded sample of the 1 GiB workload),
     built from the unmodified header into oracle/_ref/ref_golden.  None when the binary or MPICH is absent."""
