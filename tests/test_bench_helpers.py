@@ -72,3 +72,18 @@ def test_roofline_uses_probe_rate_and_falls_back_to_spec():
     assert bench.link_rate_from_probe(None, 8) is None
     assert bench.link_rate_from_probe({"error": "x"}, 8) is None
     assert bench.link_rate_from_probe(probe, 1) is None
+
+
+def test_reference_mpi_path_runs_the_reference_on_the_host():
+    """bench.py's N>1 line item `reference_cpu_mpi`: the reference's own MPI_Allreduce_FT (oracle/_ref/ref_golden
+    arbench, built from the unmodified mpi_mod.hpp) with P MPI ranks on the host, timed like benchmark.cpp.
+    Runs here on CPU (no GPU needed); P = 1 has nothing to time."""
+    import bench
+    ref = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "ref_golden")
+    if not (os.path.exists(ref) and os.path.exists("/opt/conda/bin/mpiexec")):
+        pytest.skip("reference driver or MPICH not built here")
+    assert bench.reference_mpi_path(1) is None
+    d = bench.reference_mpi_path(2, n=1 << 16, repeat=3, seconds=60)
+    assert "error" not in d, d
+    assert d["kind"] == "reference" and d["P"] == 2 and d["n"] == 1 << 16 and d["topo"] == "1"
+    assert 0 < d["min_s"] <= d["first_s"] and d["algbw_GBps_min"] > 0
