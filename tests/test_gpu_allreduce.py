@@ -500,3 +500,31 @@ def test_reduce_stream_cu_mask_same_bits(cus):
             assert outs[r].tobytes() == ref[r].tobytes(), r
     finally:
         g.set_reduce_cus(0)
+
+
+def test_rccl_single_rank_allreduce_captures_into_a_hip_graph():
+    """The product's process model (one rank per process over RCCL) under stream capture: a 1-rank RCCL
+    communicator's ftar_allreduce (the reference's P <= 1 copy, mpi_mod.hpp:1739) captured with torch.cuda.graph
+    and replayed on new inputs; every replay's output is the new input.  (P > 1 over RCCL needs two GPUs.)"""
+    import torch
+    import ftar
+    comm = ftar.Comm.init_rank(1, ftar.get_unique_id(), 0, 0)
+    try:
+        n = 1 << 20
+        x = torch.rand(n, device="cuda")
+        y = torch.empty_like(x)
+        comm.allreduce(x, y, n, "f32", "sum", stream=torch.cuda.current_stream())   # warm-up outside capture
+        torch.cuda.synchronize()
+        s0 = torch.cuda.Stream()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s0):
+            comm.allreduce(x, y, n, "f32", "sum", stream=s0)
+        for it in range(3):
+            x.copy_(torch.full((n,), float(it + 1), device="cuda") + torch.arange(n, device="cuda") * 1e-3)
+            y.zero_()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(y, x), it
+    finally:
+        comm.destroy()
