@@ -700,6 +700,11 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   FTAR_CHECK_HIP(hipStreamIsCapturing(stream, &cs));
   const bool capturing = cs != hipStreamCaptureStatusNone;
+  if (capturing && !c->tp->async_p2p() && c->nranks > 1) {  // its barriers synchronise the host
+    set_error("a host-bootstrapped communicator cannot run under stream capture (its barriers synchronise the host)",
+              __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
   if (!capturing && c->done_recorded && c->done_stream != stream)
     FTAR_CHECK_HIP(hipStreamWaitEvent(stream, c->done_ev, 0));
   c->capturing = capturing;
