@@ -870,6 +870,10 @@ hipError_t variant_prog(int v, const void* const* srcs, void* dst, size_t nvec, 
     case 57: return launch_lds<Tr, K, 1, 3>(srcs, dst, nvec, s);
     case 58: return launch_lds<Tr, K, 3, 1>(srcs, dst, nvec, s);
     case 59: return launch_lds<Tr, K, 4, 1>(srcs, dst, nvec, s);
+    // load cache policy (the aux operand of global_load_lds) at the production shape: 2 = nt (production)
+    case 60: return launch_lds<Tr, K, kLdsTiles<Tr, K>, kLdsWaves<Tr, K>, 1>(srcs, dst, nvec, s);
+    case 61: return launch_lds<Tr, K, kLdsTiles<Tr, K>, kLdsWaves<Tr, K>, 3>(srcs, dst, nvec, s);
+    case 62: return launch_lds<Tr, K, kLdsTiles<Tr, K>, kLdsWaves<Tr, K>, 2>(srcs, dst, nvec, s);
   }
   return hipErrorInvalidValue;
 }
