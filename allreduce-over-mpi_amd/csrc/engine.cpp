@@ -691,8 +691,12 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
 // overwrite scratch the previous call's reduces are still reading.
 ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                         const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr) {
-  if (!c || !recvbuf) return FTAR_ERR_INVALID_ARG;
+  if (!c) return FTAR_ERR_INVALID_ARG;
   if (!dtype_op_supported(dt, op)) return FTAR_ERR_UNSUPPORTED;
+  if (!recvbuf) {  // MPI allows null buffers with count 0 (e.g. an empty pinned tensor): nothing to do
+    if (count) set_error("recvbuf is NULL", __FILE__, __LINE__);
+    return count ? FTAR_ERR_INVALID_ARG : FTAR_SUCCESS;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   // under capture the graph's own dependencies order its replays: an event recorded outside the capture

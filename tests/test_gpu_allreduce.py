@@ -334,8 +334,10 @@ def test_random_soak_all_forms(seed):
         ag = rng.choice(["stages", "direct", "collective"])
         peer = rng.choice([0, 0, "read", "write"])
         nt, lds, dma = rng.random() < 0.7, rng.random() < 0.7, rng.random() < 0.2   # bench.py's peer variants
+        cus = rng.choice([0, 0, 0, 0, 0, 0, 0, 128])   # now and then the reduce stream on half the CUs
         g = group(c["P"])
         g.set_peer_direct(peer)
+        g.set_reduce_cus(cus)
         for cm in g.comms:
             cm.peer_tuning(nt=nt, lds=lds, dma=dma)
         try:
@@ -343,6 +345,7 @@ def test_random_soak_all_forms(seed):
                              c["oop"], chunk_bytes=c["chunk"], ag=ag, rs=rs)
         finally:
             g.set_peer_direct(0)
+            g.set_reduce_cus(0)
             for cm in g.comms:
                 cm.peer_tuning()
         for r in range(c["P"]):
@@ -528,3 +531,25 @@ def test_rccl_single_rank_allreduce_captures_into_a_hip_graph():
             assert torch.equal(y, x), it
     finally:
         comm.destroy()
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_soak_host_buffers(seed):
+    """Seeded random cases through ftar_allreduce_host (the MPI_Allreduce_FT path: H2D, exchange and D2H
+    pipelined and skewed per piece): topologies incl. lonely, dtypes, ops, ragged sizes, random host pieces,
+    both data-movement forms, pinned or pageable, in place or out of place.  Bit-exact vs the oracle.
+    FTAR_SOAK scales the case count (default 40 per seed)."""
+    import os
+    import random
+    import random_cases
+    per = max(1, int(os.environ.get("FTAR_SOAK", "100")) * 2 // 5)
+    rng = random.Random(2000 + seed)
+    for c in random_cases.cases(seed=700 + seed, count=per, max_p=12):
+        form = rng.choice(["stages", "direct"])
+        chunk = rng.choice([0, 256, 4096, 1 << 16])
+        pinned = rng.random() < 0.8
+        outs = run_group_host(c["ins"], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]], 0 if c["op"] == "sum" else 1,
+                              c["oop"], host_chunk=chunk, ag=form, rs=form, pinned=pinned)
+        for r in range(c["P"]):
+            assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"],
+                                                                form, chunk, pinned, r)
