@@ -205,3 +205,38 @@ def test_reduce_captures_into_a_hip_graph(shape):
     ftar.reduce(ptrs, eager.data_ptr(), n, "f32", "sum", stream=torch.cuda.current_stream(), shape=shape)
     torch.cuda.synchronize()
     assert torch.equal(out.view(torch.int32), eager.view(torch.int32))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_soak_reduce(seed):
+    """Seeded random ftar_reduce calls: k = 1..64, every dtype and op, sizes from 0 to 300k elements (block
+    remainders of every kind), element offsets that are co-aligned with the destination (vector path with
+    heads/tails) or not (element-wise path), and in place.  Bit-exact vs the oracle.  FTAR_SOAK scales the
+    case count (default 60 per seed)."""
+    import os
+    import random
+    rng = random.Random(3000 + seed)
+    per = max(1, int(os.environ.get("FTAR_SOAK", "100")) * 3 // 5)
+    for i in range(per):
+        dt = rng.choice(["f32", "f32", "bf16", "f64", "u8", "i8", "u16", "i16", "i32", "i64", "bool"])
+        op = "band" if dt in ("u8", "i8", "u16", "i16", "i32", "i64") and rng.random() < 0.3 else "sum"
+        k = rng.choice([1, 2, 2, 3, 4, 5, 6, 7, 8, 8, 9, 12, 16, 17, 24, 33, 64])
+        n = rng.choice([0, 1, 7, 15, 16, 17, 63, 64, 65, rng.randint(1, 5000), rng.randint(5000, 300_000)])
+        vec = 16 // np.dtype(fi.np_dtype(dt)).itemsize
+        mode = rng.choice(["aligned", "co-aligned", "mixed", "inplace"])
+        if mode == "aligned":
+            offs, out_off = [0] * k, 0
+        elif mode == "co-aligned":   # same address mod 16 everywhere: vector path + head/tail
+            o = rng.randint(0, max(0, vec - 1))
+            offs, out_off = [o] * k, o
+        elif mode == "mixed":        # at least one source off: element-wise path
+            offs, out_off = [rng.randint(0, 7) for _ in range(k)], rng.randint(0, 7)
+        else:
+            offs, out_off = None, 0
+        ins = [fi.fill(dt, 4000 + i, j, n) for j in range(k)]
+        if op == "band":
+            mask = fi.fill(dt, 4001 + i, 0, n)
+            ins = [np.bitwise_or(x, mask) for x in ins]
+        got = run_reduce(ins, dt, op, offsets=offs, out_offset=out_off, inplace=(mode == "inplace"))
+        exp = oracle_lib.reduce(fi.BY_NAME[dt], 0 if op == "sum" else 1, ins, copy_k1=True)
+        assert got.view(np.uint8).tobytes() == exp.view(np.uint8).tobytes(), (seed, i, dt, op, k, n, mode, offs, out_off)
