@@ -240,3 +240,42 @@ def test_random_soak_reduce(seed):
         got = run_reduce(ins, dt, op, offsets=offs, out_offset=out_off, inplace=(mode == "inplace"))
         exp = oracle_lib.reduce(fi.BY_NAME[dt], 0 if op == "sum" else 1, ins, copy_k1=True)
         assert got.view(np.uint8).tobytes() == exp.view(np.uint8).tobytes(), (seed, i, dt, op, k, n, mode, offs, out_off)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_soak_reduce_nested(seed):
+    """Seeded random nested folds (ftar_reduce_nested): random mixed-radix shapes of 2-4 levels and k up to 64
+    (compile-time shapes, runtime codes, runtime-k loops), float dtypes, sizes with every kind of remainder,
+    co-aligned heads/tails or element-wise offsets, in place.  Bit-exact vs per-node oracle reduces.
+    FTAR_SOAK scales the case count (default 40 per seed)."""
+    import os
+    import random
+    import ftar
+    rng = random.Random(5000 + seed)
+    per = max(1, int(os.environ.get("FTAR_SOAK", "100")) * 2 // 5)
+    for i in range(per):
+        while True:
+            shape = [rng.choice([1, 2, 2, 3, 4]) for _ in range(rng.randint(2, 4))]
+            k = int(np.prod(shape))
+            if 2 <= k <= 64:
+                break
+        dt = rng.choice(["f32", "bf16", "f64"])
+        n = rng.choice([1, 15, 16, 17, 255, rng.randint(1, 9000), rng.randint(9000, 200_000)])
+        vec = 16 // np.dtype(fi.np_dtype(dt)).itemsize
+        mode = rng.choice(["aligned", "co-aligned", "mixed", "inplace"])
+        o = rng.randint(0, vec - 1)
+        offs = {"aligned": [0] * k, "co-aligned": [o] * k, "inplace": [o] * k,
+                "mixed": [rng.randint(0, 7) for _ in range(k)]}[mode]
+        ins = [fi.fill(dt, 6000 + i, j, n) for j in range(k)]
+        devs = [to_dev(x, offset_elems=off) for x, off in zip(ins, offs)]
+        if mode == "inplace":
+            dst_t, dst = devs[0]
+            out_off = offs[0]
+        else:
+            out_off = o if mode == "co-aligned" else 0
+            dst_t, dst = filled_dev((n + out_off) * ins[0].itemsize)
+            dst += out_off * ins[0].itemsize
+        ftar.reduce([p for _, p in devs], dst, n, dt, "sum", shape=shape)
+        got = from_dev(dst_t, ins[0].dtype, n, out_off)
+        exp = nested_oracle(fi.BY_NAME[dt], 0, ins, shape)
+        assert got.view(np.uint8).tobytes() == exp.view(np.uint8).tobytes(), (seed, i, shape, dt, n, mode, offs[:4])
