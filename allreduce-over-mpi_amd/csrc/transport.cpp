@@ -44,8 +44,14 @@ bool ipc_size_guard() {
   return on;
 }
 
+// Exportable sizes: at least 2 MiB, because the runtime sub-allocates small
+// hipMalloc requests out of a shared block that hipMemGetAddressRange / IPC
+// export do not see as an allocation of its own (a 4-byte exchange buffer for a
+// one-element bucket failed "named symbol not found"); and round past sizes
+// with bit 31 set where the runtime blocks opening them (ipc_size_guard).
 size_t ipc_safe_size(size_t bytes) {
-  const size_t bit31 = size_t(1) << 31, mask4g = (size_t(1) << 32) - 1;
+  const size_t bit31 = size_t(1) << 31, mask4g = (size_t(1) << 32) - 1, min_bytes = size_t(2) << 20;
+  bytes = std::max(bytes, min_bytes);
   return (ipc_size_guard() && (bytes & bit31)) ? (bytes | mask4g) + 1 : bytes;  // up to the next 4 GiB
 }
 

@@ -142,3 +142,24 @@ def test_harness_host_buffer_registration(tmp_path, ranks):
     assert rc == 0, out
     for r in range(ranks):
         assert f"REGISTER_CHECK {r}: ok" in out, out
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n,device", [(2, "1", 1, False), (3, "3", 1003, False), (4, "2,2", 65541, True),
+                                                 (4, "4", 17, False), (2, "2", (1 << 20) + 3, True),
+                                                 (3, "1", 300_007, False)])
+def test_harness_matches_oracle_on_odd_shapes(tmp_path, ranks, topo, n, device):
+    """MPI_Allreduce_FT (host buffers) / MPI_Allreduce_FT_device across real MPI processes on ragged sizes and
+    3-rank layouts the reference fixtures do not hold: every rank's dumped buffer equals the pinned oracle's
+    result for benchmark.cpp's inputs (data[i] = i * 0.1f on every rank, one call in place)."""
+    import numpy as np
+    import oracle_lib
+    args = ["--size", str(n), "--repeat", "1", "--dump", "out"] + (["--device"] if device else [])
+    rc, out = run(ranks, args, tmp_path, {"FT_TOPO": topo})
+    assert rc == 0, out
+    x = (np.arange(n, dtype=np.float64).astype(np.float32) * np.float32(0.1)).astype(np.float32)
+    ref = oracle_lib.allreduce([x.copy() for _ in range(ranks)], topo)
+    for r in range(ranks):
+        got = np.fromfile(os.path.join(tmp_path, f"out.{r}.bin"), dtype=np.float32)
+        assert got.tobytes() == ref[r].tobytes(), (ranks, topo, n, r)
