@@ -229,3 +229,20 @@ def test_cost_params_set_and_restore(monkeypatch):
         ftar.cost_params(0.0, 0.0, 0.0)
     monkeypatch.delenv("FTAR_COST_LINK_GBPS")
     assert ftar.cost_params() == base and ftar.topo_cost("8", 8, 1 << 30) == c0
+
+
+def test_mpi_dropin_type_and_op_mapping(tmp_path):
+    """libftar_mpi.so's MPI datatype/op mapping against the reference's handle_reduce dispatch list
+    (mpi_mod.hpp:1363-1412), its error classes, and MPI_Allreduce_FT's P <= 1 copy (mpi_mod.hpp:1739) for
+    every type, from a C program under mpiexec -n 1 (no GPU)."""
+    import subprocess
+    lib_dir = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib")
+    if not (os.path.exists(os.path.join(lib_dir, "libftar_mpi.so")) and os.path.exists("/opt/conda/bin/mpiexec")):
+        pytest.skip("libftar_mpi.so or MPICH not available")
+    exe = str(tmp_path / "mpi_dtypes")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-I", "/opt/conda/include",
+                    os.path.join(ROOT, "tests", "c", "mpi_dtypes.c"), "-o", exe, "-L", lib_dir, "-lftar_mpi", "-lftar",
+                    f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath-link,/usr/lib/x86_64-linux-gnu", "-Wl,-rpath-link,/opt/rocm/lib",
+                    "/opt/conda/lib/libmpi.so", "-Wl,-rpath,/opt/conda/lib"], check=True)
+    out = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "1", exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "mpi dtypes ok" in out.stdout, (out.returncode, out.stdout, out.stderr)

@@ -148,7 +148,7 @@ def test_harness_host_buffer_registration(tmp_path, ranks):
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks,topo,n,device", [(2, "1", 1, False), (3, "3", 1003, False), (4, "2,2", 65541, True),
                                                  (4, "4", 17, False), (2, "2", (1 << 20) + 3, True),
-                                                 (3, "1", 300_007, False)])
+                                                 (3, "1", 300_007, False), (2, "1", 0, False), (3, "3", 0, True)])
 def test_harness_matches_oracle_on_odd_shapes(tmp_path, ranks, topo, n, device):
     """MPI_Allreduce_FT (host buffers) / MPI_Allreduce_FT_device across real MPI processes on ragged sizes and
     3-rank layouts the reference fixtures do not hold: every rank's dumped buffer equals the pinned oracle's
