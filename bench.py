@@ -656,7 +656,7 @@ def bench_distributed(a):
                        "chunk_bytes": chunk, "form": form, "xgmi_links": links, "parallelism": f"dp{world}"
                        + (f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), host-bootstrapped "
                           "communicator; not an xGMI measurement)" if a.host_comm and world > torch.cuda.device_count()
-                          else " (host-bootstrapped communicator: RCCL failed to initialise)" if a.host_comm else "")},
+                          else " (host-bootstrapped communicator: RCCL unavailable, see rccl_init_error)" if a.host_comm else "")},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": roof,
             "value_convention": "value = N x bucket bytes / t (aggregate algBW); algbw = bucket / t per rank; "
@@ -675,9 +675,32 @@ def bench_distributed(a):
     else:
         default_topo = ftar.topo_from_env(world, bucket)
     default_chunk = a.chunk_bytes or comm.chunk_bytes
-    fn_default = run_with(default_topo, default_chunk, base_form)
-    ms_default = timed(fn_default, a.steps, a.warmup)
-    ok_default, why_default = check_y(fn_default)
+    err = ""
+    try:
+        if os.environ.get("FTAR_BENCH_FAIL_DEFAULT") and not a.host_comm:   # rehearses the fallback below
+            raise RuntimeError("FTAR_BENCH_FAIL_DEFAULT set")
+        fn_default = run_with(default_topo, default_chunk, base_form)
+        ms_default = timed(fn_default, a.steps, a.warmup)
+        ok_default, why_default = check_y(fn_default)
+    except Exception as e:  # noqa: BLE001
+        if a.host_comm:
+            raise
+        err = str(e)[:200]
+    bad = torch.tensor([1 if err else 0], dtype=torch.int32)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)   # every rank takes the same path
+    if bad.item():
+        # the first RCCL p2p transfers of the run failed: the IPC peer forms over a host-bootstrapped
+        # communicator still move the data over xGMI, so the run keeps a measured line (the broken RCCL
+        # communicator is left alone: destroying it could block)
+        rccl_error = f"default configuration over RCCL failed: {err or 'on another rank'}"
+        sys.stderr.write(f"[bench rank {rank}] {rccl_error}; falling back to the host-bootstrapped peer forms\n")
+        a.host_comm = True
+        comm = ftar.dist.init_host_comm(device=local)
+        base_form = "peer-read"
+        default_chunk = a.chunk_bytes or comm.chunk_bytes
+        fn_default = run_with(default_topo, default_chunk, base_form)
+        ms_default = timed(fn_default, a.steps, a.warmup)
+        ok_default, why_default = check_y(fn_default)
     default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": base_form,
                     "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
                     "check": "ok" if ok_default else f"MISMATCH ({why_default})"}
