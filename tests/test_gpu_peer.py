@@ -336,3 +336,68 @@ def test_peer_tuning_same_bits(mode, nt, lds, dma, P, topo, dt):
     ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt], outofplace=True)
     for r in range(P):
         assert np.array_equal(got[r].view(np.uint8), ref[r].view(np.uint8)), (r, mode, nt, lds)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_soak_registered_subranges(seed):
+    """Seeded random calls on SUB-RANGES of registered buffers (ftar_comm_register over a larger allocation,
+    the call's buffers at the same offset on every rank, as ftar.h requires): the zero-copy peer paths map
+    each peer's pointer as its registration base + my offset.  Random P, one-round topologies (ring, single
+    stage, nested trees), dtypes, ops, ragged sizes, offsets, read/write, in place or out of place, and
+    registrations of the input only, the output only, both, or a decoy registered first.  Bit-exact vs the
+    oracle; a second call on the swapped buffers catches stale mappings."""
+    import random
+
+    import random_cases
+    torch = __import__("torch")
+    rng = random.Random(4000 + seed)
+    for _ in range(int(__import__("os").environ.get("FTAR_SOAK", "100")) // 4):
+        P = rng.choice([2, 3, 4, 6, 8])
+        topo = rng.choice(["1"] + [",".join(map(str, f)) for f in random_cases.factorizations(P)])
+        dt = rng.choice(["f32", "f32", "bf16", "f64", "i32", "u8", "i64"])
+        op = "band" if dt in ("i32", "u8", "i64") and rng.random() < 0.3 else "sum"
+        n = rng.choice([1, P - 1, P + 1, rng.randint(2, 5000), rng.randint(5000, 300_000)])
+        off = rng.choice([0, 1, 3, 64, 1000])
+        tail = rng.choice([0, 1, 4096])
+        mode = rng.choice(["read", "write"])
+        oop = rng.random() < 0.5
+        which = rng.choice(["both", "both", "in", "out", "decoy"])
+        dti, npdt = fi.BY_NAME[dt], fi.np_dtype(dt)
+        esz = np.dtype(npdt).itemsize
+        sd = rng.randint(0, 1 << 30)
+        ins = [fi.fill(dt, sd, r, n) for r in range(P)]
+        ref = oracle_lib.allreduce(ins, topo, 0, dti, 0 if op == "sum" else 1, outofplace=oop)
+        ref2 = oracle_lib.allreduce(ref, topo, 0, dti, 0 if op == "sum" else 1, outofplace=oop)
+        g = group(P)
+        g.set_peer_direct(mode)
+        g.set_allgather("direct")
+        g.set_reduce_scatter("direct")
+        total = (off + n + tail) * esz
+        a = [to_dev(x, pad_elems=tail, offset_elems=off)[0] for x in ins]
+        b = [torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda") for _ in range(P)] if oop else a
+        ids = []
+        try:
+            if which == "decoy":
+                decoy = [torch.empty(4096, dtype=torch.uint8, device="cuda") for _ in range(P)]
+                ids.append(g.register([t.data_ptr() for t in decoy], 4096))
+            if which in ("both", "in", "decoy"):
+                ids.append(g.register([t.data_ptr() for t in a], total))
+            if oop and which in ("both", "out", "decoy"):
+                ids.append(g.register([t.data_ptr() for t in b], total))
+            if not oop and which == "out":
+                ids.append(g.register([t.data_ptr() for t in a], total))
+            pa = [t.data_ptr() + off * esz for t in a]
+            pb = [t.data_ptr() + off * esz for t in b]
+            g.allreduce(pa if oop else None, pb, n, dti, 0 if op == "sum" else 1, topo_=topo)
+            got = [from_dev(t, npdt, n, off) for t in b]
+            for r in range(P):
+                assert got[r].tobytes() == ref[r].tobytes(), (P, topo, dt, op, n, off, mode, oop, which, r)
+            # second call: the result as input (out of place: the buffers swap roles)
+            g.allreduce(pb if oop else None, pa if oop else pb, n, dti, 0 if op == "sum" else 1, topo_=topo)
+            got = [from_dev(t, npdt, n, off) for t in (a if oop else b)]
+            for r in range(P):
+                assert got[r].tobytes() == ref2[r].tobytes(), ("repeat", P, topo, dt, op, n, off, mode, oop, which, r)
+        finally:
+            for i in ids:
+                g.deregister(i)
+            g.set_peer_direct(False)
