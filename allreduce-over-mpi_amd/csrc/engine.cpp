@@ -22,6 +22,7 @@
 #include <cstring>
 #include <cstdio>
 #include <initializer_list>
+#include <cstdint>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -81,6 +82,9 @@ struct ftar_comm {
   hipStream_t done_stream = nullptr;
   bool done_recorded = false;
   int reduce_cus = 0;      // CUs the reduce stream may use (0 = all; ftar_comm_set_reduce_cus)
+  // host buffers on a host-bootstrapped communicator in the read form: piece-pipelined
+  // (peer_allreduce_host); FTAR_HOST_PEER_PIPELINE=0 takes the whole-bucket path instead (A/B)
+  bool host_peer_pipeline = true;
   bool capturing = false;  // the current call's stream is being captured: no allocation, no host sync
   // events handed to captured calls: each captured call records a fresh set
   // (an event is never re-recorded inside one capture), kept until teardown
@@ -173,6 +177,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
     c->peer_direct = m == "write" ? FTAR_PEER_WRITE : m == "read" ? FTAR_PEER_READ
                      : std::max(0, std::min(2, atoi(pd)));
   }
+  if (const char* hp = getenv("FTAR_HOST_PEER_PIPELINE")) c->host_peer_pipeline = atoi(hp) != 0;
   const char* hcb = getenv("FTAR_HOST_CHUNK_BYTES");
   c->host_chunk_bytes = hcb ? strtoull(hcb, nullptr, 0) : kDefaultHostChunkBytes;
   if (c->host_chunk_bytes && c->host_chunk_bytes < 256) c->host_chunk_bytes = 256;
@@ -331,24 +336,26 @@ ftar_status_t ensure_xbuf(ftar_comm* c, size_t bytes) {
   return FTAR_SUCCESS;
 }
 
-// the plan's fold of my block with operand i read from where(i)
+// the plan's fold of my block with operand i read from where(i); elements
+// [lo, lo + len) of the block only (a piece of it, host mode), dst at element lo
 template <class Where>
 ftar_status_t peer_fold(const ReduceItem& r, const Plan& plan, ftar_dtype_t dt, ftar_op_t op, void* dst,
-                        hipStream_t s, bool lds, Where where) {
+                        hipStream_t s, bool lds, Where where, size_t lo = 0, size_t len = SIZE_MAX) {
   std::map<size_t, int> slot_peer;  // scratch slot -> the rank that would have sent it
   for (const Transfer& x : plan.stages[0].recvs) slot_peer[x.off] = x.peer;
   std::vector<const void*> srcs;
   for (const Operand& o : r.srcs) {
     if (o.buf == BUF_SRC) {
-      srcs.push_back(where(-1, o.off));
+      srcs.push_back(where(-1, o.off + lo));
     } else {
       auto it = slot_peer.find(o.off);
       if (it == slot_peer.end()) return FTAR_ERR_INTERNAL;
-      srcs.push_back(where(it->second, r.off));
+      srcs.push_back(where(it->second, r.off + lo));
     }
   }
-  return launch_reduce(srcs.data(), (int)srcs.size(), dst, r.len, dt, op, s, r.round_each, r.shape.data(),
-                       (int)r.shape.size(), lds);
+  if (lo >= r.len) return FTAR_SUCCESS;
+  return launch_reduce(srcs.data(), (int)srcs.size(), dst, std::min(len, r.len - lo), dt, op, s, r.round_each,
+                       r.shape.data(), (int)r.shape.size(), lds);
 }
 }  // namespace
 
@@ -569,6 +576,94 @@ struct HostIO {
   char* dst;
 };
 
+// Host buffers on a communicator without point-to-point transfers (ftar_comm_init_host: the MPI
+// drop-in's `ipc` transport), the read form piece by piece, as the p2p host path pipelines its
+// stages.  Piece k is elements [k*chunk, (k+1)*chunk) of every block.
+//   * every piece goes H2D straight into the exchange buffer X on its own stream, all issued up
+//     front, so the copy engines run ahead (no staging buffer, no copy-in pass);
+//   * once every rank's piece k is in (a barrier), the fold of my block's piece k reads the peers'
+//     copies from their X over xGMI and writes my X in place (the plan's fold: same bits);
+//   * once every rank's fold of piece k is done (the next barrier, which also says piece k+1 is in
+//     everywhere), the other owners' final pieces are pulled into my X at their offsets, and piece
+//     k of the whole bucket goes D2H on its own stream while later pieces come in.
+// A peer reads my X only at its own block (fold) and at my block (gather), and I overwrite my X
+// only at my block (fold, before anyone gathers it) and at the others' blocks (gather, after every
+// fold of that piece), so pieces never conflict.  The barriers synchronise the host: m pieces take
+// m + 2 barriers, the last so that no peer still reads my X when the next call's H2D refills it.
+ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t dt, ftar_op_t op, const Plan& plan,
+                                  ftar_comm* c, hipStream_t stream) {
+  const size_t esz = dtype_size(dt), bytes = count * esz;
+  FTAR_RETURN_IF(ensure_xbuf(c, bytes));
+  Transport* tp = c->tp.get();
+  char* X = static_cast<char*>(c->xbuf);
+  const std::vector<char*>& Xq = c->xpeers;
+  const Stage& rs = plan.stages[0];
+  const Stage& ag = plan.stages[1];
+  const size_t P = (size_t)c->nranks, split = plan.split;
+  // auto pieces: at least 8 per block down to 4 MiB (2 ranks on one GPU, 64 MiB buckets: 4 MiB pieces
+  // 16.5 GB/s vs 12.6 with two 16 MiB pieces; profiles/r02/s4/host_ipc/), else the p2p host path's rule
+  const size_t chunk_bytes = c->host_chunk_bytes
+                                 ? c->host_chunk_bytes
+                                 : std::max(split * esz / 64, std::min<size_t>(16u << 20, std::max<size_t>(4u << 20, split * esz / 8)));
+  const size_t chunk = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63));
+  const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
+  FTAR_RETURN_IF(grow_events(c, 5 + 2 * m));
+  hipEvent_t* ev = c->events.data();
+  auto ev_h = [&](size_t k) { return ev[5 + 2 * k]; };      // piece k is in my X
+  auto ev_g = [&](size_t k) { return ev[5 + 2 * k + 1]; };  // piece k is final in my X
+  auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {  // piece k of every block, clipped
+    for (size_t b = 0; b < P; ++b) {
+      const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
+      if (lo < end) FTAR_RETURN_IF(fn(lo, std::min(chunk, end - lo)));
+    }
+    return FTAR_SUCCESS;
+  };
+  FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
+  for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
+  c->nmarks = 0;
+  FTAR_RETURN_IF(mark(c, "start", c->comm_s));
+  for (size_t k = 0; k < m; ++k) {
+    FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
+      FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
+      return FTAR_SUCCESS;
+    }));
+    FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
+  }
+  FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
+  FTAR_RETURN_IF(tp->barrier(c->comm_s));  // piece 0 is in everywhere
+  FTAR_RETURN_IF(mark(c, "piece 0 in", c->comm_s));
+  std::vector<Segment> segs;
+  for (size_t k = 0; k < m; ++k) {
+    const size_t lo = k * chunk;
+    for (const ReduceItem& r : rs.reduces)
+      FTAR_RETURN_IF(peer_fold(
+          r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
+          [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
+    if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
+    FTAR_RETURN_IF(tp->barrier(c->comm_s));  // piece k folded everywhere (and piece k+1 in)
+    segs.clear();
+    for (const Transfer& x : ag.recvs)
+      if (x.len > lo)
+        segs.push_back({Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
+    if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
+    FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
+    FTAR_RETURN_IF(for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+      FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+      return FTAR_SUCCESS;
+    }));
+  }
+  FTAR_RETURN_IF(mark(c, "pieces folded and gathered", c->comm_s));
+  FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my X after the call
+  FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
+  FTAR_RETURN_IF(tp->before_join());
+  FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[2], c->d2h_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[3], c->h2d_s));
+  for (int i = 1; i <= 3; ++i) FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[i], 0));
+  return FTAR_SUCCESS;
+}
+
 namespace {
 
 // The call's topology (argument, FT_TOPO at init, or the cost model) and its
@@ -749,12 +844,17 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
   }
+  if (host && c->peer_direct == FTAR_PEER_READ && !c->tp->async_p2p() && peer_eligible(plan) &&
+      c->host_peer_pipeline) {
+    // host buffers on a transport without p2p (a communicator bootstrapped over MPI with no RCCL,
+    // ftar_comm_init_host): the read form piece by piece, H2D / exchange / D2H overlapped
+    FTAR_RETURN_IF(grow_events(c, 5));
+    return peer_allreduce_host(*host, count, dt, op, plan, c, stream);
+  }
   if (host && c->peer_direct && !c->tp->async_p2p() && peer_eligible(plan)) {
-    // host buffers on a transport without p2p (a communicator bootstrapped
-    // over MPI with no RCCL, ftar_comm_init_host): the whole bucket in, the
-    // peer exchange in HBM, the whole bucket out -- same plan, same bits, not
-    // pipelined piece by piece like the p2p path below (which transports with
-    // stream-ordered p2p keep using for host buffers even in peer-direct mode)
+    // the write form (or FTAR_HOST_PEER_PIPELINE=0): the whole bucket in, the peer exchange in HBM,
+    // the whole bucket out -- same plan, same bits, not pipelined (transports with stream-ordered
+    // p2p keep using the pipelined p2p path below for host buffers even in peer-direct mode)
     const size_t bytes = count * esz;
     if (bytes > c->staging_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the staging buffer"));
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));

@@ -337,8 +337,9 @@ def bench_distributed(a):
     cannot cost the run its result:
       1. the default configuration (FT_TOPO/--topo, else the cost model; RCCL p2p, direct forms) timed for
          exactly K steps after W warmup -- the headline unless the sweep finds a faster *validated* one;
-      2. the sweep (BASELINE configs[3]: topology x chunk x data-movement form), RCCL forms first, the
-         IPC peer forms (read, write) last, inside a time budget every rank agrees on;
+      2. the sweep (BASELINE configs[3]: topology x chunk x data-movement form) inside a time budget every
+         rank agrees on, in tiers: the default topology's direct RCCL forms, its IPC peer forms (after the
+         xGMI probe), the other topologies' direct/collective forms, the staged rounds, other peer forms;
       3. the sweep's best, re-timed for exactly K steps after W warmup, if it beats the default;
       4. RCCL's own ncclAllReduce on the same bucket (yardstick).
     A watchdog (FTAR_BENCH_BUDGET_S, default 300 s) prints the best line measured so far and ends every
@@ -606,7 +607,8 @@ def bench_distributed(a):
         hx = x.cpu().pin_memory()
         hy = torch.empty_like(hx).pin_memory()
         comm.chunk_bytes = default_chunk
-        comm.peer_direct = 0
+        # RCCL: the p2p host path; a host-bootstrapped communicator: the read form piece by piece
+        comm.peer_direct = "read" if a.host_comm else 0
         comm.allgather = "direct"
         comm.reduce_scatter = "direct"
         comm.peer_tuning()
@@ -707,7 +709,7 @@ def bench_distributed(a):
     state["line"] = make_result(ms_default, default_topo, default_chunk, base_form, ok_default, a.steps, a.warmup,
                                 {"config_selection": "default (sweep not reached)", "default_config": default_info})
 
-    # 2. the sweep: every factorization of P and the ring x chunk sizes x form; RCCL forms first, peer reads last
+    # 2. the sweep: every factorization of P and the ring x chunk sizes x form, in tiers (below)
     phase("sweep")
     sweep = []
     cands = [str(default_topo)] + (["1"] if world > 1 else []) + [",".join(map(str, f)) for f in _factorizations(world)]
@@ -735,7 +737,18 @@ def bench_distributed(a):
                 plan += [(t, default_chunk, f) for f in ("peer-read-reg:plain", "peer-write-reg:plain",
                                                          "peer-read-reg:vec", "peer-write-reg:vec",
                                                          "peer-read-reg:dma", "peer-write-reg:dma", "peer-read:dma")]
-    plan.sort(key=lambda p: p[2].startswith("peer-"))  # stable: every RCCL configuration before any peer one
+    # stable sort into tiers, so the likeliest winners are timed before the budget can run out: the default
+    # topology's direct RCCL forms, then its peer forms (the xGMI probe runs before the first of them), then
+    # the other topologies' direct/collective forms, the reference's staged rounds, the other peer forms
+    def tier(p):
+        t, _, form = p
+        default = str(t) == str(default_topo)
+        if form.startswith("peer-"):
+            return 1 if default else 4
+        if form.startswith("direct"):
+            return 0 if default else 2
+        return 2 if form == "collective" else 3
+    plan.sort(key=tier)
     sweep_t0 = time.time()
     probed = False
     for t, chunk, form in plan:

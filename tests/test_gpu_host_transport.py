@@ -166,3 +166,83 @@ def test_exchange_buffer_past_2gib():
     affected = int(torch.version.hip.split(".")[0]) * 100 + int(torch.version.hip.split(".")[1]) < 702
     if affected and os.environ.get("FTAR_IPC_SIZE_GUARD", "") != "0":
         assert res[0]["reg2g"] != "registered", res
+
+
+HOST_CASES = {2: [("1", "f32"), ("2", "bf16"), ("1", "i32")],
+              3: [("3", "f32"), ("1", "f64")],
+              4: [("2,2", "f32"), ("1", "bf16"), ("4", "u8")]}
+
+
+def _host_worker(rank, world, port, n, q):
+    """Host buffers on the host-bootstrapped communicator (the MPI drop-in's `ipc` transport): the read form
+    piece by piece (peer_allreduce_host), 4 KiB and default pieces, pinned and pageable, in place and out of
+    place, repeated; the write form keeps the whole-bucket path."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ftar
+    import ftar.dist
+    import ftar_inputs as fi
+    out = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        comm = ftar.dist.init_host_comm(device=0)
+        for topo, dt in HOST_CASES[world]:
+            x = fi.fill(dt, 31, rank, n).view(np.uint8)
+            for mode in ("read", "write"):
+                comm.peer_direct = mode
+                for piece in (4096, 0):
+                    comm.host_chunk_bytes = piece
+                    for pinned in (True, False):
+                        for oop in (False, True):
+                            def buf(init):
+                                if pinned:
+                                    b = torch.empty(init.size, dtype=torch.uint8, pin_memory=True).numpy()
+                                    b[:] = init
+                                    return b
+                                return init.copy()
+                            src = buf(x)
+                            dst = buf(np.full_like(x, 0x5A)) if oop else src
+                            for rep in range(2):  # a second call reuses the exchange buffer
+                                if rep and not oop:
+                                    src[:] = x
+                                comm.allreduce_host(src if oop else None, dst, n, dt, "sum", topo_=topo)
+                                torch.cuda.synchronize()
+                            out[(topo, dt, mode, piece, pinned, oop)] = dst.tobytes()
+                            dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001  report, don't hang the parent
+        import traceback
+        out["error"] = traceback.format_exc()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_host_buffers_across_processes(world):
+    import ftar_inputs as fi
+    import oracle_lib
+    n = 70_001
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_host_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    for topo, dt in HOST_CASES[world]:
+        ins = [fi.fill(dt, 31, r, n) for r in range(world)]
+        ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+        keys = [k for k in res[0] if isinstance(k, tuple) and k[:2] == (topo, dt)]
+        assert len(keys) == 16, keys
+        for key in keys:
+            for r in range(world):
+                assert res[r][key] == ref[r].tobytes(), (world, key, r)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: smoke, GPU tests, bench, rocprof. Every GPU step has its
 # own time limit; a fault/abort/timeout (exit >= 124) stops the script there.
-# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host dist1 dist2h dist4h dist2f peer2
+# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host hostipc hosttests dist1 dist2h dist4h dist2f peer2
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -35,6 +35,9 @@ for s in "${steps[@]}"; do
     dist4h) FTAR_BENCH_BUDGET_S=150 run dist4h 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29535 bench.py --host-comm --steps 5 --warmup 2 ;;
     dist2f) FTAR_BENCH_BUDGET_S=150 run dist2f 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29537 bench.py --steps 5 --warmup 2 ;;
     peer2) run peer2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29536 tools/peer_rehearsal.py ;;
+    hostipc) run hostipc2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29538 tools/host_ipc_rate.py --sizes 24,26,28 --pieces 0,4194304 &&
+             run hostipc4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29539 tools/host_ipc_rate.py --sizes 24,26 --topo 4 ;;
+    hosttests) run pytest_host 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_host_transport.py tests/test_harness.py -m gpu ;;
     dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
   esac
