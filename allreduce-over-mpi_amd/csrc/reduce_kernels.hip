@@ -57,6 +57,12 @@ constexpr int kTreeLevels = kMaxFoldLevels;
 constexpr int kUnroll = 2;
 constexpr int kVecThreads = 512;
 constexpr bool kNtLoads = true, kNtStores = true;
+#ifndef KHW_BF16_DEFAULT
+#define KHW_BF16_DEFAULT true
+#endif
+#ifndef KLDS_DEEP_BF16
+#define KLDS_DEEP_BF16 true
+#endif
 // Tiles per wave (U) and waves per workgroup (W) of the LDS-staged kernel by
 // element size and k, from a cold-data sweep of 14 (U, W) shapes x k = 2..16
 // x {f32, bf16} on MI355X (tools/kbench_cold.py variants 40-53,
@@ -134,7 +140,18 @@ struct F64Sum {
   __device__ static VA v_add(VA a, VA b) { return a + b; }
   __device__ static VA v_rnd(VA a) { return a; }
 };
-struct BF16Sum {
+// bf16 rounding of two floats at once.  HW: gfx950's v_cvt_pk_bf16_f32 (RNE); every one of the 2^32
+// float bit patterns converts to the same bf16 bits as bf16_round_bits, NaNs included
+// (ftar_debug_bf16_cvt_check, tests/test_gpu_reduce.py), so the two are interchangeable.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+template <bool HW>
+__device__ __forceinline__ unsigned pack_bf16(float lo, float hi) {
+  if constexpr (HW) return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
+  else return (bf16_round_bits(lo) >> 16) | bf16_round_bits(hi);
+}
+template <bool HW>
+struct BF16SumT {
   using S = unsigned short;
   using SA = float;
   struct VA {
@@ -156,14 +173,17 @@ struct BF16Sum {
     VA b = v_init(x);
     return {a.lo + b.lo, a.hi + b.hi};
   }
-  __device__ static unsigned pack(float lo, float hi) { return (bf16_round_bits(lo) >> 16) | bf16_round_bits(hi); }
+  __device__ static unsigned pack(float lo, float hi) { return pack_bf16<HW>(lo, hi); }
   __device__ static u32x4 v_fin(VA a) {
     return u32x4{pack(a.lo.x, a.lo.y), pack(a.lo.z, a.lo.w), pack(a.hi.x, a.hi.y), pack(a.hi.z, a.hi.w)};
   }
   // nested folds: an inner node's value is stored as bf16 by the staged
   // schedule, so it is rounded before its parent adds it
   __device__ static float rnd(float f) { return __uint_as_float(bf16_round_bits(f)); }
-  __device__ static f32x4 rnd4(f32x4 v) { return f32x4{rnd(v.x), rnd(v.y), rnd(v.z), rnd(v.w)}; }
+  __device__ static f32x4 rnd4(f32x4 v) {
+    if constexpr (HW) return unpack(pack(v.x, v.y), pack(v.z, v.w));
+    else return f32x4{rnd(v.x), rnd(v.y), rnd(v.z), rnd(v.w)};
+  }
   __device__ static SA s_add(SA a, SA b) { return a + b; }
   __device__ static SA s_rnd(SA a) { return rnd(a); }
   __device__ static VA v_add(VA a, VA b) { return {a.lo + b.lo, a.hi + b.hi}; }
@@ -171,14 +191,28 @@ struct BF16Sum {
 };
 // bf16 folded hop by hop: every add rounds to bf16 (the one-round ring fold has
 // to reproduce the staged ring, which rounds once per hop)
-struct BF16SumHop : BF16Sum {
-  __device__ static SA s_comb(SA a, S x) { return rnd(a + bf16_to_f32(x)); }
+template <bool HW>
+struct BF16SumHopT : BF16SumT<HW> {
+  using B = BF16SumT<HW>;
+  using typename B::S;
+  using typename B::SA;
+  using typename B::VA;
+  __device__ static SA s_comb(SA a, S x) { return B::rnd(a + bf16_to_f32(x)); }
   __device__ static VA v_comb(VA a, u32x4 x) {
-    VA b = v_init(x);
+    VA b = B::v_init(x);
     const f32x4 lo = a.lo + b.lo, hi = a.hi + b.hi;
-    return {rnd4(lo), rnd4(hi)};
+    return {B::rnd4(lo), B::rnd4(hi)};
   }
 };
+constexpr bool kHwBf16 = KHW_BF16_DEFAULT;
+// bf16 nested folds of three and four levels (2,2,2), (2,2,2,2) on the LDS-staged kernel: with the
+// integer RNE their per-level rounds made them ALU-bound there (round 2: -2 to -25 %); with
+// v_cvt_pk_bf16_f32 rounding they gain +6.6 % and +3.6 % over the register kernel (cold,
+// profiles/r02/s4/kbench_nested_bf16_lds.log).  Runtime-coded bf16 shapes still lose there (2,3: -11 %,
+// 3,3: -4 %) and keep the register kernel.
+constexpr bool kLdsDeepBf16 = KLDS_DEEP_BF16;
+using BF16Sum = BF16SumT<kHwBf16>;
+using BF16SumHop = BF16SumHopT<kHwBf16>;
 // modular integer sums on packed lanes (SWAR for 8/16-bit lanes)
 template <class S_, unsigned HI>
 struct SwarSum {
@@ -755,18 +789,20 @@ hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const
   // the multi-stage trees of 4, 8 and 16 ranks: compile-time shapes.
   // LDS-staged (production, round 2): cold A/B against the register kernel
   // (profiles/r02/kbench_cold_nested_lds.log): fp32 +4 to +10 % on every
-  // shape; bf16 +4 to +8 % on the two-level shapes, but its per-level rounds
-  // make deeper and runtime-coded folds ALU-bound at the LDS kernel's
-  // occupancy (-2 to -25 %), so those keep the register kernel.
+  // shape; bf16 +4 to +8 % on the two-level shapes, and since bf16 rounds with
+  // v_cvt_pk_bf16_f32 (kLdsDeepBf16) on (2,2,2) and (2,2,2,2) too; its
+  // runtime-coded folds still lose there and keep the register kernel.
   if (lds) {
     if (is({2, 2})) return launch_tree_lds<Tr, 4, StaticShape<2, 2>>(srcs, tc, dst, nvec, h, tail, s);
     if (is({2, 4})) return launch_tree_lds<Tr, 8, StaticShape<2, 4>>(srcs, tc, dst, nvec, h, tail, s);
     if (is({4, 2})) return launch_tree_lds<Tr, 8, StaticShape<4, 2>>(srcs, tc, dst, nvec, h, tail, s);
     if (is({4, 4})) return launch_tree_lds<Tr, 16, StaticShape<4, 4>>(srcs, tc, dst, nvec, h, tail, s);
   }
-  if (lds && sizeof(S) >= 4) {
+  if (lds && (sizeof(S) >= 4 || kLdsDeepBf16)) {
     if (is({2, 2, 2})) return launch_tree_lds<Tr, 8, StaticShape<2, 2, 2>>(srcs, tc, dst, nvec, h, tail, s);
     if (is({2, 2, 2, 2})) return launch_tree_lds<Tr, 16, StaticShape<2, 2, 2, 2>>(srcs, tc, dst, nvec, h, tail, s);
+  }
+  if (lds && sizeof(S) >= 4) {
     switch (k) {  // other shapes: runtime leaf codes
       case 4: return launch_tree_lds<Tr, 4>(srcs, tc, dst, nvec, h, tail, s);
       case 6: return launch_tree_lds<Tr, 6>(srcs, tc, dst, nvec, h, tail, s);
@@ -935,6 +971,16 @@ hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t n
 }
 }  // namespace
 
+hipError_t hop_variant(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
+  switch (k) {
+    case 2: return variant_prog<BF16SumHop, 2>(v, srcs, dst, nvec, s);
+    case 4: return variant_prog<BF16SumHop, 4>(v, srcs, dst, nvec, s);
+    case 8: return variant_prog<BF16SumHop, 8>(v, srcs, dst, nvec, s);
+    case 16: return variant_prog<BF16SumHop, 16>(v, srcs, dst, nvec, s);
+  }
+  return hipErrorInvalidValue;
+}
+
 size_t dtype_size(ftar_dtype_t dt) {
   switch (dt) {
     case FTAR_UINT8: case FTAR_INT8: case FTAR_BOOL: return 1;
@@ -1048,6 +1094,57 @@ extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, int dtype, const
   if (dtype == FTAR_FLOAT32 && count % 4 == 0) e = ftar::variant_tr<ftar::F32Sum>(variant, srcs, k, dst, count / 4, s);
   else if (dtype == FTAR_BFLOAT16 && count % 8 == 0)
     e = ftar::variant_tr<ftar::BF16Sum>(variant, srcs, k, dst, count / 8, s);
+  // 100 + bf16: the ring's hop fold (rounds after every add), production shape (variant 62), k = 2, 4, 8, 16.
+  // (The round-2 A/B of the two bf16 conversions, profiles/r02/s4/kbench_bf16_cvt.log, also built
+  // 200 + bf16 / 300 + bf16 for the flat and hop folds with the integer RNE; dropped to keep build time.)
+  else if (dtype == 100 + FTAR_BFLOAT16 && count % 8 == 0)
+    e = ftar::hop_variant(variant, srcs, k, dst, count / 8, s);
   else return FTAR_ERR_INVALID_ARG;
   return e == hipSuccess ? FTAR_SUCCESS : FTAR_ERR_HIP;
+}
+
+namespace ftar {
+namespace {
+// every float bit pattern u (lo half) and u ^ 0x80000001 (hi half) through both bf16 conversions
+__global__ void __launch_bounds__(256) bf16_cvt_check_kernel(unsigned long long* bad, unsigned* first) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * 256;
+  unsigned long long mine = 0;
+  unsigned first_mine = 0xffffffffu;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < (1ull << 32); i += stride) {
+    const unsigned u = (unsigned)i, v = u ^ 0x80000001u;
+    const float lo = __uint_as_float(u), hi = __uint_as_float(v);
+    if (pack_bf16<true>(lo, hi) != pack_bf16<false>(lo, hi)) {
+      ++mine;
+      first_mine = first_mine < u ? first_mine : u;
+    }
+  }
+  if (mine) {
+    atomicAdd(bad, mine);
+    atomicMin(first, first_mine);
+  }
+}
+}  // namespace
+}  // namespace ftar
+
+// Test hook (not in ftar.h): how many of the 2^32 float bit patterns convert to different bf16 bits
+// through v_cvt_pk_bf16_f32 than through the bit-exact RNE (bf16_round_bits); the first such pattern.
+extern "C" ftar_status_t ftar_debug_bf16_cvt_check(unsigned long long* mismatches, unsigned* first) {
+  if (!mismatches || !first) return FTAR_ERR_INVALID_ARG;
+  unsigned long long* d_bad = nullptr;
+  unsigned* d_first = nullptr;
+  FTAR_CHECK_HIP(hipMalloc(&d_bad, sizeof *d_bad));
+  FTAR_CHECK_HIP(hipMalloc(&d_first, sizeof *d_first));
+  ftar_status_t st = FTAR_SUCCESS;
+  if (hipMemset(d_bad, 0, sizeof *d_bad) != hipSuccess || hipMemset(d_first, 0xff, sizeof *d_first) != hipSuccess)
+    st = FTAR_ERR_HIP;
+  if (st == FTAR_SUCCESS) {
+    hipLaunchKernelGGL(ftar::bf16_cvt_check_kernel, dim3(8192), dim3(256), 0, nullptr, d_bad, d_first);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(mismatches, d_bad, sizeof *d_bad, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(first, d_first, sizeof *d_first, hipMemcpyDeviceToHost) != hipSuccess)
+      st = FTAR_ERR_HIP;
+  }
+  ftar::hip_ignore(hipFree(d_bad));
+  ftar::hip_ignore(hipFree(d_first));
+  return st;
 }

@@ -279,3 +279,91 @@ def test_random_soak_reduce_nested(seed):
         got = from_dev(dst_t, ins[0].dtype, n, out_off)
         exp = nested_oracle(fi.BY_NAME[dt], 0, ins, shape)
         assert got.view(np.uint8).tobytes() == exp.view(np.uint8).tobytes(), (seed, i, shape, dt, n, mode, offs[:4])
+
+
+def test_bf16_hardware_conversion_is_the_rne_for_every_float():
+    """gfx950's v_cvt_pk_bf16_f32 against the bit-exact integer RNE (the oracle's f32_to_bf16_rne) on all
+    2^32 float bit patterns, NaN payloads, infinities and denormals included: the kernels may use either."""
+    import ctypes
+    import ftar
+    lib = ftar.lib()
+    lib.ftar_debug_bf16_cvt_check.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
+    bad, first = ctypes.c_ulonglong(0), ctypes.c_uint(0)
+    assert lib.ftar_debug_bf16_cvt_check(ctypes.byref(bad), ctypes.byref(first)) == 0
+    assert bad.value == 0, f"{bad.value} patterns differ, first 0x{first.value:08x}"
+
+
+def assert_bits_equal_nan_as_nan(got, exp, dt):
+    """Bit-exact wherever the expected value is a number (infinities and signed zeros included); NaN exactly
+    where it is NaN.  Which NaN a sum returns when NaNs meet (its sign and payload, and the sign of the
+    default NaN of inf - inf) is left open by IEEE 754 and by the LLVM IR the kernels compile from (fadd is
+    commutative there, so operand order is the compiler's), and the reference's own NaN bits depend on its
+    x86 compiler's operand order in the same way: that is outside the bit-exact contract."""
+    if dt == "bf16":
+        g, e = fi.bf16_bits_to_f32(got.view(np.uint16)), fi.bf16_bits_to_f32(exp.view(np.uint16))
+        gb, eb = got.view(np.uint16), exp.view(np.uint16)
+    else:
+        g, e = got.view(np.float32), exp.view(np.float32)
+        gb, eb = got.view(np.uint32), exp.view(np.uint32)
+    nan = np.isnan(e)
+    np.testing.assert_array_equal(np.isnan(g), nan)
+    np.testing.assert_array_equal(gb[~nan], eb[~nan])
+    assert nan.any()  # the inputs do exercise NaN
+
+
+def _bf16_specials(seed, j, n):
+    """bf16 inputs with NaNs (both signs, several payloads), infinities, bf16 denormals, values whose sum
+    overflows and ties that round to even, mixed into random values"""
+    x = fi.fill("bf16", seed, j, n).copy()
+    specials = np.array([0x7FC0, 0xFFC0, 0x7F81, 0xFF81, 0x7FBF, 0x7F80, 0xFF80, 0x0001, 0x8001, 0x007F,
+                         0x7F7F, 0xFF7F, 0x0000, 0x8000, 0x3F80, 0x3B80], dtype=np.uint16)
+    rng = np.random.default_rng(seed * 31 + j)
+    idx = rng.choice(n, size=n // 8, replace=False)
+    x.view(np.uint16)[idx] = specials[rng.integers(0, specials.size, idx.size)]
+    return x
+
+
+def _f32_specials(seed, j, n):
+    x = fi.fill("f32", seed, j, n).copy()
+    specials = np.array([0x7FC00000, 0xFFC00000, 0x7F800001, 0xFF812345, 0x7FBFFFFF, 0x7F800000, 0xFF800000,
+                         0x00000001, 0x80000001, 0x7F7FFFFF, 0xFF7FFFFF, 0x00000000, 0x80000000], dtype=np.uint32)
+    rng = np.random.default_rng(seed * 37 + j)
+    idx = rng.choice(n, size=n // 8, replace=False)
+    x.view(np.uint32)[idx] = specials[rng.integers(0, specials.size, idx.size)]
+    return x
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("k", [2, 3, 8, 16])
+def test_reduce_special_values_vs_oracle(k, dt):
+    n = 100_003
+    ins = [(_bf16_specials if dt == "bf16" else _f32_specials)(7, j, n) for j in range(k)]
+    got = run_reduce(ins, dt, "sum")
+    exp = oracle_lib.reduce(fi.BY_NAME[dt], 0, ins)
+    assert_bits_equal_nan_as_nan(got, exp, dt)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("form", ["direct", "stages"])
+@pytest.mark.parametrize("topo", ["1", "2,2", "4"])
+def test_allreduce_special_values_vs_oracle(topo, form, dt):
+    """NaNs (both signs, several payloads), infinities, denormals and overflow through the one-round and the
+    staged forms, 4 in-process ranks: bit-exact except which NaN comes out where NaNs meet
+    (assert_bits_equal_nan_as_nan)"""
+    import ftar
+    import torch
+    P, n = 4, 50_001
+    xs = [(_bf16_specials if dt == "bf16" else _f32_specials)(11, r, n) for r in range(P)]
+    view = np.int16 if dt == "bf16" else np.int32
+    group = ftar.Comm.init_local(P)
+    try:
+        group.set_reduce_scatter(form)
+        group.set_allgather(form)
+        bufs = [torch.from_numpy(x.view(view).copy()).cuda() for x in xs]
+        group.allreduce(None, bufs, n, dt, "sum", topo_=topo)
+        torch.cuda.synchronize()
+        ref = oracle_lib.allreduce(xs, topo, dtype=fi.BY_NAME[dt])
+        for r in range(P):
+            assert_bits_equal_nan_as_nan(bufs[r].cpu().numpy().view(view), ref[r].view(view), dt)
+    finally:
+        group.destroy()

@@ -50,7 +50,9 @@ variants = [int(v) for v in a.variants.split(",")]
 S = max(setss)
 K = max(ks)
 bufs = [[torch.rand(n, device="cuda") for _ in range(K + 1)] for _ in range(S)]  # K sources + dst per set
-ESZ = {"f32": 4, "bf16": 2}
+ESZ = {"f32": 4, "bf16": 2, "bf16hop": 2}
+# dtype code of ftar_debug_reduce_variant for the ring's bf16 hop fold (rounds after every add; variant 62)
+CODE = {"bf16hop": ftar.DTYPE["bf16"] + 100}
 stream = torch.cuda.current_stream()
 res = {}
 for r in range(a.rounds):
@@ -67,7 +69,7 @@ for r in range(a.rounds):
                             return lib.ftar_debug_reduce_nested_lds(v, arrs[i % sets], k, bufs[i % sets][K].data_ptr(),
                                                                     m, ftar.DTYPE[d], sh_c, len(sh), stream.cuda_stream)
                         dst = bufs[i % sets][0 if a.inplace else K].data_ptr()
-                        return lib.ftar_debug_reduce_variant(v, ftar.DTYPE[d], arrs[i % sets], k, dst, m,
+                        return lib.ftar_debug_reduce_variant(v, CODE.get(d) or ftar.DTYPE[d], arrs[i % sets], k, dst, m,
                                                              stream.cuda_stream)
                     if launch(0) != 0:  # variant not built for this k (or its LDS would exceed 160 KiB)
                         continue
