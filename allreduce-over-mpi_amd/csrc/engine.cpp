@@ -102,6 +102,7 @@ constexpr size_t kDefaultChunkBytes = 16u << 20;
 // every block each).  16 MiB was the best or near-best size in every sweep
 // (profiles/r01/host/): 8 pieces per block at P = 8 x 1 GiB.
 constexpr size_t kDefaultHostChunkBytes = 0;
+constexpr size_t kMaxHostPeerPieces = 1024;  // peer_allreduce_host: pieces per call (a host barrier each)
 size_t auto_host_chunk(size_t split_bytes) { return std::max<size_t>(16u << 20, split_bytes / 64); }
 
 // phase timing: one timing event per boundary, on the stream that reaches it
@@ -605,7 +606,9 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   const size_t chunk_bytes = c->host_chunk_bytes
                                  ? c->host_chunk_bytes
                                  : std::max(split * esz / 64, std::min<size_t>(16u << 20, std::max<size_t>(4u << 20, split * esz / 8)));
-  const size_t chunk = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63));
+  // every piece costs a host barrier and two events: at most kMaxHostPeerPieces pieces per call
+  const size_t floor_elems = (split + kMaxHostPeerPieces - 1) / kMaxHostPeerPieces;
+  const size_t chunk = std::max<size_t>({64, (chunk_bytes / esz) & ~size_t(63), (floor_elems + 63) & ~size_t(63)});
   const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
   FTAR_RETURN_IF(grow_events(c, 5 + 2 * m));
   hipEvent_t* ev = c->events.data();
