@@ -214,6 +214,17 @@ def _host_worker(rank, world, port, n, q):
                                 torch.cuda.synchronize()
                             out[(topo, dt, mode, piece, pinned, oop)] = dst.tobytes()
                             dist.barrier()
+            # 256-B pieces on a bucket that would need more than 1024 of them: the read form's
+            # piece count is capped (every piece costs a host barrier), same bits
+            if world == 2:
+                comm.peer_direct = "read"
+                comm.host_chunk_bytes = 256
+                big = fi.fill(dt, 33, rank, 600_001).view(np.uint8)
+                y = np.full_like(big, 0x5A)
+                comm.allreduce_host(big, y, 600_001, dt, "sum", topo_=topo)
+                torch.cuda.synchronize()
+                out[("cap", topo, dt)] = y.tobytes()
+                dist.barrier()
         comm.destroy()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001  report, don't hang the parent
@@ -246,3 +257,8 @@ def test_host_buffers_across_processes(world):
         for key in keys:
             for r in range(world):
                 assert res[r][key] == ref[r].tobytes(), (world, key, r)
+        if world == 2:
+            big_ref = oracle_lib.allreduce([fi.fill(dt, 33, r, 600_001) for r in range(world)], topo,
+                                           dtype=fi.BY_NAME[dt])
+            for r in range(world):
+                assert res[r][("cap", topo, dt)] == big_ref[r].tobytes(), (topo, dt, r)
