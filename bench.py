@@ -612,6 +612,7 @@ def bench_distributed(a):
         comm.allgather = "direct"
         comm.reduce_scatter = "direct"
         comm.peer_tuning()
+        comm.reduce_cus = 0   # the sweep's last configuration may have left the reduce stream on a CU subset
 
         def fnh():
             comm.allreduce_host(hx, hy, n, a.dtype, "sum", topo_=default_topo, stream=stream)
