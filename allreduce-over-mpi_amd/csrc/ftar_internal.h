@@ -122,7 +122,7 @@ ftar_status_t build_plan(const Topology& t, int nranks, int rank, size_t count, 
 ftar_status_t check_world(const Topology& t, int nranks, size_t count, Form form);
 
 // ---------------------------------------------------------------------------
-// reduce kernels (reduce_kernels.hip)
+// reduce kernels (reduce_impl.h; dispatch in reduce_kernels.hip)
 // ---------------------------------------------------------------------------
 // srcs: host array of k device pointers. k == 1 copies.
 // round_each: bf16 sums round to bf16 after every add (no effect on other dtypes).

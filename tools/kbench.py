@@ -3,7 +3,7 @@
 
     python tools/kbench.py [--elements N] [--rounds R] [--variants 0,1,..] [--ks 2,4,8] [--dtypes f32,bf16]
 Each variant = (vectors/lane, nt loads, nt stores, workgroup size, grid cap),
-see ftar_debug_reduce_variant in csrc/reduce_kernels.hip.  Prints median/min
+see ftar_debug_reduce_variant in csrc/reduce_variants.hip.  Prints median/min
 kernel time and GB/s ((k+1)*n*esz bytes) per (dtype, k, variant), plus a
 device-to-device copy as a reference point.  Every variant's output is
 compared with variant 0's.
