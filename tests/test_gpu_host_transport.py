@@ -262,3 +262,83 @@ def test_host_buffers_across_processes(world):
                                            dtype=fi.BY_NAME[dt])
             for r in range(world):
                 assert res[r][("cap", topo, dt)] == big_ref[r].tobytes(), (topo, dt, r)
+
+
+SOAK_TOPOS = {2: ["1", "2"], 3: ["1", "3"], 4: ["1", "4", "2,2"]}
+SOAK_DTYPES = ["f32", "bf16", "f64", "i32", "u8", "i16"]
+
+
+def _soak_cases(world, count, seed):
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(count):
+        n = int(rng.choice([0, 1, 3, world - 1, world + 1, int(rng.integers(2, 5000)), int(rng.integers(5000, 300_000))]))
+        cases.append((i, n, str(rng.choice(SOAK_DTYPES)), str(rng.choice(SOAK_TOPOS[world])),
+                      int(rng.choice([256, 4096, 65536, 0])), bool(rng.integers(0, 2)), bool(rng.integers(0, 2))))
+    return cases
+
+
+def _soak_worker(rank, world, port, cases, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ftar
+    import ftar.dist
+    import ftar_inputs as fi
+    out = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        comm = ftar.dist.init_host_comm(device=0)
+        comm.peer_direct = "read"
+        for i, n, dt, topo, piece, pinned, oop in cases:
+            x = fi.fill(dt, 500 + i, rank, n).view(np.uint8)
+
+            def buf(init):
+                if pinned and init.size:
+                    b = torch.empty(init.size, dtype=torch.uint8, pin_memory=True).numpy()
+                    b[:] = init
+                    return b
+                return init.copy()
+            src = buf(x)
+            dst = buf(np.full_like(x, 0x5A)) if oop else src
+            comm.host_chunk_bytes = piece
+            comm.allreduce_host(src if oop else None, dst if dst.size else None, n, dt, "sum", topo_=topo)
+            torch.cuda.synchronize()
+            out[i] = dst.tobytes()
+        dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        out["error"] = traceback.format_exc()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_host_buffers_random_soak(world):
+    """The piece-pipelined host path on the host-bootstrapped communicator: 40 random cases per world size
+    (empty and ragged buckets, six dtypes, ring and one-round trees, 256 B to auto pieces, pinned and
+    pageable, in and out of place), bit-exact against the oracle"""
+    import ftar_inputs as fi
+    import oracle_lib
+    cases = _soak_cases(world, 40, 1000 + world)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_soak_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+    for i, n, dt, topo, piece, pinned, oop in cases:
+        ins = [fi.fill(dt, 500 + i, r, n) for r in range(world)]
+        ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
+        for r in range(world):
+            assert res[r][i] == ref[r].tobytes(), (world, i, n, dt, topo, piece, pinned, oop, r)
