@@ -577,6 +577,19 @@ struct HostIO {
   char* dst;
 };
 
+// Elements per piece of peer_allreduce_host.  Auto: at least 8 pieces per block down to 4 MiB (2 ranks
+// on one GPU, 64 MiB buckets: 4 MiB pieces 16.5 GB/s vs 12.6 with two 16 MiB pieces;
+// profiles/r02/s4/host_ipc/), else the p2p host path's rule; every piece costs a host barrier and two
+// events, so at most kMaxHostPeerPieces pieces per call.
+size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
+  const size_t chunk_bytes =
+      c->host_chunk_bytes
+          ? c->host_chunk_bytes
+          : std::max(split * esz / 64, std::min<size_t>(16u << 20, std::max<size_t>(4u << 20, split * esz / 8)));
+  const size_t floor_elems = (split + kMaxHostPeerPieces - 1) / kMaxHostPeerPieces;
+  return std::max<size_t>({64, (chunk_bytes / esz) & ~size_t(63), (floor_elems + 63) & ~size_t(63)});
+}
+
 // Host buffers on a communicator without point-to-point transfers (ftar_comm_init_host: the MPI
 // drop-in's `ipc` transport), the read form piece by piece, as the p2p host path pipelines its
 // stages.  Piece k is elements [k*chunk, (k+1)*chunk) of every block.
@@ -601,14 +614,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   const Stage& rs = plan.stages[0];
   const Stage& ag = plan.stages[1];
   const size_t P = (size_t)c->nranks, split = plan.split;
-  // auto pieces: at least 8 per block down to 4 MiB (2 ranks on one GPU, 64 MiB buckets: 4 MiB pieces
-  // 16.5 GB/s vs 12.6 with two 16 MiB pieces; profiles/r02/s4/host_ipc/), else the p2p host path's rule
-  const size_t chunk_bytes = c->host_chunk_bytes
-                                 ? c->host_chunk_bytes
-                                 : std::max(split * esz / 64, std::min<size_t>(16u << 20, std::max<size_t>(4u << 20, split * esz / 8)));
-  // every piece costs a host barrier and two events: at most kMaxHostPeerPieces pieces per call
-  const size_t floor_elems = (split + kMaxHostPeerPieces - 1) / kMaxHostPeerPieces;
-  const size_t chunk = std::max<size_t>({64, (chunk_bytes / esz) & ~size_t(63), (floor_elems + 63) & ~size_t(63)});
+  const size_t chunk = host_peer_piece(c, split, esz);
   const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
   FTAR_RETURN_IF(grow_events(c, 5 + 2 * m));
   hipEvent_t* ev = c->events.data();
@@ -848,9 +854,11 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
   }
   if (host && c->peer_direct == FTAR_PEER_READ && !c->tp->async_p2p() && peer_eligible(plan) &&
-      c->host_peer_pipeline) {
+      c->host_peer_pipeline && host_peer_piece(c, plan.split, esz) < plan.split) {
     // host buffers on a transport without p2p (a communicator bootstrapped over MPI with no RCCL,
-    // ftar_comm_init_host): the read form piece by piece, H2D / exchange / D2H overlapped
+    // ftar_comm_init_host): the read form piece by piece, H2D / exchange / D2H overlapped.  A bucket
+    // of one piece per block gains nothing from it and takes the whole-bucket path below, whose one
+    // copy each way beats one per block (C1 through the MPI harness: 0.453 vs 0.487 ms)
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce_host(*host, count, dt, op, plan, c, stream);
   }

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--pieces", default="0", help="host piece bytes for the pipelined path (0 = auto)")
     ap.add_argument("--topo", default="1")
+    ap.add_argument("--inplace", action="store_true", help="MPI_IN_PLACE, as the reference harness calls it")
+    ap.add_argument("--register", action="store_true", help="hipHostRegister'ed numpy buffers (the MPI drop-in's "
+                    "MPI_Allreduce_FT_register) instead of torch pinned allocations")
     a = ap.parse_args()
 
     import numpy as np
@@ -44,9 +47,17 @@ def main():
         comms[name].peer_direct = "read"
     for tok in a.sizes.split(","):
         n = 1 << int(tok)
-        x = torch.empty(n, dtype=torch.float32, pin_memory=True).numpy()
+        if a.register:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            x, y = np.empty(n, np.float32), np.empty(n, np.float32)
+            for b in (x, y):
+                rc = hip.hipHostRegister(ctypes.c_void_p(b.ctypes.data), ctypes.c_size_t(b.nbytes), ctypes.c_uint(0))
+                assert rc == 0, rc
+        else:
+            x = torch.empty(n, dtype=torch.float32, pin_memory=True).numpy()
+            y = torch.empty(n, dtype=torch.float32, pin_memory=True).numpy()
         x[:] = np.float32(rank + 1)
-        y = torch.empty(n, dtype=torch.float32, pin_memory=True).numpy()
         want = np.float32(world * (world + 1) // 2)
         configs = [("whole", 0)] + [("pipelined", int(p)) for p in a.pieces.split(",")]
         times = {c: [] for c in configs}
@@ -56,10 +67,16 @@ def main():
                 c.host_chunk_bytes = piece
                 dist.barrier()
                 t0 = time.perf_counter()
-                c.allreduce_host(x, y, n, "f32", "sum", topo_=a.topo)
+                if a.inplace:
+                    c.allreduce_host(None, x, n, "f32", "sum", topo_=a.topo)
+                else:
+                    c.allreduce_host(x, y, n, "f32", "sum", topo_=a.topo)
                 torch.cuda.synchronize()
                 t = time.perf_counter() - t0
-                ok = bool((y[:: max(1, n // 4096)] == want).all() and y[-1] == want)
+                out = x if a.inplace else y
+                ok = bool((out[:: max(1, n // 4096)] == want).all() and out[-1] == want)
+                if a.inplace:
+                    x[:] = np.float32(rank + 1)
                 tt = torch.tensor([t, 0.0 if ok else 1.0], dtype=torch.float64)
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                 if tt[1] > 0:
