@@ -204,6 +204,11 @@ __global__ void __launch_bounds__(W * 64) k_prog(Srcs<K> src, f32x4* dst, size_t
   } else if constexpr (SW == 2) {  // XCD-chunked: runs of 8 consecutive tiles per XCD
     const size_t g = b / 64, r = b % 64;
     if ((g + 1) * 64 <= gridDim.x) b = g * 64 + (r % 8) * 8 + r / 8;
+  } else if constexpr (SW >= 3) {  // R regions interleaved: block b works in region b % R, so the
+    // workgroups resident at one time stream from R distant places of every buffer (R x the streams)
+    constexpr size_t R = SW == 3 ? 2 : SW == 4 ? 4 : 8;
+    const size_t per = gridDim.x / R;
+    if (b < per * R) b = (b % R) * per + b / R;
   }
   const size_t base = (b * W + wave) * (U * 64);
   if (base + U * 64 > nvec) return;
@@ -302,6 +307,13 @@ template <int K>
 std::vector<Var> variants() {
   std::vector<Var> v;
   v.push_back({"prog U4 W2 (production k8)", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2>});
+  v.push_back({"prog U4 W2, 2 regions", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 3>});
+  v.push_back({"prog U4 W2, 4 regions", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 4>});
+  v.push_back({"prog U4 W2, 8 regions", 128, 2 * 4 * 64, 0, L_prog<K, 4, 2, 5>});
+  v.push_back({"prog U1 W2 (production k2)", 128, 2 * 1 * 64, 0, L_prog<K, 1, 2>});
+  v.push_back({"prog U1 W2, 2 regions", 128, 2 * 1 * 64, 0, L_prog<K, 1, 2, 3>});
+  v.push_back({"prog U1 W2, 4 regions", 128, 2 * 1 * 64, 0, L_prog<K, 1, 2, 4>});
+  v.push_back({"prog U1 W2, 8 regions", 128, 2 * 1 * 64, 0, L_prog<K, 1, 2, 5>});
   // one-wave workgroups: LDS per WG = U x K KiB, so up to 160 / (U K) workgroups per CU
   v.push_back({"prog U2 W1", 64, 1 * 2 * 64, 0, L_prog<K, 2, 1>});
   v.push_back({"prog U1 W1", 64, 1 * 1 * 64, 0, L_prog<K, 1, 1>});
