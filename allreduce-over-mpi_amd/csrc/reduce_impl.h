@@ -834,8 +834,11 @@ hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const
   }
 }
 
-template <class Tr>
-hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hipStream_t s, bool hot) {
+// HOT: the largest k with an unrolled LDS-staged kernel (fp32/bf16 16, the other types 8; 0 = k = 2
+// only); larger k take the runtime-k register kernel.  The other types gained 4-6 % at k = 8 on the
+// LDS kernel (tools/dtype_rates.py, profiles/r02/s4/dtype_rates*.log).
+template <class Tr, int HOT>
+hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hipStream_t s) {
   using S = typename Tr::S;
   constexpr size_t VE = 16 / sizeof(S);
   const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
@@ -853,28 +856,16 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
   if (head > count) head = count;
   const size_t nvec = (count - head) / VE;
   const size_t tail = count - head - nvec * VE;
-  if (hot) {
-    switch (k) {
-      case 2: return launch_k<Tr, 2>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 3: return launch_k<Tr, 3>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 4: return launch_k<Tr, 4>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 5: return launch_k<Tr, 5>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 6: return launch_k<Tr, 6>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 7: return launch_k<Tr, 7>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 8: return launch_k<Tr, 8>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 9: return launch_k<Tr, 9>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 10: return launch_k<Tr, 10>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 11: return launch_k<Tr, 11>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 12: return launch_k<Tr, 12>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 13: return launch_k<Tr, 13>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 14: return launch_k<Tr, 14>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 15: return launch_k<Tr, 15>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      case 16: return launch_k<Tr, 16>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-      default: break;
-    }
-  } else if (k == 2) {
-    return launch_k<Tr, 2>(srcs, k, dst, nvec, (int)head, (int)tail, s);
-  }
+  hipError_t e = hipErrorInvalidValue;
+  bool done = false;
+  [&]<int... I>(std::integer_sequence<int, I...>) {  // k = 2 .. max(2, HOT), unrolled
+    ((k == I + 2 && (I + 2 == 2 || I + 2 <= HOT)
+          ? (e = launch_k<Tr, (I + 2 <= (HOT > 2 ? HOT : 2) ? I + 2 : 2)>(srcs, k, dst, nvec, (int)head, (int)tail, s),
+             done = true)
+          : false),
+     ...);
+  }(std::make_integer_sequence<int, (HOT > 2 ? HOT : 2) - 1>{});
+  if (done) return e;
   return launch_k<Tr, 0>(srcs, k, dst, nvec, (int)head, (int)tail, s);
 }
 

@@ -75,24 +75,24 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   }
   if (op == FTAR_SUM) {
     switch (dt) {
-      case FTAR_FLOAT32: e = launch_tr<F32Sum>(srcs, k, dst, count, s, lds); break;
+      case FTAR_FLOAT32: e = (lds ? launch_tr<F32Sum, 16>(srcs, k, dst, count, s) : launch_tr<F32Sum, 0>(srcs, k, dst, count, s)); break;
       case FTAR_BFLOAT16:
-        e = round_each && k > 2 ? launch_tr<BF16SumHop>(srcs, k, dst, count, s, lds)
-                                : launch_tr<BF16Sum>(srcs, k, dst, count, s, lds);
+        e = round_each && k > 2 ? (lds ? launch_tr<BF16SumHop, 16>(srcs, k, dst, count, s) : launch_tr<BF16SumHop, 0>(srcs, k, dst, count, s))
+                                : (lds ? launch_tr<BF16Sum, 16>(srcs, k, dst, count, s) : launch_tr<BF16Sum, 0>(srcs, k, dst, count, s));
         break;
-      case FTAR_FLOAT64: e = launch_tr<F64Sum>(srcs, k, dst, count, s, false); break;
-      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum>(srcs, k, dst, count, s, false); break;
-      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<U16Sum>(srcs, k, dst, count, s, false); break;
-      case FTAR_INT32: e = launch_tr<U32Sum>(srcs, k, dst, count, s, false); break;
-      case FTAR_INT64: e = launch_tr<U64Sum>(srcs, k, dst, count, s, false); break;
-      case FTAR_BOOL: e = launch_tr<BoolSum>(srcs, k, dst, count, s, false); break;
+      case FTAR_FLOAT64: e = launch_tr<F64Sum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<U16Sum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_INT32: e = launch_tr<U32Sum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_INT64: e = launch_tr<U64Sum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_BOOL: e = launch_tr<BoolSum, 8>(srcs, k, dst, count, s); break;
     }
   } else {
     switch (dt) {
-      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<Band<unsigned char>>(srcs, k, dst, count, s, false); break;
-      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<Band<unsigned short>>(srcs, k, dst, count, s, false); break;
-      case FTAR_INT32: e = launch_tr<Band<unsigned>>(srcs, k, dst, count, s, false); break;
-      case FTAR_INT64: e = launch_tr<Band<unsigned long long>>(srcs, k, dst, count, s, false); break;
+      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<Band<unsigned char>, 8>(srcs, k, dst, count, s); break;
+      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<Band<unsigned short>, 8>(srcs, k, dst, count, s); break;
+      case FTAR_INT32: e = launch_tr<Band<unsigned>, 8>(srcs, k, dst, count, s); break;
+      case FTAR_INT64: e = launch_tr<Band<unsigned long long>, 8>(srcs, k, dst, count, s); break;
       default: return FTAR_ERR_UNSUPPORTED;
     }
   }
