@@ -318,7 +318,9 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   ftar_topo_t t{};
   if (ft_lonely && *ft_lonely) t.lonely = atoi(ft_lonely);
   if (!ft_topo || !*ft_topo) {
-    if (nranks == 1) {  // one rank: a copy (mpi_mod.hpp:1739-1746); reported as the ring, like any width 1
+    // one rank and no lonely ranks: a copy (mpi_mod.hpp:1739-1746); reported as the ring, like any width 1.
+    // The reference's check (:1471) takes the unset FT_TOPO as a product of 1, so FT_LONELY must be 0 here.
+    if (nranks == 1 && t.lonely == 0) {
       t.nstages = 1;
       t.stages[0] = 1;
       t.ring = 1;
@@ -423,10 +425,12 @@ int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out) {
 }
 
 ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out) {
-  ftar_status_t st = ftar_topo_parse(getenv("FT_TOPO"), getenv("FT_LONELY"), nranks, out);
-  if (st == FTAR_SUCCESS) return st;
-  if (getenv("FT_TOPO") && *getenv("FT_TOPO")) return st;  // set but invalid: report it
-  return ftar_topo_choose(nranks, bytes, out);
+  // the engine's rule for topo == NULL (engine.cpp env_topology): both unset (FT_LONELY "0" = unset) ->
+  // the cost model; anything else must parse, or it is reported
+  const char* et = getenv("FT_TOPO");
+  const char* el = getenv("FT_LONELY");
+  if ((!et || !*et) && (!el || !*el || !strcmp(el, "0"))) return ftar_topo_choose(nranks, bytes, out);
+  return ftar_topo_parse(et, el, nranks, out);
 }
 
 double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes) {

@@ -64,10 +64,16 @@ struct ftar_comm {
   };
   std::map<int, Reg> regs;
   int next_reg = 1;
-  bool auto_topo = true;
+  // FT_TOPO / FT_LONELY are read on every call with topo == NULL, as the
+  // reference's get_stages is (mpi_mod.hpp:1732); the last strings seen and
+  // what they parsed to are kept, so an unchanged environment costs two getenv
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
-  ftar::Topology topo;
+  bool env_seen = false;
+  std::string env_topo, env_lonely;  // the strings last parsed ("" = unset)
+  ftar_status_t env_status = FTAR_SUCCESS;
+  bool env_auto = true;              // both unset: the cost model's choice per call
+  ftar::Topology env_t;
   std::map<std::string, std::shared_ptr<ftar::Plan>> plans;
   std::vector<hipEvent_t> events;
   // phase timing (diagnostic, ftar_comm_set_phase_timing): timing events
@@ -191,12 +197,41 @@ ftar_status_t comm_setup(ftar_comm* c) {
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
   if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
-  ftar_topo_t t;
-  if (ftar_topo_parse(getenv("FT_TOPO"), getenv("FT_LONELY"), c->nranks, &t) == FTAR_SUCCESS) {
-    c->auto_topo = false;
-    return to_topology(&t, c->nranks, &c->topo);
+  return FTAR_SUCCESS;
+}
+
+// The topology of a call with topo == NULL, from the environment AT THIS CALL
+// (get_stages, mpi_mod.hpp:1419-1486, re-run by every MPI_Allreduce_FT call,
+// :1732).  FT_TOPO and FT_LONELY both unset (or FT_LONELY "0"): *is_auto, the
+// cost model chooses (the reference exit(1)s here for P > 1).
+// Anything else must parse for this communicator's size, or the call fails
+// with FTAR_ERR_INVALID_TOPO before it enqueues anything (the reference:
+// "invalid FT_TOPO" and exit(1), :1471-1475) -- on every rank alike, since
+// every rank reads the same environment.
+static ftar_status_t env_topology(ftar_comm* c, bool* is_auto, Topology* out) {
+  const char* et = getenv("FT_TOPO");
+  const char* el = getenv("FT_LONELY");
+  const std::string st = et ? et : "", sl = el ? el : "";
+  if (!c->env_seen || st != c->env_topo || sl != c->env_lonely) {
+    c->env_seen = true;
+    c->env_topo = st;
+    c->env_lonely = sl;
+    c->env_auto = st.empty() && (sl.empty() || sl == "0");
+    c->env_status = FTAR_SUCCESS;
+    if (!c->env_auto) {
+      ftar_topo_t t;
+      c->env_status = ftar_topo_parse(st.c_str(), sl.c_str(), c->nranks, &t);
+      if (c->env_status == FTAR_SUCCESS) c->env_status = to_topology(&t, c->nranks, &c->env_t);
+      if (c->env_status != FTAR_SUCCESS) c->env_status = FTAR_ERR_INVALID_TOPO;
+    }
   }
-  c->auto_topo = true;
+  if (c->env_status != FTAR_SUCCESS) {
+    set_error("invalid FT_TOPO '" + st + "' / FT_LONELY '" + sl + "' for " + std::to_string(c->nranks) + " ranks",
+              __FILE__, __LINE__);
+    return c->env_status;
+  }
+  *is_auto = c->env_auto;
+  if (!c->env_auto) *out = c->env_t;
   return FTAR_SUCCESS;
 }
 
@@ -675,16 +710,18 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
 
 namespace {
 
-// The call's topology (argument, FT_TOPO at init, or the cost model) and its
-// cached plan; check_world once per (topology, count, form).
+// The call's topology (argument, FT_TOPO/FT_LONELY read at this call, or the
+// cost model) and its cached plan; check_world once per (topology, count, form).
 ftar_status_t resolve_plan(ftar_comm* c, const ftar_topo_t* topo, size_t count, size_t esz, const Form& form,
                            const Plan** out) {
   Topology t;
+  bool is_auto = false;
   if (topo) {
     FTAR_RETURN_IF(to_topology(topo, c->nranks, &t));
-  } else if (!c->auto_topo) {
-    t = c->topo;
   } else {
+    FTAR_RETURN_IF(env_topology(c, &is_auto, &t));
+  }
+  if (is_auto) {
     ftar_topo_t ch;
     FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
     FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
@@ -830,6 +867,11 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
                                const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host) {
   const size_t esz = dtype_size(dt);
   if (sendbuf == recvbuf) sendbuf = nullptr;
+  {  // the topology is checked first, as get_stages runs before the P <= 1 copy (mpi_mod.hpp:1732-1746)
+    Topology t;
+    bool is_auto = false;
+    FTAR_RETURN_IF(topo ? to_topology(topo, c->nranks, &t) : env_topology(c, &is_auto, &t));
+  }
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
     if (sendbuf && count && host)
       FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, hipMemcpyHostToHost, stream));

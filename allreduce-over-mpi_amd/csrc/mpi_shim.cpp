@@ -2,7 +2,9 @@
 // (allreduce_over_mpi/mpi_mod.hpp:1723-1778) re-expressed over libftar.
 //
 //   reference                               here
-//   get_stages() every call (:1732)         FT_TOPO/FT_LONELY read once per communicator
+//   get_stages() every call (:1732)         same: FT_TOPO/FT_LONELY read on every call; unset
+//   invalid FT_TOPO -> exit(1) (:1471-1475)  -> cost model; set but invalid -> MPI_ERR_ARG on
+//                                           every rank, before anything moves (P = 1 included)
 //   FlexTree_Context (:1734)                ftar plan cache (per topology, count)
 //   P <= 1 -> memcpy (:1739-1746)           same, on the host
 //   static grow-only host recv_buffer       grow-only DEVICE staging buffer per communicator
@@ -194,6 +196,49 @@ int init_entry(Entry* e, MPI_Comm comm) {
   return MPI_SUCCESS;
 }
 
+// get_stages runs first on every call (mpi_mod.hpp:1732), so an invalid
+// FT_TOPO fails every call, a 1-rank call (whose copy never reaches the
+// engine) included.  The engine re-checks, per call, for C-ABI callers.
+// The last verdict per (FT_TOPO, FT_LONELY, size) is kept: a lonely layout's
+// check builds every rank's plan, and an unchanged environment should cost
+// two getenv per call.
+int check_env_topo(int nranks) {
+  const char* t = getenv("FT_TOPO");
+  const char* l = getenv("FT_LONELY");
+  if ((!t || !*t) && (!l || !*l || !strcmp(l, "0"))) return MPI_SUCCESS;  // unset: the cost model
+  static std::mutex mu;
+  static std::string last_t, last_l;
+  static int last_n = -1, last_rc = MPI_SUCCESS;
+  std::lock_guard<std::mutex> g(mu);
+  const std::string st = t ? t : "", sl = l ? l : "";
+  if (nranks != last_n || st != last_t || sl != last_l) {
+    ftar_topo_t x;
+    last_rc = ftar_topo_parse(t, l, nranks, &x) == FTAR_SUCCESS ? MPI_SUCCESS : MPI_ERR_ARG;
+    last_n = nranks;
+    last_t = st;
+    last_l = sl;
+  }
+  return last_rc;
+}
+
+// before the communicator's bring-up, as get_stages precedes everything in the
+// reference's call: a bad FT_TOPO fails every rank alike, GPU or not
+int check_topo_first(MPI_Comm comm) {
+  int size = 1;
+  if (MPI_Comm_size(comm, &size) != MPI_SUCCESS) return MPI_ERR_COMM;
+  return check_env_topo(size);
+}
+
+int status_to_mpi(ftar_status_t st) {
+  switch (st) {
+    case FTAR_SUCCESS: return MPI_SUCCESS;
+    case FTAR_ERR_NO_MEMORY: return MPI_ERR_NO_MEM;
+    case FTAR_ERR_INVALID_TOPO:
+    case FTAR_ERR_INVALID_ARG: return MPI_ERR_ARG;
+    default: return MPI_ERR_OTHER;
+  }
+}
+
 // device + stream on first GPU use (a 1-rank communicator's host path never needs them)
 int ensure_stream(Entry* e) {
   if (hipSetDevice(e->device) != hipSuccess) return MPI_ERR_OTHER;
@@ -316,6 +361,7 @@ int MPI_Allreduce_FT(const void* sendbuf, void* recvbuf, int count, MPI_Datatype
   Entry* e;
   int rc = lookup(comm, &e);
   if (rc != MPI_SUCCESS) return rc;
+  if ((rc = check_topo_first(comm)) != MPI_SUCCESS) return rc;
   std::lock_guard<std::mutex> g(e->mu);
   if ((rc = init_entry(e, comm)) != MPI_SUCCESS) return rc;
   const size_t bytes = (size_t)count * ftar_dtype_size(dt);
@@ -330,8 +376,7 @@ int MPI_Allreduce_FT(const void* sendbuf, void* recvbuf, int count, MPI_Datatype
   if (src != recvbuf) pin.b = acquire_pinned(recvbuf, bytes);
   const ftar_status_t st = ftar_allreduce_host(src == recvbuf ? nullptr : src, recvbuf, (size_t)count, dt, fo,
                                                nullptr, e->comm, e->stream);
-  if (st == FTAR_ERR_NO_MEMORY) return MPI_ERR_NO_MEM;
-  if (st != FTAR_SUCCESS) return MPI_ERR_OTHER;
+  if (st != FTAR_SUCCESS) return status_to_mpi(st);
   if (hipStreamSynchronize(e->stream) != hipSuccess) return MPI_ERR_OTHER;
   return MPI_SUCCESS;
 }
@@ -346,6 +391,7 @@ int MPI_Allreduce_FT_device(const void* sendbuf, void* recvbuf, int count, MPI_D
   Entry* e;
   int rc = lookup(comm, &e);
   if (rc != MPI_SUCCESS) return rc;
+  if ((rc = check_topo_first(comm)) != MPI_SUCCESS) return rc;
   std::lock_guard<std::mutex> g(e->mu);
   if ((rc = init_entry(e, comm)) != MPI_SUCCESS) return rc;
   if ((rc = ensure_stream(e)) != MPI_SUCCESS) return rc;
@@ -357,8 +403,7 @@ int MPI_Allreduce_FT_device(const void* sendbuf, void* recvbuf, int count, MPI_D
       return MPI_ERR_OTHER;
   } else {
     const ftar_status_t st = ftar_allreduce(src, recvbuf, (size_t)count, dt, fo, nullptr, e->comm, s);
-    if (st == FTAR_ERR_NO_MEMORY) return MPI_ERR_NO_MEM;
-    if (st != FTAR_SUCCESS) return MPI_ERR_OTHER;
+    if (st != FTAR_SUCCESS) return status_to_mpi(st);
   }
   if (!stream && hipStreamSynchronize(s) != hipSuccess) return MPI_ERR_OTHER;
   return MPI_SUCCESS;

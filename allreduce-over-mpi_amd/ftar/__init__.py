@@ -637,8 +637,9 @@ def MPI_Allreduce_FT(sendbuf, recvbuf, count, datatype, op, comm, stream=None):
 
     sendbuf=MPI_IN_PLACE (None) reduces recvbuf in place; datatype/op accept the
     reference's MPI names ("MPI_FLOAT", "MPI_SUM"); the topology comes from
-    FT_TOPO/FT_LONELY at communicator creation (or the cost model).  Returns 0
-    like the reference; raises FtarError where the reference would exit(1).
+    FT_TOPO/FT_LONELY read at this call, as get_stages is (mpi_mod.hpp:1732;
+    both unset: the cost model).  Returns 0 like the reference; raises
+    FtarError where the reference would exit(1) (an invalid FT_TOPO among them).
     """
     comm.allreduce(sendbuf, recvbuf, count, datatype, op, stream=stream)
     return 0

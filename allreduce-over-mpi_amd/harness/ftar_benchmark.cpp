@@ -48,6 +48,34 @@ static void die(int rank, const std::string& msg) {
   MPI_Abort(MPI_COMM_WORLD, 1);
 }
 
+// A failed MPI_Allreduce_FT.  The reference exit(1)s inside the call (an
+// invalid FT_TOPO, mpi_mod.hpp:1471-1475); here the call returned an MPI error
+// class.  An argument error fails every rank at the same call, so the ranks
+// agree on it (a non-blocking allreduce, 10 s at most) and end together with
+// exit code 1; a rank whose peers went on aborts the job.
+[[noreturn]] static void call_failed(int rank, int P, const char* when, int rc) {
+  char msg[MPI_MAX_ERROR_STRING] = "";
+  int len = 0;
+  MPI_Error_string(rc, msg, &len);
+  const char* topo = getenv("FT_TOPO");
+  fprintf(stderr, "[rank %d] allreduce failed (%s): MPI error %d: %s; FT_TOPO=%s; %s\n", rank, when, rc, msg,
+          topo ? topo : "(unset)", ftar_last_error());
+  fflush(stderr);
+  int one = 1, failed = 0;
+  MPI_Request rq;
+  MPI_Iallreduce(&one, &failed, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD, &rq);
+  int done = 0;
+  for (int i = 0; i < 1000 && !done; ++i) {
+    MPI_Test(&rq, &done, MPI_STATUS_IGNORE);
+    if (!done) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  if (!done) MPI_Abort(MPI_COMM_WORLD, 1);
+  if (rank == 0) printf("FAILED: allreduce failed on %d of %d ranks\n", failed, P);
+  fflush(stdout);
+  MPI_Finalize();
+  exit(1);
+}
+
 int main(int argc, char** argv) {
   int provided = 0, rank = 0, P = 1;
   MPI_Init_thread(&argc, &argv, MPI_THREAD_MULTIPLE, &provided);  // benchmark.cpp:50
@@ -127,7 +155,7 @@ int main(int argc, char** argv) {
 
   // warm-up calls change the data (in place, x P each); restart from i*0.1 afterwards
   for (int i = 0; i < warmup; ++i)
-    if (one_call() != MPI_SUCCESS) die(rank, "allreduce failed (warmup)");
+    if (int rc = one_call()) call_failed(rank, P, "warmup", rc);
   if (warmup) {
     for (size_t i = 0; i < data_len; ++i) data[i] = i * base;
     if (device && hipMemcpy(dptr, data.data(), data_len * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
@@ -139,7 +167,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < repeat; ++i) {  // benchmark.cpp:157-167
     MPI_Barrier(MPI_COMM_WORLD);
     const double t1 = MPI_Wtime();
-    if (one_call() != MPI_SUCCESS) die(rank, "allreduce failed");
+    if (int rc = one_call()) call_failed(rank, P, "timed call", rc);
     const double t2 = MPI_Wtime();
     times.push_back(t2 - t1);
     sum_time += t2 - t1;

@@ -245,9 +245,13 @@ ftar_status_t ftar_comm_register(ftar_comm_t comm, void* buf, size_t bytes, int*
 ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg);
 
 /* ---- AllReduce (device resident) -------------------------------------------
- * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL: the
- * communicator's topology (FT_TOPO/FT_LONELY from the environment at init,
- * else the cost-model choice).  Enqueued on `stream`; returns once enqueued. */
+ * sendbuf == NULL or == recvbuf: in place (MPI_IN_PLACE).  topo == NULL:
+ * FT_TOPO/FT_LONELY read from the environment at THIS call, as get_stages is
+ * on every MPI_Allreduce_FT call (mpi_mod.hpp:1732); both unset: the cost
+ * model's choice; set but invalid for the communicator's size:
+ * FTAR_ERR_INVALID_TOPO before anything is enqueued (the reference exit(1)s,
+ * :1471-1475), 1-rank communicators included.  Enqueued on `stream`; returns
+ * once enqueued. */
 ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
                              const ftar_topo_t* topo, ftar_comm_t comm, void* stream);
 /* Drive every rank of an ftar_comm_init_local group from this one call

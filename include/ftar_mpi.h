@@ -10,8 +10,12 @@
  *
  * Same arguments and semantics: host buffers (the MPI send/recv buffers of
  * the caller), sendbuf == MPI_IN_PLACE reduces recvbuf in place, collective
- * over `comm`, FT_TOPO / FT_LONELY from the environment (unset: the
- * re-fitted cost model instead of the reference's exit(1)).  Underneath:
+ * over `comm`, FT_TOPO / FT_LONELY read from the environment on EVERY call as
+ * get_stages is (mpi_mod.hpp:1732; both unset: the re-fitted cost model
+ * instead of the reference's exit(1); set but invalid for the communicator's
+ * size: MPI_ERR_ARG on every rank before anything moves, 1-rank calls
+ * included, where the reference prints "invalid FT_TOPO" and exit(1)s,
+ * :1471-1475).  Underneath:
  * one GPU per rank (node-local rank % visible devices, or FTAR_DEVICE),
  * H2D -> device AllReduce (RCCL p2p over xGMI + HIP reduce kernel) -> D2H.
  * FTAR_MPI_TRANSPORT=auto (default) | rccl | ipc: ipc bootstraps over `comm`

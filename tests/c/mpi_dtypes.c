@@ -2,8 +2,13 @@
    (allreduce_over_mpi/mpi_mod.hpp:1363-1412): every MPI datatype the reference reduces maps to the ftar
    dtype of the same width and signedness, BAND is accepted, anything else is MPI_ERR_TYPE / MPI_ERR_OP, and
    MPI_Allreduce_FT on a 1-rank communicator copies (mpi_mod.hpp:1739-1746) for every type.
+   FT_TOPO / FT_LONELY are read on every call (get_stages, mpi_mod.hpp:1732): a value invalid for the
+   communicator's size is MPI_ERR_ARG even on one rank (the reference: "invalid FT_TOPO", exit(1),
+   :1471-1475), and a change between two calls takes effect at the next call.
    Built and run by tests/test_capi.py under mpiexec -n 1 (no GPU needed). */
+#define _POSIX_C_SOURCE 200112L /* setenv / unsetenv under -std=c99 */
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "ftar_mpi.h"
@@ -50,6 +55,31 @@ int main(int argc, char** argv) {
   bad += MPI_Allreduce_FT(in, NULL, 4, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_ERR_ARG;
   bad += MPI_Allreduce_FT(NULL, NULL, 0, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_SUCCESS;
   bad += MPI_Allreduce_FT(in, out, 4, MPI_FLOAT, MPI_SUM, MPI_COMM_NULL) != MPI_ERR_COMM;
+  /* FT_TOPO per call */
+  {
+    static const char* bad_topos[] = {"3", "2,2", "0", "2,x", "-1", "abc"};
+    size_t t;
+    for (t = 0; t < sizeof bad_topos / sizeof *bad_topos; ++t) {
+      setenv("FT_TOPO", bad_topos[t], 1);
+      memset(out, 0, sizeof out);
+      if (MPI_Allreduce_FT(in, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_ERR_ARG) {
+        printf("FT_TOPO=%s accepted on 1 rank\n", bad_topos[t]);
+        ++bad;
+      }
+      bad += MPI_Allreduce_FT(MPI_IN_PLACE, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_ERR_ARG;
+    }
+    setenv("FT_TOPO", "1", 1); /* the ring at any P: valid, the copy runs */
+    memset(out, 0, sizeof out);
+    bad += MPI_Allreduce_FT(in, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_SUCCESS;
+    bad += memcmp(in, out, 64) != 0;
+    unsetenv("FT_TOPO");
+    setenv("FT_LONELY", "1", 1); /* lonely ranks without FT_TOPO: invalid */
+    bad += MPI_Allreduce_FT(in, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_ERR_ARG;
+    setenv("FT_LONELY", "0", 1); /* "0" is the same as unset */
+    bad += MPI_Allreduce_FT(in, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_SUCCESS;
+    unsetenv("FT_LONELY");
+    bad += MPI_Allreduce_FT(in, out, 16, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD) != MPI_SUCCESS;
+  }
   MPI_Allreduce_FT_finalize();
   MPI_Finalize();
   printf(bad ? "mpi dtypes FAILED (%d)\n" : "mpi dtypes ok\n", bad);

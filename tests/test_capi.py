@@ -51,6 +51,9 @@ def test_topo_parse_valid(spec, lonely, P, expect):
     (None, None, 4),     # unset FT_TOPO with P > 1 (reference: exit(1))
     ("", None, 4),
     ("2,x", None, 4),
+    ("3", None, 1),      # checked before the P <= 1 copy (mpi_mod.hpp:1732-1746)
+    (None, "1", 1),      # lonely ranks with FT_TOPO unset: product 1 + 1 != 1
+    ("2", "1", 1),
 ])
 def test_topo_parse_invalid(spec, lonely, P):
     import ftar
@@ -96,6 +99,14 @@ def test_topo_from_env(monkeypatch):
     monkeypatch.setenv("FT_TOPO", "3")
     with pytest.raises(ftar.FtarError):
         ftar.topo_from_env(5, 1 << 20)
+    monkeypatch.delenv("FT_TOPO")
+    with pytest.raises(ftar.FtarError):   # FT_LONELY alone is not "unset": reported, not the cost model
+        ftar.topo_from_env(5, 1 << 20)
+    monkeypatch.setenv("FT_LONELY", "0")  # ... but "0" is
+    assert str(ftar.topo_from_env(8, 1 << 30)) == "8"
+    monkeypatch.setenv("FT_TOPO", "1")    # the ring at any P, FT_LONELY ignored (mpi_mod.hpp:1461-1464)
+    monkeypatch.setenv("FT_LONELY", "3")
+    assert str(ftar.topo_from_env(8, 1 << 30)) == "ring"
     monkeypatch.delenv("FT_TOPO")
     monkeypatch.delenv("FT_LONELY")
     assert str(ftar.topo_from_env(8, 1 << 30)) == "8"

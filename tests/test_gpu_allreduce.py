@@ -113,6 +113,46 @@ def test_allreduce_default_topology_is_cost_model_choice():
         np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32))
 
 
+def test_allreduce_reads_ft_topo_on_every_call(monkeypatch):
+    """topo == NULL: FT_TOPO / FT_LONELY are read at each call, as get_stages is on every MPI_Allreduce_FT
+    call (mpi_mod.hpp:1732), on one communicator (no re-creation).  A value invalid for P fails the call
+    on every rank with FTAR_ERR_INVALID_TOPO before anything is enqueued (the reference: "invalid FT_TOPO",
+    exit(1), :1471-1475) -- the buffers stay untouched -- never the cost model silently; a valid value
+    afterwards works again on the same communicator, and unset means the cost model's choice."""
+    import ftar
+    P, n = 4, 30_011
+    ins = [fi.fill("f32", 21, r, n) for r in range(P)]
+    monkeypatch.delenv("FT_LONELY", raising=False)
+    for spec, oracle_topo in (("2,2", "2,2"), ("1", "1"), ("4", "4"), (None, None), ("2,2", "2,2")):
+        if spec is None:
+            monkeypatch.delenv("FT_TOPO", raising=False)
+            chosen = str(ftar.topo_choose(P, n * 4))
+            oracle_topo = "1" if chosen == "ring" else chosen
+        else:
+            monkeypatch.setenv("FT_TOPO", spec)
+        outs = run_group(ins, None)
+        ref = oracle_lib.allreduce(ins, oracle_topo)
+        for r in range(P):
+            np.testing.assert_array_equal(outs[r].view(np.uint32), ref[r].view(np.uint32), err_msg=f"{spec} r{r}")
+        for bad, lonely in (("3", None), ("2,x", None), ("8", None), ("2", "1"), (None, "2")):
+            if bad is None:
+                monkeypatch.delenv("FT_TOPO", raising=False)
+            else:
+                monkeypatch.setenv("FT_TOPO", bad)
+            if lonely is None:
+                monkeypatch.delenv("FT_LONELY", raising=False)
+            else:
+                monkeypatch.setenv("FT_LONELY", lonely)
+            bufs = [to_dev(x) for x in ins]
+            with pytest.raises(ftar.FtarError) as ei:
+                group(P).allreduce(None, [p for _, p in bufs], n, "f32", "sum")
+            assert ei.value.status == 3, str(ei.value)
+            for r in range(P):
+                np.testing.assert_array_equal(from_dev(bufs[r][0], np.float32, n).view(np.uint32),
+                                              ins[r].view(np.uint32))
+        monkeypatch.delenv("FT_LONELY", raising=False)
+
+
 def test_allreduce_zero_count_and_unsupported():
     import ftar
     g = group(2)

@@ -51,6 +51,59 @@ def test_harness_rejects_unknown_arguments(tmp_path):
 
 
 @needs
+@pytest.mark.parametrize("ranks", [1, 2])
+@pytest.mark.parametrize("topo,lonely", [("3", None), ("2,x", None), ("0", None), ("4", None), (None, "1"),
+                                         ("2", "1")])
+def test_harness_invalid_ft_topo_fails_every_rank(tmp_path, ranks, topo, lonely):
+    """An FT_TOPO / FT_LONELY invalid for the job's size: the reference prints "invalid FT_TOPO" and
+    exit(1)s inside MPI_Allreduce_FT on every rank (get_stages, mpi_mod.hpp:1471-1475), 1-rank jobs included
+    (the check precedes the P <= 1 copy, :1732-1746).  Here the call returns MPI_ERR_ARG on every rank before
+    the communicator is brought up (so no GPU is involved), and the harness ends with exit code 1, every rank
+    reporting the failure -- never the cost model's topology silently."""
+    env = {}
+    if topo is not None:
+        env["FT_TOPO"] = topo
+    if lonely is not None:
+        env["FT_LONELY"] = lonely
+    if ranks == 2 and topo == "2" and lonely is None:
+        pytest.skip("valid at 2 ranks")
+    base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY")}
+    p = subprocess.run([MPIEXEC, "-n", str(ranks), BIN, "--size", "4096", "--repeat", "2", "--check"], cwd=tmp_path,
+                       env=dict(base, **env), capture_output=True, text=True, timeout=120)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0, out
+    assert f"FAILED: allreduce failed on {ranks} of {ranks} ranks" in out, out
+    for r in range(ranks):
+        assert re.search(rf"\[rank {r}\] allreduce failed \(timed call\): MPI error \d+", out), out
+    assert "test passed" not in out
+
+
+@needs
+def test_harness_ft_topo_valid_single_rank(tmp_path):
+    """The valid spellings at one rank (the ring "1", unset) still copy: the P <= 1 path."""
+    base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY")}
+    for env in ({}, {"FT_TOPO": "1"}, {"FT_TOPO": "1", "FT_LONELY": "0"}):
+        p = subprocess.run([MPIEXEC, "-n", "1", BIN, "--size", "1000", "--repeat", "2", "--check"], cwd=tmp_path,
+                           env=dict(base, **env), capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0 and "(test passed)" in p.stdout, (env, p.stdout + p.stderr)
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [[], ["--device"]], ids=["host", "device"])
+def test_harness_invalid_ft_topo_two_ranks_on_gpu(tmp_path, extra):
+    """The same through a brought-up communicator on the GPU (2 MPI ranks, the ipc transport on the box's
+    one GPU): --device first brings the communicator up (MPI_Allreduce_FT_comm), then FT_TOPO=3 fails the
+    device call on both ranks before anything is enqueued."""
+    base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY")}
+    p = subprocess.run([MPIEXEC, "-n", "2", BIN, "--size", "65536", "--repeat", "1"] + extra, cwd=tmp_path,
+                       env=dict(base, FT_TOPO="3"), capture_output=True, text=True, timeout=120)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0, out
+    assert "FAILED: allreduce failed on 2 of 2 ranks" in out, out
+
+
+@needs
 @pytest.mark.gpu
 def test_harness_device_resident_single_rank(tmp_path):
     rc, out = run(1, ["--size", "1048576", "--repeat", "3", "--warmup", "1", "--check", "--device"], tmp_path)
