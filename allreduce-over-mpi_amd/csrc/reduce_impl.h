@@ -8,7 +8,7 @@
 // Design (bandwidth-bound: (k+1)*n*sizeof(T) bytes, ~0 flops per byte, no MFMA):
 //   * 16 B per lane per access, one wave instruction = 1 KiB contiguous per
 //     source: fully coalesced;
-//   * k = 2..16 (fp32/bf16; k = 2 for every type): reduce_lds_kernel stages
+//   * k = 2..16 for fp32/bf16, k = 2..8 for the other types: reduce_lds_kernel stages
 //     U tiles of every source per wave through LDS with LDS-DMA
 //     (global_load_lds_dwordx4, nontemporal) and folds tile by tile as each
 //     tile lands (counted vmcnt); stores are nontemporal too (cold data: every
@@ -41,6 +41,16 @@
 #include "ftar_internal.h"
 
 namespace ftar {
+
+// The kernel the launchers below launched last on this thread (its host-side handle):
+// ftar_debug_last_kernel names it, so bench.py reports PMC traffic only for the kernel it timed.
+inline thread_local const void* g_last_kernel = nullptr;
+#define FTAR_LAUNCH(KERNEL, ...)                                         \
+  do {                                                                   \
+    ::ftar::g_last_kernel = reinterpret_cast<const void*>(KERNEL);       \
+    hipLaunchKernelGGL(KERNEL, __VA_ARGS__);                             \
+  } while (0)
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -451,7 +461,7 @@ hipError_t launch_lds(const void* const* srcs, void* dst, size_t nvec, hipStream
     for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
     const size_t per_block = (size_t)W * U * 64;
     const size_t blocks = (nvec + per_block - 1) / per_block;
-    hipLaunchKernelGGL((reduce_lds_kernel<Tr, K, U, W, AUX, PROG>), dim3((unsigned)(blocks ? blocks : 1)),
+    FTAR_LAUNCH((reduce_lds_kernel<Tr, K, U, W, AUX, PROG>), dim3((unsigned)(blocks ? blocks : 1)),
                        dim3(W * 64), 0, s, a, dst, nvec, head, tail);
     return hipGetLastError();
   }
@@ -711,7 +721,7 @@ hipError_t launch_cfg(const void* const* srcs, int k, void* dst, size_t nvec, in
   if (blocks == 0) blocks = 1;  // head/tail only
   if (max_blocks && blocks > max_blocks) blocks = max_blocks;  // grid-stride over the rest
   if (blocks > 0x7fffffffull) blocks = 0x7fffffffull;
-  hipLaunchKernelGGL((reduce_vec_kernel<Tr, K, U, NTL, NTS, BS>), dim3((unsigned)blocks), dim3(BS), 0, s, a, k, dst,
+  FTAR_LAUNCH((reduce_vec_kernel<Tr, K, U, NTL, NTS, BS>), dim3((unsigned)blocks), dim3(BS), 0, s, a, k, dst,
                      nvec, head, tail);
   return hipGetLastError();
 }
@@ -747,7 +757,7 @@ hipError_t launch_tree_k(const void* const* srcs, int k, const TreeCode& tc, voi
   size_t blocks = (nvec + (size_t)U * kThreads - 1) / ((size_t)U * kThreads);
   if (blocks == 0) blocks = 1;
   if (blocks > 0x7fffffffull) blocks = 0x7fffffffull;
-  hipLaunchKernelGGL((reduce_tree_kernel<Tr, K, U, Sh>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
+  FTAR_LAUNCH((reduce_tree_kernel<Tr, K, U, Sh>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
                      nvec, head, tail);
   return hipGetLastError();
 }
@@ -760,7 +770,7 @@ hipError_t launch_tree_lds(const void* const* srcs, const TreeCode& tc, void* ds
   for (int j = 0; j < K; ++j) a.p[j] = srcs[j];
   const size_t per_block = (size_t)W * U * 64;
   const size_t blocks = (nvec + per_block - 1) / per_block;
-  hipLaunchKernelGGL((reduce_tree_lds_kernel<Tr, K, U, W, Sh>), dim3((unsigned)(blocks ? blocks : 1)), dim3(W * 64),
+  FTAR_LAUNCH((reduce_tree_lds_kernel<Tr, K, U, W, Sh>), dim3((unsigned)(blocks ? blocks : 1)), dim3(W * 64),
                      0, s, a, tc, dst, nvec, head, tail);
   return hipGetLastError();
 }
@@ -778,7 +788,7 @@ hipError_t launch_tree(const void* const* srcs, int k, const TreeCode& tc, const
     for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
     size_t blocks = (count + kThreads - 1) / kThreads;
     blocks = blocks > 8192 ? 8192 : blocks;
-    hipLaunchKernelGGL((reduce_tree_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
+    FTAR_LAUNCH((reduce_tree_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, tc, dst,
                        count);
     return hipGetLastError();
   }
@@ -849,7 +859,7 @@ hipError_t launch_tr(const void* const* srcs, int k, void* dst, size_t count, hi
     for (int j = 0; j < k; ++j) a.p[j] = srcs[j];
     size_t blocks = (count + kThreads - 1) / kThreads;
     blocks = blocks > 8192 ? 8192 : blocks;
-    hipLaunchKernelGGL((reduce_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, dst, count);
+    FTAR_LAUNCH((reduce_elem_kernel<Tr>), dim3((unsigned)blocks), dim3(kThreads), 0, s, a, k, dst, count);
     return hipGetLastError();
   }
   size_t head = mis ? (16 - mis) / sizeof(S) : 0;

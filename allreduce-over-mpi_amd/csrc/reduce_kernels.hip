@@ -3,6 +3,11 @@
 // (allreduce_over_mpi/mpi_mod.hpp:812-1251) and reduce_sum_gpu (vector_add/reduce_sum_gpu.h:205).
 #include "reduce_impl.h"
 
+#include <cxxabi.h>
+
+#include <cstdlib>
+#include <cstring>
+
 namespace ftar {
 
 size_t dtype_size(ftar_dtype_t dt) {
@@ -42,12 +47,20 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, 
   bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
   if (max_wg_per_seg) bx = std::min(bx, max_wg_per_seg);
   if (nt)
-    hipLaunchKernelGGL(gather_kernel<true>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+    FTAR_LAUNCH(gather_kernel<true>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
   else
-    hipLaunchKernelGGL(gather_kernel<false>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+    FTAR_LAUNCH(gather_kernel<false>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
   FTAR_CHECK_HIP(hipGetLastError());
   return FTAR_SUCCESS;
 }
+
+namespace {
+// the LDS-staged kernel up to k = HOT, or (lds == false: the peer forms' ":vec" A/B) only at k = 2
+template <class Tr, int HOT>
+hipError_t tr(bool lds, const void* const* srcs, int k, void* dst, size_t count, hipStream_t s) {
+  return lds ? launch_tr<Tr, HOT>(srcs, k, dst, count, s) : launch_tr<Tr, 0>(srcs, k, dst, count, s);
+}
+}  // namespace
 
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
                             hipStream_t s, bool round_each, const int* shape, int nlevels, bool lds) {
@@ -75,24 +88,24 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   }
   if (op == FTAR_SUM) {
     switch (dt) {
-      case FTAR_FLOAT32: e = (lds ? launch_tr<F32Sum, 16>(srcs, k, dst, count, s) : launch_tr<F32Sum, 0>(srcs, k, dst, count, s)); break;
+      case FTAR_FLOAT32: e = tr<F32Sum, 16>(lds, srcs, k, dst, count, s); break;
       case FTAR_BFLOAT16:
-        e = round_each && k > 2 ? (lds ? launch_tr<BF16SumHop, 16>(srcs, k, dst, count, s) : launch_tr<BF16SumHop, 0>(srcs, k, dst, count, s))
-                                : (lds ? launch_tr<BF16Sum, 16>(srcs, k, dst, count, s) : launch_tr<BF16Sum, 0>(srcs, k, dst, count, s));
+        e = round_each && k > 2 ? tr<BF16SumHop, 16>(lds, srcs, k, dst, count, s)
+                                : tr<BF16Sum, 16>(lds, srcs, k, dst, count, s);
         break;
-      case FTAR_FLOAT64: e = launch_tr<F64Sum, 8>(srcs, k, dst, count, s); break;
-      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<U8Sum, 8>(srcs, k, dst, count, s); break;
-      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<U16Sum, 8>(srcs, k, dst, count, s); break;
-      case FTAR_INT32: e = launch_tr<U32Sum, 8>(srcs, k, dst, count, s); break;
-      case FTAR_INT64: e = launch_tr<U64Sum, 8>(srcs, k, dst, count, s); break;
-      case FTAR_BOOL: e = launch_tr<BoolSum, 8>(srcs, k, dst, count, s); break;
+      case FTAR_FLOAT64: e = tr<F64Sum, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_UINT8: case FTAR_INT8: e = tr<U8Sum, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_UINT16: case FTAR_INT16: e = tr<U16Sum, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_INT32: e = tr<U32Sum, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_INT64: e = tr<U64Sum, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_BOOL: e = tr<BoolSum, 8>(lds, srcs, k, dst, count, s); break;
     }
   } else {
     switch (dt) {
-      case FTAR_UINT8: case FTAR_INT8: e = launch_tr<Band<unsigned char>, 8>(srcs, k, dst, count, s); break;
-      case FTAR_UINT16: case FTAR_INT16: e = launch_tr<Band<unsigned short>, 8>(srcs, k, dst, count, s); break;
-      case FTAR_INT32: e = launch_tr<Band<unsigned>, 8>(srcs, k, dst, count, s); break;
-      case FTAR_INT64: e = launch_tr<Band<unsigned long long>, 8>(srcs, k, dst, count, s); break;
+      case FTAR_UINT8: case FTAR_INT8: e = tr<Band<unsigned char>, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_UINT16: case FTAR_INT16: e = tr<Band<unsigned short>, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_INT32: e = tr<Band<unsigned>, 8>(lds, srcs, k, dst, count, s); break;
+      case FTAR_INT64: e = tr<Band<unsigned long long>, 8>(lds, srcs, k, dst, count, s); break;
       default: return FTAR_ERR_UNSUPPORTED;
     }
   }
@@ -101,6 +114,28 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
 }
 
 }  // namespace ftar
+
+// The kernel the reduce/copy launchers last launched on the calling thread, demangled the way rocprofv3
+// prints kernel names ("void ftar::(anonymous namespace)::reduce_lds_kernel<...>(...)"); bench.py
+// ties the PMC traffic it reports to this symbol.  Returns the length needed (excluding the NUL), or
+// -1 when nothing was launched on this thread.
+extern "C" long ftar_debug_last_kernel(char* buf, size_t buflen) {
+  const void* k = ftar::g_last_kernel;
+  if (!k) return -1;
+  const char* raw = hipKernelNameRefByPtr(k, nullptr);
+  if (!raw) return -1;
+  int status = 0;
+  char* dem = abi::__cxa_demangle(raw, nullptr, nullptr, &status);
+  const char* name = status == 0 && dem ? dem : raw;
+  const size_t need = strlen(name);
+  if (buf && buflen) {
+    const size_t m = need < buflen - 1 ? need : buflen - 1;
+    memcpy(buf, name, m);
+    buf[m] = 0;
+  }
+  free(dem);
+  return (long)need;
+}
 
 // A/B of the nested fold: lds = 1 the LDS-staged kernel (production), 0 the
 // register kernel of round 1 (tools/kbench_cold.py --shapes).
@@ -139,10 +174,11 @@ extern "C" ftar_status_t ftar_debug_bf16_cvt_check(unsigned long long* mismatche
   if (!mismatches || !first) return FTAR_ERR_INVALID_ARG;
   unsigned long long* d_bad = nullptr;
   unsigned* d_first = nullptr;
-  FTAR_CHECK_HIP(hipMalloc(&d_bad, sizeof *d_bad));
-  FTAR_CHECK_HIP(hipMalloc(&d_first, sizeof *d_first));
-  ftar_status_t st = FTAR_SUCCESS;
-  if (hipMemset(d_bad, 0, sizeof *d_bad) != hipSuccess || hipMemset(d_first, 0xff, sizeof *d_first) != hipSuccess)
+  ftar_status_t st = FTAR_SUCCESS;  // both buffers are freed on every path below
+  if (hipMalloc(&d_bad, sizeof *d_bad) != hipSuccess || hipMalloc(&d_first, sizeof *d_first) != hipSuccess)
+    st = FTAR_ERR_NO_MEMORY;
+  if (st == FTAR_SUCCESS &&
+      (hipMemset(d_bad, 0, sizeof *d_bad) != hipSuccess || hipMemset(d_first, 0xff, sizeof *d_first) != hipSuccess))
     st = FTAR_ERR_HIP;
   if (st == FTAR_SUCCESS) {
     hipLaunchKernelGGL(ftar::bf16_cvt_check_kernel, dim3(8192), dim3(256), 0, nullptr, d_bad, d_first);

@@ -18,6 +18,8 @@ import ctypes
 import json
 import os
 
+from .names import kernel_symbol  # noqa: F401  (re-exported)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FTAR_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libftar.so"))
 
@@ -149,6 +151,8 @@ _lib.ftar_comm_get_reduce_scatter.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_comm_set_allgather.argtypes = [_vp, _int]
 _lib.ftar_comm_get_allgather.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_plan_json.restype = ctypes.c_long
+_lib.ftar_debug_last_kernel.argtypes = [ctypes.c_char_p, _sz]
+_lib.ftar_debug_last_kernel.restype = ctypes.c_long
 
 
 def lib():
@@ -157,6 +161,11 @@ def lib():
 
 def version():
     return _lib.ftar_version().decode()
+
+
+def last_error():
+    """ftar_last_error(): detail of the last failure on the calling thread ("" if none)."""
+    return _lib.ftar_last_error().decode(errors="replace")
 
 
 def _check(st, what):
@@ -205,6 +214,17 @@ def _stream(s):
 
 def dtype_size(dtype):
     return _lib.ftar_dtype_size(_dt(dtype))
+
+
+def last_kernel():
+    """The kernel ftar's reduce/copy launchers last launched on this thread (ftar_debug_last_kernel), as
+    kernel_symbol() of its demangled name, or None."""
+    n = _lib.ftar_debug_last_kernel(None, 0)
+    if n < 0:
+        return None
+    buf = ctypes.create_string_buffer(n + 1)
+    _lib.ftar_debug_last_kernel(buf, n + 1)
+    return kernel_symbol(buf.value.decode())
 
 
 # ---- L3: one-device reduce ----------------------------------------------------

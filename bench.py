@@ -58,30 +58,92 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(workload):
-    """Per-launch HBM bytes measured with rocprofv3 --pmc (profiles/pmc_summary.json), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+KERNEL_SOURCES = ("allreduce-over-mpi_amd/csrc/reduce_impl.h", "allreduce-over-mpi_amd/csrc/reduce_kernels.hip")
+
+
+def kernel_source_digest(root=ROOT):
+    """sha256 (16 hex digits) of the reduce kernels' sources: a PMC measurement belongs to the kernels
+    these sources compile to, so bench.py and tools/pmc_summary.py both stamp it."""
+    import hashlib
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(workload, kernel, summary=None):
+    """Per-launch HBM bytes of `workload` measured with rocprofv3 --pmc (profiles/pmc_summary.json) -- only
+    when that measurement was taken on the kernel this run launched (same template id, same kernel sources).
+    Returns (bytes or None, provenance dict): a measurement of another kernel is never reported as this one's."""
+    p = summary or os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(p) as f:
-            d = json.load(f)
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+            e = json.load(f).get(workload)
     except (OSError, ValueError):
-        return None
+        e = None
+    if not e:
+        return None, {"traffic_note": f"no PMC measurement of {workload} in profiles/pmc_summary.json"}
+    digest = kernel_source_digest()
+    src = {"file": "profiles/pmc_summary.json", "kernel": e.get("kernel"), "commit": e.get("commit"),
+           "kernel_sources_sha": e.get("kernel_sources_sha"), "profiles": e.get("source")}
+    if e.get("kernel") != kernel:
+        return None, {"traffic_note": f"the PMC summary measured {e.get('kernel')}; this run launched {kernel}",
+                      "traffic_source": src}
+    if e.get("kernel_sources_sha") != digest:
+        return None, {"traffic_note": f"the PMC summary was taken on kernel sources {e.get('kernel_sources_sha')}; "
+                                      f"this tree's are {digest}", "traffic_source": src}
+    return e.get("hbm_bytes_per_launch"), {"traffic_source": src}
+
+
+def host_cores():
+    """The CPU this process may actually use: its affinity set and its cgroup quota (cpu.max, v2; cfs
+    quota/period, v1), next to the machine's count.  os.cpu_count() counts the whole machine, which on a
+    shared GPU box is many times the share a job gets."""
+    info = {"machine_cpus": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = None
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    info["cgroup_quota_cpus"] = round(quota, 2) if quota else None
+    avail = [v for v in (info["affinity_cpus"], quota) if v]
+    info["available_cpus"] = round(min(avail), 2) if avail else info["machine_cpus"]
+    return info
 
 
 def cpu_baseline(k, n, seconds):
-    """The reference's reduce_sum<float> (mpi_mod.hpp:812, 14 OpenMP threads) on this host,
-    built from the unmodified header into oracle/_ref/ref_golden; else the oracle port."""
+    """The reference's reduce_sum<float> (mpi_mod.hpp:812, 14 OpenMP threads, :820) on this host,
+    built from the unmodified header into oracle/_ref/ref_golden; else the oracle port.  `cores` = the
+    threads it ran; `cores_available` = what this process may use (affinity, cgroup quota)."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
-    ncpu = os.cpu_count() or 1
+    hc = host_cores()
     if os.path.exists(ref):
         try:
             out = subprocess.run([ref, "bench", "--k", str(k), "--n", str(n), "--seconds", str(seconds)],
                                  capture_output=True, text=True, timeout=seconds * 6 + 120, check=True).stdout
             d = json.loads(out.strip().splitlines()[-1])
             return {"value": round(d["GBps_best"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+                    "cores_available": hc,
                     "sample": f"FlexTree::reduce_sum<float> k={k} n={n} fp32, best of {d['iters']} calls in ~{seconds:.0f}s "
-                              f"(mean {d['GBps_mean']:.2f} GB/s), host nproc={ncpu}"}
+                              f"(mean {d['GBps_mean']:.2f} GB/s); {d['threads']} OpenMP threads (mpi_mod.hpp:820) on "
+                              f"{hc['available_cpus']} available CPUs (affinity {hc['affinity_cpus']}, cgroup quota "
+                              f"{hc['cgroup_quota_cpus']}, machine {hc['machine_cpus']})"}
         except Exception as e:  # fall through to the port
             sys.stderr.write(f"reference cpu baseline failed: {e}\n")
     import numpy as np
@@ -97,7 +159,8 @@ def cpu_baseline(k, n, seconds):
         best = min(best, time.perf_counter() - t0)
         iters += 1
     return {"value": round((k + 1) * m * 4 / best / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"oracle reduce k={k} n={m} fp32 single thread, best of {iters}, host nproc={ncpu}"}
+            "cores_available": hc,
+            "sample": f"oracle reduce k={k} n={m} fp32 single thread, best of {iters}"}
 
 
 def bench_single(a):
@@ -150,6 +213,7 @@ def bench_single(a):
         return e0.elapsed_time(e1) / steps, time.perf_counter() - t0   # one kernel per step, same stream
 
     ms, wall = run(a.steps, a.warmup, rotate=True)
+    kernel = ftar.last_kernel()   # the kernel those launches ran (the PMC traffic must be this one's)
     ms_same, _ = run(a.steps, a.warmup, rotate=False)
     algo_bytes = (k + 1) * n * esz
     gbps = algo_bytes / (ms * 1e-3) / 1e9
@@ -175,6 +239,7 @@ def bench_single(a):
         check = "bit-exact" if ok else "MISMATCH"
 
     workload = f"reduce_k{k}_{a.dtype}_n{n}"
+    traffic, prov = pmc_traffic(workload, kernel)
     res = {
         "metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X",
         "value": round(gbps, 2), "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": a.warmup,
@@ -184,7 +249,8 @@ def bench_single(a):
                    "elements_per_bucket": n, "bucket_bytes": n * esz, "algorithmic_bytes_per_step": algo_bytes,
                    "buffer_sets": sets},
         "roofline": {"bound": "hbm", "achieved": round(gbps, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(workload)},
+                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kernel,
+                     "kernel_sources_sha": kernel_source_digest(), **prov},
         "same_buffers": {"GBps": round(gbps_same, 2), "ms_per_step": round(ms_same, 5),
                          "note": "every step on set 0 (the reference harness's loop); the Infinity Cache absorbs "
                                  "part of the rewritten destination, so this overstates HBM"},
@@ -211,9 +277,11 @@ def bench_single(a):
             torch.cuda.synchronize()
             return e0.elapsed_time(e1) / reps
         t = timed_k(lambda i: sd[i].data_ptr())
+        kern = ftar.last_kernel()
         bw = (kk + 1) * n * esz / (t * 1e-3) / 1e9
+        tr, pv = pmc_traffic(f"reduce_k{kk}_{a.dtype}_n{n}", kern)
         sweep[kk] = {"ms": round(t, 4), "GBps": round(bw, 1), "frac": round(bw / HBM_PEAK_GBPS, 4),
-                     "traffic": pmc_traffic(f"reduce_k{kk}_{a.dtype}_n{n}")}
+                     "kernel": kern, "traffic": tr, **pv}
         if kk == 8 and not a.sweep:
             # in place (destination = source 0): the width-8 tree's fold in an MPI_IN_PLACE AllReduce, whose own
             # block is operand and result; same bytes, (k+1) x n x 4 (the values grow; timing only)
@@ -278,15 +346,21 @@ def link_rate_from_probe(probe, world):
     return max(rates) if rates else None
 
 
+XGMI_CONVENTION = ("achieved = busBW = algBW x 2(P-1)/P: the bytes one rank sends (and, at the same time, "
+                   "receives) per second; peak = links x 76.8 GB/s, the ONE-direction rate of a 153.6 GB/s "
+                   "bidirectional xGMI link")
+
+
 def allreduce_roofline(world, gpus, bucket, ms, links, probe_link_gbps=None):
     """Roofline object of one N>1 AllReduce line (ms per call, bucket bytes per rank).
 
     - P = 1: nothing crosses a link; the call is one pass over the bucket (read + write), so the bound is
       HBM and achieved = 2 * bucket / t.
     - ranks sharing GPUs (the --host-comm rehearsal): neither an xGMI nor a per-GPU HBM figure; None.
-    - P > 1: busBW = algBW * 2(P-1)/P (bytes each rank sends, and receives, per second) against
-      links x per-link rate in ONE direction: the probe's measured rate when it ran, else the spec
-      76.8 GB/s (153.6 GB/s bidirectional).  A probe rate the run beats falls back to the spec.
+    - P > 1: busBW = algBW * 2(P-1)/P (bytes each rank sends, and receives, per second) against the SPEC
+      peak, links x 76.8 GB/s per direction (153.6 GB/s bidirectional).  The xGMI probe's measured per-link
+      rate, when the run has one, only gives a second ratio, `frac_of_probe`: a slow or under-driven probe
+      must not flatter `frac`.
     Never returns a frac outside (0, 1]: a denominator the work exceeds does not describe it, and the
     object then carries frac None and says why."""
     if ms <= 0 or bucket <= 0:
@@ -301,20 +375,54 @@ def allreduce_roofline(world, gpus, bucket, ms, links, probe_link_gbps=None):
         return None
     busbw = algbw * 2 * (world - 1) / world
     links = max(1, min(XGMI_LINKS, links))
-    cands = []
-    if probe_link_gbps:
-        cands.append((probe_link_gbps, "measured by ftar_xgmi_probe (this run)"))
-    cands.append((XGMI_LINK_GBPS, "spec, 153.6 GB/s bidirectional"))
-    for rate, src in cands:
-        peak = links * rate
-        if 0 < busbw / peak <= 1:
-            return {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 2), "unit": "GB/s",
-                    "frac": round(busbw / peak, 4), "traffic": None,
-                    "note": f"busBW vs {links} xGMI link(s) x {rate:.1f} GB/s per direction ({src})"}
-    return {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(links * XGMI_LINK_GBPS, 2),
-            "unit": "GB/s", "frac": None, "traffic": None,
-            "note": f"busBW exceeds {links} link(s) x {XGMI_LINK_GBPS} GB/s per direction: the link count "
-                    "does not describe this run's data movement; no fraction reported"}
+    peak = links * XGMI_LINK_GBPS
+    res = {"bound": "xgmi", "achieved": round(busbw, 2), "peak": round(peak, 2), "unit": "GB/s",
+           "frac": round(busbw / peak, 4) if busbw <= peak else None, "traffic": None,
+           "direction_convention": XGMI_CONVENTION,
+           "note": f"busBW vs {links} xGMI link(s) x {XGMI_LINK_GBPS} GB/s per direction (spec)"}
+    if busbw > peak:
+        res["note"] = (f"busBW exceeds {links} link(s) x {XGMI_LINK_GBPS} GB/s per direction: the link count "
+                       "does not describe this run's data movement; no fraction reported")
+    if probe_link_gbps and probe_link_gbps > 0:
+        res["probe_peak"] = round(links * probe_link_gbps, 2)
+        res["frac_of_probe"] = round(busbw / (links * probe_link_gbps), 4)
+        res["probe_note"] = (f"{links} link(s) x {probe_link_gbps:.1f} GB/s, the per-link one-direction rate "
+                             "ftar_xgmi_probe measured in this run (a ratio to what copy kernels reached, not "
+                             "to the hardware)")
+    return res
+
+
+def links_driven(world, topology, form):
+    """xGMI links one rank drives at once: every peer in the one-round forms (direct, collective, peer);
+    in the reference's rounds ("stages"), one neighbour (ring) or the widest stage's group (tree).
+    `topology` is the str() of a Topo ("ring", "2,4", "2,2+1")."""
+    if form.split(":")[0] != "stages":
+        return min(XGMI_LINKS, world - 1)
+    if topology == "ring":
+        return 1
+    widths = [int(w) for w in topology.split("+")[0].split(",")]
+    return min(XGMI_LINKS, max(widths) - 1)
+
+
+RCCL_P2P_FORMS = ("direct", "stages")   # ncclSend/ncclRecv both ways ("collective" ends in ncclAllGather)
+
+
+def rccl_p2p_best(sweep, world, gpus, bucket, links_of):
+    """The fastest validated sweep entry whose data moved by RCCL point-to-point (north_star's transport:
+    ncclSend/ncclRecv, forms "direct", "direct:cusN", "stages"), with its roofline -- reported next to the
+    headline, which may be an IPC peer form, so the RCCL path is graded on its own.  links_of(entry) gives the
+    links one rank drives in that entry's form.  None when no such entry validated."""
+    ok = [r for r in sweep if "ms" in r and r.get("check") == "ok" and r.get("form", "").split(":")[0] in RCCL_P2P_FORMS]
+    if not ok:
+        return None
+    b = min(ok, key=lambda r: r["ms"])
+    alg = bucket / (b["ms"] * 1e-3) / 1e9
+    return {"topology": b["topology"], "chunk_bytes": b["chunk_bytes"], "form": b["form"], "ms": b["ms"],
+            "algbw_GBps_per_rank": round(alg, 2),
+            "busbw_GBps_per_rank": round(alg * 2 * (world - 1) / world if world > 1 else alg, 2),
+            "roofline": allreduce_roofline(world, gpus, bucket, b["ms"], links_of(b)),
+            "note": "fastest validated sweep entry moved by RCCL ncclSend/ncclRecv (sweep timing: "
+                    "min(5, steps) calls after 1 warmup)"}
 
 
 def _factorizations(n):
@@ -377,6 +485,8 @@ def bench_distributed(a):
         if state["line"] is not None:
             res = dict(state["line"])
             res["watchdog"] = f"run cut at {budget:.0f}s in phase '{state['phase']}'; headline = last complete measurement"
+            res["stage_wall_s"] = dict(stage_t, **({state["major"][0] + " (cut)": round(time.time() - state["major"][1], 2)}
+                                                   if state.get("major") else {}))
             emit(res)
         sys.stdout.flush()
         sys.stderr.flush()
@@ -384,14 +494,30 @@ def bench_distributed(a):
 
     threading.Thread(target=watchdog, daemon=True).start()
 
-    def phase(name):
-        """progress on stderr (rank 0): a long N>1 run never looks idle"""
+    stage_t = {}   # major stage -> wall seconds (this rank), reported as stage_wall_s
+
+    def phase(name, major=True):
+        """progress on stderr (rank 0): a long N>1 run never looks idle; major stages are timed"""
+        now = time.time()
+        if major:
+            last = state.get("major")
+            if last is not None:
+                stage_t[last[0]] = round(stage_t.get(last[0], 0.0) + now - last[1], 2)
+            state["major"] = (name, now)
         state["phase"] = name
         if rank == 0:
             sys.stderr.write(f"[bench {time.time() - t_start:7.1f}s] {name}\n")
             sys.stderr.flush()
 
     dist.init_process_group("gloo")   # host-side barrier/max only; the data path is ftar+RCCL
+
+    def all_errors(err):
+        """every rank's view of a failure (its exception and ftar_last_error), gathered over gloo, so one
+        driver record diagnoses a first RCCL contact that failed on some rank"""
+        mine = {"rank": rank, "error": err or "", "ftar_last_error": ftar.last_error()}
+        allv = [None] * world
+        dist.all_gather_object(allv, mine)
+        return allv
     if a.host_comm or world > torch.cuda.device_count():
         # rehearsal: ranks share the visible GPUs, IPC peer forms over a gloo-bootstrapped communicator;
         # exercises this whole function at P > 1 on a 1-GPU box (timings are not xGMI numbers).  Without
@@ -399,7 +525,7 @@ def bench_distributed(a):
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    comm, rccl_error = None, None
+    comm, rccl_error, rccl_ranks = None, None, None
     if not a.host_comm:
         try:
             comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
@@ -408,6 +534,7 @@ def bench_distributed(a):
         ok = torch.tensor([0 if rccl_error else 1], dtype=torch.int32)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank takes the same path
         if not ok.item():
+            rccl_ranks = all_errors(rccl_error)
             # RCCL could not come up on some rank: the peer forms over a gloo-bootstrapped communicator still
             # move the data over xGMI (IPC), so the run keeps a measured line
             if comm is not None:
@@ -636,14 +763,7 @@ def bench_distributed(a):
 
     def make_result(ms, topo_, chunk, form, ok, steps, warmup, extra):
         algbw, busbw = bws(ms)
-        # links one rank drives at once: every peer in the one-round (direct/collective/peer) forms; in the
-        # reference's rounds, one neighbour (ring) or the widest stage's group (tree)
-        if form != "stages":
-            links = min(XGMI_LINKS, world - 1)
-        elif topo_.ring:
-            links = 1
-        else:
-            links = min(XGMI_LINKS, max(topo_.widths) - 1)
+        links = links_driven(world, str(topo_), form)
         probe = state.get("line", {}).get("xgmi_probe_GBps") if isinstance(state.get("line"), dict) else None
         roof = allreduce_roofline(world, torch.cuda.device_count(), bucket, ms, links,
                                   link_rate_from_probe(probe, world))
@@ -668,6 +788,7 @@ def bench_distributed(a):
         }
         if rccl_error:
             res["rccl_init_error"] = rccl_error
+            res["rccl_error_by_rank"] = rccl_ranks
         res.update(extra)
         return res
 
@@ -695,6 +816,7 @@ def bench_distributed(a):
         # the first RCCL p2p transfers of the run failed: the IPC peer forms over a host-bootstrapped
         # communicator still move the data over xGMI, so the run keeps a measured line (the broken RCCL
         # communicator is left alone: destroying it could block)
+        rccl_ranks = all_errors(err)
         rccl_error = f"default configuration over RCCL failed: {err or 'on another rank'}"
         sys.stderr.write(f"[bench rank {rank}] {rccl_error}; falling back to the host-bootstrapped peer forms\n")
         a.host_comm = True
@@ -788,7 +910,7 @@ def bench_distributed(a):
             sweep.append({"skipped": f"sweep budget {sweep_budget:.0f}s reached ({len(plan) - len(sweep)} left)"})
             break
         key = str(t)
-        phase(f"sweep {key} {form} {chunk}")
+        phase(f"sweep {key} {form} {chunk}", major=False)
         try:
             fn = run_with(t, chunk, form)
             ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
@@ -818,11 +940,20 @@ def bench_distributed(a):
             state["line"]["config_selection"] = "default (sweep best not faster when re-timed)"
     else:
         state["line"]["config_selection"] = "default (fastest validated configuration)"
-    # the roofline again, now against the probe's per-link rate if the sweep reached the probe
+    # the roofline again, now with the probe's per-link rate (frac_of_probe) if the sweep reached the probe
     hl = state["line"]
     hl["roofline"] = allreduce_roofline(world, torch.cuda.device_count(), bucket, hl["ms_per_step"],
                                         hl["config"]["xgmi_links"],
                                         link_rate_from_probe(hl.get("xgmi_probe_GBps"), world))
+    # north_star's transport is RCCL point-to-point: its best validated configuration is graded on its own,
+    # whatever form won the headline
+    if not a.host_comm:
+        hl["rccl_p2p_best"] = rccl_p2p_best(sweep + [{**default_info, "check": "ok" if ok_default else "x"}],
+                                            world, torch.cuda.device_count(), bucket,
+                                            lambda r: links_driven(world, r["topology"], r["form"]))
+        if hl["rccl_p2p_best"] is not None:
+            hl["rccl_p2p_best"]["is_headline"] = all(hl["config"][f] == hl["rccl_p2p_best"][f]
+                                                     for f in ("form", "topology", "chunk_bytes"))
 
     # phase timelines (rank 0's view) of the default and of the fastest validated configuration of each form:
     # where a call's time goes (transfer rounds vs folds vs barriers), for the next round's tuning
@@ -903,6 +1034,8 @@ def bench_distributed(a):
         state["line"]["reference_cpu_mpi"] = reference_mpi_path(world)
     dist.barrier()
 
+    phase("end")
+    state["line"]["stage_wall_s"] = dict(stage_t)
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
     state["done"] = True

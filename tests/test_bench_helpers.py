@@ -55,7 +55,9 @@ def test_roofline_xgmi_frac_in_range(world, links):
     assert r["frac"] is None and "no fraction" in r["note"]
 
 
-def test_roofline_uses_probe_rate_and_falls_back_to_spec():
+def test_roofline_frac_is_against_the_spec_and_the_probe_only_adds_a_ratio():
+    """frac is always busBW / (links x 76.8 GB/s spec, one direction); the probe's measured per-link
+    rate gives only `frac_of_probe`, so a slow or under-driven probe cannot raise frac."""
     import bench
     probe = {"read_one_peer": [60.0, 62.0], "read_all_peers": [400.0, 410.0], "write_one_peer": [50.0, 51.0],
              "write_all_peers": [350.0, 360.0], "note": "x"}
@@ -64,14 +66,105 @@ def test_roofline_uses_probe_rate_and_falls_back_to_spec():
     bucket = 1 << 30
     ms = bucket * 2 * 7 / 8 / (7 * 50.0 * 1e9) * 1e3   # busBW 50 GB/s per link
     r = bench.allreduce_roofline(8, 8, bucket, ms, 7, rate)
-    assert "ftar_xgmi_probe" in r["note"] and r["peak"] == pytest.approx(420.0, rel=1e-3)
-    assert r["frac"] == pytest.approx(50.0 / 60.0, abs=1e-4)
-    ms2 = bucket * 2 * 7 / 8 / (7 * 70.0 * 1e9) * 1e3  # beats the probe's rate: spec denominator
-    r2 = bench.allreduce_roofline(8, 8, bucket, ms2, 7, rate)
-    assert "spec" in r2["note"] and 0 < r2["frac"] <= 1
+    assert r["peak"] == pytest.approx(7 * 76.8) and r["frac"] == pytest.approx(50.0 / 76.8, abs=1e-4)
+    assert r["probe_peak"] == pytest.approx(420.0) and r["frac_of_probe"] == pytest.approx(50.0 / 60.0, abs=1e-4)
+    assert "ONE-direction" in r["direction_convention"]
+    slow = bench.allreduce_roofline(8, 8, bucket, ms, 7, 10.0)   # a bad probe: frac unchanged
+    assert slow["frac"] == r["frac"] and slow["frac_of_probe"] > 1
+    assert "frac_of_probe" not in bench.allreduce_roofline(8, 8, bucket, ms, 7)
     assert bench.link_rate_from_probe(None, 8) is None
     assert bench.link_rate_from_probe({"error": "x"}, 8) is None
     assert bench.link_rate_from_probe(probe, 1) is None
+
+
+def test_links_driven():
+    import bench
+    assert bench.links_driven(8, "8", "direct") == 7
+    assert bench.links_driven(8, "ring", "peer-read-reg:dma") == 7
+    assert bench.links_driven(8, "ring", "stages") == 1
+    assert bench.links_driven(8, "2,4", "stages") == 3
+    assert bench.links_driven(5, "2,2+1", "stages") == 1
+    assert bench.links_driven(2, "2", "direct:cus224") == 1
+
+
+def test_rccl_p2p_best_is_reported_when_a_peer_form_wins():
+    """VERDICT r2 #3: the headline may be an IPC peer form; the fastest validated RCCL ncclSend/ncclRecv
+    configuration is reported next to it with its own roofline.  Invalid entries, errors and the collective
+    form (ncclAllGather) do not count."""
+    import bench
+    bucket = 1 << 30
+    sweep = [
+        {"topology": "8", "chunk_bytes": 16 << 20, "form": "direct", "ms": 6.0, "check": "ok"},
+        {"topology": "8", "chunk_bytes": 1 << 20, "form": "direct", "ms": 5.5, "check": "MISMATCH (sample)"},
+        {"topology": "8", "chunk_bytes": 4 << 20, "form": "direct:cus224", "ms": 5.8, "check": "ok"},
+        {"topology": "8", "chunk_bytes": 16 << 20, "form": "collective", "ms": 5.0, "check": "ok"},
+        {"topology": "ring", "chunk_bytes": 16 << 20, "form": "stages", "ms": 40.0, "check": "ok"},
+        {"topology": "8", "chunk_bytes": 16 << 20, "form": "peer-write-reg", "ms": 4.0, "check": "ok"},
+        {"topology": "2,4", "chunk_bytes": 16 << 20, "form": "direct", "error": "ncclSend failed"},
+        {"skipped": "sweep budget"},
+    ]
+    best = bench.rccl_p2p_best(sweep, 8, 8, bucket, lambda r: bench.links_driven(8, r["topology"], r["form"]))
+    assert best["form"] == "direct:cus224" and best["chunk_bytes"] == 4 << 20 and best["ms"] == 5.8
+    assert best["roofline"]["bound"] == "xgmi" and best["roofline"]["peak"] == pytest.approx(7 * 76.8)
+    alg = bucket / 5.8e-3 / 1e9
+    assert best["busbw_GBps_per_rank"] == pytest.approx(alg * 14 / 8, rel=1e-3)
+    only_peer = [e for e in sweep if e.get("form", "").startswith("peer")]
+    assert bench.rccl_p2p_best(only_peer, 8, 8, bucket, lambda r: 7) is None
+
+
+def test_pmc_traffic_only_for_the_kernel_it_measured(tmp_path):
+    """VERDICT r2 next #1: roofline.traffic comes from profiles/pmc_summary.json only when that entry measured
+    the kernel this run launched (same template id) built from the same kernel sources; otherwise None and a
+    note saying which kernel the summary holds."""
+    import json
+    import bench
+    dig = bench.kernel_source_digest()
+    k = "reduce_lds_kernel<F32Sum, 2, 1, 2, 2, true>"
+    entry = {"kernel": k, "commit": "abc", "kernel_sources_sha": dig, "hbm_bytes_per_launch": 805339648.0,
+             "source": "profiles/r03/final"}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({"reduce_k2_f32_n67108864": entry}))
+    t, prov = bench.pmc_traffic("reduce_k2_f32_n67108864", k, str(p))
+    assert t == 805339648.0 and prov["traffic_source"]["commit"] == "abc"
+    t, prov = bench.pmc_traffic("reduce_k2_f32_n67108864", "reduce_lds_kernel<F32Sum, 2, 4, 4, 2, true>", str(p))
+    assert t is None and k in prov["traffic_note"]
+    p.write_text(json.dumps({"reduce_k2_f32_n67108864": dict(entry, kernel_sources_sha="0" * 16)}))
+    t, prov = bench.pmc_traffic("reduce_k2_f32_n67108864", k, str(p))
+    assert t is None and "kernel sources" in prov["traffic_note"]
+    t, prov = bench.pmc_traffic("reduce_k8_f32_n67108864", k, str(p))
+    assert t is None and "no PMC measurement" in prov["traffic_note"]
+
+
+def test_committed_pmc_summary_names_kernel_commit_and_sources():
+    """Every entry of the committed summary says which kernel, commit and kernel sources it measured."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "pmc_summary.json")) as f:
+        d = json.load(f)
+    for key, e in d.items():
+        assert e["kernel"].startswith("reduce_"), key
+        assert e.get("commit") and e.get("kernel_sources_sha"), key
+        assert 0.99 < e["traffic_over_algorithmic"] < 1.05, key
+
+
+def test_kernel_symbol_normalises_rocprof_names():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "allreduce-over-mpi_amd", "ftar"))
+    from names import kernel_symbol
+    raw = ("void ftar::(anonymous namespace)::reduce_lds_kernel<ftar::(anonymous namespace)::F32Sum, 8, 4, 2, 2, "
+           "true>(ftar::(anonymous namespace)::Srcs<8>, void*, unsigned long, int, int)")
+    assert kernel_symbol(raw) == "reduce_lds_kernel<F32Sum, 8, 4, 2, 2, true>"
+    assert kernel_symbol("void ftar::(anonymous namespace)::gather_kernel<true>(ftar::SegArgs, int)") == \
+        "gather_kernel<true>"
+
+
+def test_host_cores_reports_the_share_not_the_machine():
+    """VERDICT r2 #5: the CPU baseline states the cores this process may use (affinity, cgroup quota)."""
+    import bench
+    hc = bench.host_cores()
+    assert hc["machine_cpus"] == os.cpu_count()
+    assert hc["affinity_cpus"] == len(os.sched_getaffinity(0))
+    assert 0 < hc["available_cpus"] <= hc["machine_cpus"]
 
 
 def test_reference_mpi_path_runs_the_reference_on_the_host():

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: smoke, GPU tests, bench, rocprof. Every GPU step has its
 # own time limit; a fault/abort/timeout (exit >= 124) stops the script there.
-# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc ktree host hostipc hosttests dist1 dist2h dist4h dist2f peer2
+# Usage: tools/gpu_run.sh [steps...]   steps: smoke tests testsall bench sweep prof pmc final ktree host hostipc hosttests dist1 dist2h dist4h dist2f peer2
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -26,6 +26,13 @@ for s in "${steps[@]}"; do
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     sweep) run bench_sweep 600 python bench.py --steps 20 --warmup 5 --sweep --no-cpu-baseline ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    # one tree, one box: the bench line, its kernel trace and both PMC passes, plus the tree's identity
+    # (FTAR_COMMIT from the caller; the box has no .git) for tools/pmc_summary.py --meta
+    final) python3 -c "import json, bench; json.dump({'commit': '${FTAR_COMMIT:-unknown}', 'kernel_sources_sha': bench.kernel_source_digest()}, open('gpurun_out/pmc_meta.json', 'w'))" &&
+           run bench 600 python bench.py --steps 20 --warmup 5 &&
+           run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline &&
+           run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
          run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     ktree) run kbench_tree 600 python tools/kbench.py --rounds 8 --dtypes f32,bf16 --shapes "8;2,4;4,2;2,2,2;4;2,2;16;4,4;2,2,2,2" ;;

@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes of the bench kernel from rocprofv3 PMC passes -> profiles/pmc_summary.json.
+"""Per-launch HBM bytes of the bench kernels from rocprofv3 PMC passes -> profiles/pmc_summary.json.
 
-    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [--elements N] [--k 2,8]
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [--elements N] [--k 2,8] [--meta META_JSON] [--source DIR]
 
 One entry per k (bench.py launches the k = 2 headline and the k = 8 line item in the same process); entries
-of other workloads already in the summary are kept.
+of other workloads already in the summary are kept.  Every entry names the kernel it measured (its template
+id, as bench.py's roofline reports the kernel it timed), the sha of the kernel sources and the commit of the
+tree the passes ran on (META_JSON, written on the GPU box by tools/gpu_run.sh final): bench.py reports the
+traffic only for that kernel built from those sources.
 
 FETCH_SIZE and WRITE_SIZE come from separate `rocprofv3 --pmc` passes (tools/gpu_run.sh pmc).  Per the
 gfx950 correction in MI355X_MICROARCH.md: read bytes = 2 x FETCH_SIZE x 1024, write bytes = WRITE_SIZE x 1024.
@@ -14,16 +17,25 @@ import csv
 import json
 import os
 import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "allreduce-over-mpi_amd", "ftar"))
+from names import kernel_symbol  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("fetch_csv")
 ap.add_argument("write_csv")
 ap.add_argument("--elements", type=int, default=1 << 26)
 ap.add_argument("--k", default="2,8")
-ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                              "profiles", "pmc_summary.json"))
+ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+ap.add_argument("--meta", default="", help="JSON with commit and kernel_sources_sha of the measured tree")
 ap.add_argument("--source", default="")
 a = ap.parse_args()
+meta = {}
+if a.meta:
+    with open(a.meta) as f:
+        meta = json.load(f)
 
 
 def rows(path, counter, k):
@@ -44,13 +56,18 @@ except (OSError, ValueError):
 for k in (int(x) for x in a.k.split(",")):
     if not values(a.fetch_csv, "FETCH_SIZE", k):
         continue
+    kernels = {kernel_symbol(r["Kernel_Name"]) for r in rows(a.fetch_csv, "FETCH_SIZE", k)}
+    kernels_w = {kernel_symbol(r["Kernel_Name"]) for r in rows(a.write_csv, "WRITE_SIZE", k)}
+    if len(kernels) != 1 or kernels != kernels_w:
+        sys.exit(f"k={k}: the two passes measured different kernels: {kernels} / {kernels_w}")
     fetch = statistics.median(values(a.fetch_csv, "FETCH_SIZE", k))
     write = statistics.median(values(a.write_csv, "WRITE_SIZE", k))
     rd, wr = 2 * fetch * 1024, write * 1024
     key = f"reduce_k{k}_f32_n{a.elements}"
     res[key] = {
-        "kernel": rows(a.fetch_csv, "FETCH_SIZE", k)[0]["Kernel_Name"].replace("ftar::(anonymous namespace)::", "")
-                                                                     .replace("void ", "").split("(")[0],
+        "kernel": kernels.pop(),
+        "commit": meta.get("commit"),
+        "kernel_sources_sha": meta.get("kernel_sources_sha"),
         "launches": len(values(a.fetch_csv, "FETCH_SIZE", k)),
         "FETCH_SIZE_kB_median": fetch, "WRITE_SIZE_kB_median": write,
         "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
