@@ -465,7 +465,7 @@ def bench_distributed(a):
     t_start = time.time()
     budget = float(os.environ.get("FTAR_BENCH_BUDGET_S", "300"))
     sweep_budget = float(os.environ.get("FTAR_BENCH_SWEEP_S", "150"))
-    state = {"line": None, "printed": False, "done": False, "phase": "init"}
+    state = {"line": None, "printed": False, "done": False, "phase": "init", "major": ("init", t_start)}
     lock = threading.Lock()
 
     def emit(res):
