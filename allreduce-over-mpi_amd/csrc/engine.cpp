@@ -642,7 +642,7 @@ size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
 ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t dt, ftar_op_t op, const Plan& plan,
                                   ftar_comm* c, hipStream_t stream) {
   const size_t esz = dtype_size(dt), bytes = count * esz;
-  FTAR_RETURN_IF(ensure_xbuf(c, bytes));
+  FTAR_RETURN_IF(ensure_xbuf(c, bytes));  // collective, before the first barrier
   Transport* tp = c->tp.get();
   char* X = static_cast<char*>(c->xbuf);
   const std::vector<char*>& Xq = c->xpeers;
@@ -651,10 +651,29 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   const size_t P = (size_t)c->nranks, split = plan.split;
   const size_t chunk = host_peer_piece(c, split, esz);
   const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
-  FTAR_RETURN_IF(grow_events(c, 5 + 2 * m));
+  // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
+  // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
+  // so all of them leave the call at the same barrier instead of some waiting in the next.
+  ftar_status_t st = grow_events(c, 5 + 2 * m);
+  auto work = [&](auto&& fn) {
+    if (st == FTAR_SUCCESS) st = fn();
+  };
+  auto sync = [&]() -> bool {  // a barrier; false: some rank failed, leave the call
+    bool all_ok = true;
+    const ftar_status_t b = tp->barrier_status(c->comm_s, st == FTAR_SUCCESS, &all_ok);
+    if (b != FTAR_SUCCESS) {  // the host collective itself failed: nothing left to agree with
+      if (st == FTAR_SUCCESS) st = b;
+      return false;
+    }
+    if (!all_ok && st == FTAR_SUCCESS) {
+      set_error("peer_allreduce_host: another rank failed", __FILE__, __LINE__);
+      st = FTAR_ERR_INTERNAL;
+    }
+    return all_ok;
+  };
   hipEvent_t* ev = c->events.data();
-  auto ev_h = [&](size_t k) { return ev[5 + 2 * k]; };      // piece k is in my X
-  auto ev_g = [&](size_t k) { return ev[5 + 2 * k + 1]; };  // piece k is final in my X
+  auto ev_h = [&](size_t k) { return c->events[5 + 2 * k]; };      // piece k is in my X
+  auto ev_g = [&](size_t k) { return c->events[5 + 2 * k + 1]; };  // piece k is final in my X
   auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {  // piece k of every block, clipped
     for (size_t b = 0; b < P; ++b) {
       const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
@@ -662,43 +681,55 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     }
     return FTAR_SUCCESS;
   };
-  FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
-  for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
-  c->nmarks = 0;
-  FTAR_RETURN_IF(mark(c, "start", c->comm_s));
-  for (size_t k = 0; k < m; ++k) {
-    FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
-      FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
-      return FTAR_SUCCESS;
-    }));
-    FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
-  }
-  FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
-  FTAR_RETURN_IF(tp->barrier(c->comm_s));  // piece 0 is in everywhere
-  FTAR_RETURN_IF(mark(c, "piece 0 in", c->comm_s));
+  work([&]() -> ftar_status_t {
+    ev = c->events.data();
+    FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
+    for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
+    c->nmarks = 0;
+    FTAR_RETURN_IF(mark(c, "start", c->comm_s));
+    for (size_t k = 0; k < m; ++k) {
+      FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
+        return FTAR_SUCCESS;
+      }));
+      FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
+    }
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
+    return FTAR_SUCCESS;
+  });
+  if (!sync()) return st;  // piece 0 is in everywhere
+  work([&] { return mark(c, "piece 0 in", c->comm_s); });
   std::vector<Segment> segs;
   for (size_t k = 0; k < m; ++k) {
     const size_t lo = k * chunk;
-    for (const ReduceItem& r : rs.reduces)
-      FTAR_RETURN_IF(peer_fold(
-          r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
-          [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
-    if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
-    FTAR_RETURN_IF(tp->barrier(c->comm_s));  // piece k folded everywhere (and piece k+1 in)
-    segs.clear();
-    for (const Transfer& x : ag.recvs)
-      if (x.len > lo)
-        segs.push_back({Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
-    if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
-    FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
-    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
-    FTAR_RETURN_IF(for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
-      FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+    work([&]() -> ftar_status_t {
+      for (const ReduceItem& r : rs.reduces)
+        FTAR_RETURN_IF(peer_fold(
+            r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
+            [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
+      if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
       return FTAR_SUCCESS;
-    }));
+    });
+    if (!sync()) return st;  // piece k folded everywhere (and piece k+1 in)
+    work([&]() -> ftar_status_t {
+      segs.clear();
+      for (const Transfer& x : ag.recvs)
+        if (x.len > lo)
+          segs.push_back(
+              {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
+      if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
+      FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
+      return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(
+            hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+        return FTAR_SUCCESS;
+      });
+    });
   }
-  FTAR_RETURN_IF(mark(c, "pieces folded and gathered", c->comm_s));
-  FTAR_RETURN_IF(tp->barrier(c->comm_s));  // no peer reads my X after the call
+  work([&] { return mark(c, "pieces folded and gathered", c->comm_s); });
+  if (!sync()) return st;  // no peer reads my X after the call
+  FTAR_RETURN_IF(st);
   FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
@@ -891,6 +922,23 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   FTAR_RETURN_IF(resolve_plan(c, topo, count, esz, form, &planp));
   const Plan& plan = *planp;
   const size_t nst = plan.stages.size();
+  if (!c->tp->async_p2p()) {
+    // A host-bootstrapped communicator's paths differ in their host barriers (peer read: 3, write: 2,
+    // host buffers pipelined: m + 2, whole bucket: 3), so every rank must take the same one with the same
+    // pieces: the settings that choose it are compared first, and a mismatch fails the call on every rank
+    //  instead of pairing barriers of different phases.
+    const uint64_t cfg[6] = {(uint64_t)c->peer_direct, (uint64_t)c->allgather, (uint64_t)c->reduce_scatter,
+                             (uint64_t)(host != nullptr), host ? (uint64_t)c->host_peer_pipeline : 0,
+                             host ? (uint64_t)host_peer_piece(c, plan.split, esz) : 0};
+    bool same = true;
+    FTAR_RETURN_IF(c->tp->agree(cfg, sizeof cfg, &same));
+    if (!same) {
+      set_error("ranks disagree on the peer form, all-gather/reduce-scatter form, FTAR_HOST_PEER_PIPELINE or the "
+                "host piece size (FTAR_HOST_CHUNK_BYTES): set them alike on every rank",
+                __FILE__, __LINE__);
+      return FTAR_ERR_INVALID_ARG;
+    }
+  }
   if (!host && c->peer_direct && peer_eligible(plan)) {
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);

@@ -176,6 +176,25 @@ class Transport {
   // rank's pointer as an address usable by kernels on its own device
   // (peers[rank] == mine).  unmap_peers undoes it.
   virtual ftar_status_t barrier(hipStream_t s) = 0;
+  // A barrier that also agrees on failures (the host transport's piece loop,
+  // engine.cpp peer_allreduce_host): mine_ok says this rank's work since the
+  // last barrier was issued without error, *all_ok that every rank's was, so
+  // all ranks leave a failed call at the same barrier instead of some waiting
+  // in the next one.  Default: the plain barrier, *all_ok = mine_ok.
+  virtual ftar_status_t barrier_status(hipStream_t s, bool mine_ok, bool* all_ok) {
+    *all_ok = mine_ok;
+    return barrier(s);
+  }
+  // Host-synchronous agreement on `bytes` of per-call settings: *same = every
+  // rank passed the same bytes.  Only the host transport's host-buffer path
+  // needs it (the pipelined and whole-bucket paths run different numbers of
+  // host barriers); elsewhere *same = true.
+  virtual ftar_status_t agree(const void* mine, size_t bytes, bool* same) {
+    (void)mine;
+    (void)bytes;
+    *same = true;
+    return FTAR_SUCCESS;
+  }
   virtual ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) = 0;
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
   // map_peers exports and opens IPC handles (false: one address space)

@@ -703,10 +703,36 @@ class HostTransport final : public Transport {
   bool async_p2p() const override { return false; }
   // everything before it on s, on every rank, is complete when it returns
   ftar_status_t barrier(hipStream_t s) override {
-    FTAR_CHECK_HIP(hipStreamSynchronize(s));
-    char mine = 1;
+    bool ok = true;
+    FTAR_RETURN_IF(barrier_status(s, true, &ok));
+    if (!ok) {
+      set_error("host transport: another rank failed before this barrier", __FILE__, __LINE__);
+      return FTAR_ERR_INTERNAL;
+    }
+    return FTAR_SUCCESS;
+  }
+  // a failed stream synchronisation is this rank's failure, reported to the others rather than returned
+  // before the host collective (which would leave them waiting in it)
+  ftar_status_t barrier_status(hipStream_t s, bool mine_ok, bool* all_ok) override {
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      set_error(std::string("host transport barrier: hipStreamSynchronize: ") + hipGetErrorString(e), __FILE__,
+                __LINE__);
+      mine_ok = false;
+    }
+    const char mine = mine_ok ? 1 : 0;
     std::vector<char> all(nranks_);
-    return gather(&mine, all.data(), 1);
+    FTAR_RETURN_IF(gather(&mine, all.data(), 1));
+    *all_ok = true;
+    for (char v : all) *all_ok = *all_ok && v == 1;
+    return FTAR_SUCCESS;
+  }
+  ftar_status_t agree(const void* mine, size_t bytes, bool* same) override {
+    std::vector<char> all((size_t)nranks_ * bytes);
+    FTAR_RETURN_IF(gather(mine, all.data(), bytes));
+    *same = true;
+    for (int q = 0; q < nranks_; ++q) *same = *same && !memcmp(all.data() + (size_t)q * bytes, mine, bytes);
+    return FTAR_SUCCESS;
   }
   ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
     if (nranks != nranks_ || rank != rank_) return FTAR_ERR_INVALID_ARG;

@@ -342,3 +342,79 @@ def test_host_buffers_random_soak(world):
         ref = oracle_lib.allreduce(ins, topo, dtype=fi.BY_NAME[dt])
         for r in range(world):
             assert res[r][i] == ref[r].tobytes(), (world, i, n, dt, topo, piece, pinned, oop, r)
+
+
+def _mismatch_worker(rank, world, port, n, q):
+    """Ranks whose host-path settings differ: the pipelined host path runs m + 2 host barriers and
+    the whole-bucket path 3, so mismatched FTAR_HOST_PEER_PIPELINE / piece sizes / peer forms would pair
+    barriers of different phases.  Every rank must get FTAR_ERR_INVALID_ARG from the same call, and the
+    communicator must stay usable for the next, matched call."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ftar
+    import ftar.dist
+    import ftar_inputs as fi
+    out = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        comm = ftar.dist.init_host_comm(device=0)
+        x = fi.fill("f32", 41, rank, n)
+        for what in ("piece", "form", "device_form"):
+            comm.peer_direct = "read"
+            comm.host_chunk_bytes = 0
+            if what == "piece":
+                comm.host_chunk_bytes = 4096 * (rank + 1)        # different piece sizes
+            elif rank == 1:
+                comm.peer_direct = "write"                       # read on rank 0, write on rank 1
+            try:
+                if what == "device_form":
+                    xt = torch.from_numpy(x.copy()).cuda()
+                    comm.allreduce(None, xt, n, "f32", "sum", topo_="1")
+                    torch.cuda.synchronize()
+                else:
+                    y = x.copy()
+                    comm.allreduce_host(None, y, n, "f32", "sum", topo_="1")
+                    torch.cuda.synchronize()
+                out[what] = "ran"
+            except ftar.FtarError as e:
+                out[what] = (e.status, "disagree" in str(e))
+            dist.barrier()
+        comm.peer_direct = "read"                                # matched again: the call works
+        comm.host_chunk_bytes = 4096
+        y = x.copy()
+        comm.allreduce_host(None, y, n, "f32", "sum", topo_="1")
+        torch.cuda.synchronize()
+        out["after"] = y.tobytes()
+        comm.destroy()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        out["error"] = traceback.format_exc()
+    q.put((rank, out))
+
+
+def test_host_path_settings_must_agree_across_ranks():
+    import ftar_inputs as fi
+    import oracle_lib
+    world, n = 2, 50_003
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_mismatch_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+        for what in ("piece", "form", "device_form"):
+            assert res[r][what] == (1, True), (r, what, res[r][what])
+    ref = oracle_lib.allreduce([fi.fill("f32", 41, r, n) for r in range(world)], "1")
+    for r in range(world):
+        assert res[r]["after"] == ref[r].tobytes(), r

@@ -8,7 +8,27 @@
 // argv[3] = k: stop after the k-th op, join every stream used so far into the
 // origin stream and end the capture there (the shortest crashing prefix).
 // argv[4] = i: skip the i-th op (which ops the crash needs).
+// drop kind 'p' (prune): simulate the capture's dependency
+// sets -- per stream the nodes its next captured op will depend on, per event
+// the set its record captured -- and skip every wait that adds nothing: all of
+// the event's nodes are already the waiting stream's dependencies or their
+// ancestors (a stream's FIRST wait, which brings it into the capture, is
+// always kept).  If the pruned replay ends its capture where the full one
+// crashes, redundant ancestor edges are what the runtime cannot handle.
+// drop kind 'l' (leaves): keep every op, but after each wait ask the runtime
+// for the stream's capture dependencies (hipStreamGetCaptureInfo_v2) and set
+// them to their leaves (hipStreamUpdateCaptureDependencies): no node then
+// depends on a node and that node's ancestor at once.  'v' prints the
+// runtime's dependency count after every wait.
+// drop kind 'f' (flat forks): right after the capture begins, every stream of
+// the op file forks from the origin stream (one event recorded there, waited
+// on by all), so no stream joins the capture through another forked stream;
+// the file's own fork waits then become ordinary cross-stream waits and the
+// dependencies stay the same (the begin event carries none).
 #include <hip/hip_runtime.h>
+
+#include <set>
+#include <vector>
 
 #include <cstdio>
 #include <cstdlib>
@@ -49,6 +69,70 @@ int main(int argc, char** argv) {
     if (!events.count(k)) CK(hipEventCreateWithFlags(&events[k], hipEventDisableTiming));
     return events[k];
   };
+  const bool leaves_only = drop.find('l') != std::string::npos, verbose = drop.find('v') != std::string::npos;
+  int leaf_removed = 0;
+  // the stream's capture dependencies reduced to their leaves; returns how many were dropped
+  auto leaf_reduce = [&](hipStream_t st, const std::string& name) -> int {
+    hipStreamCaptureStatus cs;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    CK(hipStreamGetCaptureInfo_v2(st, &cs, nullptr, nullptr, &deps, &nd));
+    if (verbose) fprintf(stderr, "replay: %s has %zu capture dependencies\n", name.c_str(), nd);
+    if (!leaves_only || cs != hipStreamCaptureStatusActive || nd < 2) return 0;
+    std::vector<hipGraphNode_t> d(deps, deps + nd);
+    std::set<hipGraphNode_t> anc;  // strict ancestors of the set's members
+    std::vector<hipGraphNode_t> st_(d.begin(), d.end());
+    while (!st_.empty()) {
+      hipGraphNode_t v = st_.back();
+      st_.pop_back();
+      size_t np = 0;
+      CK(hipGraphNodeGetDependencies(v, nullptr, &np));
+      std::vector<hipGraphNode_t> ps(np);
+      if (np) CK(hipGraphNodeGetDependencies(v, ps.data(), &np));
+      for (hipGraphNode_t u : ps)
+        if (anc.insert(u).second) st_.push_back(u);
+    }
+    std::vector<hipGraphNode_t> keep;
+    std::set<hipGraphNode_t> seen;
+    for (hipGraphNode_t v : d)
+      if (!anc.count(v) && seen.insert(v).second) keep.push_back(v);
+    if (keep.size() == nd) return 0;
+    CK(hipStreamUpdateCaptureDependencies(st, keep.data(), keep.size(), hipStreamSetCaptureDependencies));
+    return (int)(nd - keep.size());
+  };
+  // prune-mode simulation of the capture graph
+  const bool prune = drop.find('p') != std::string::npos;
+  std::vector<std::set<int>> node_deps;           // captured work nodes (M, K) and their dependencies
+  std::map<std::string, std::set<int>> sdeps;     // stream -> dependency set of its next captured op
+  std::map<std::string, bool> scap;               // stream is part of the capture
+  std::map<std::string, std::set<int>> edeps;     // event -> the set its record captured
+  std::map<std::string, bool> ecap;
+  int pruned = 0, kept_waits = 0;
+  auto closure = [&](const std::set<int>& from) {  // the set and all its ancestors
+    std::set<int> out;
+    std::vector<int> st(from.begin(), from.end());
+    while (!st.empty()) {
+      const int v = st.back();
+      st.pop_back();
+      if (!out.insert(v).second) continue;
+      for (int d : node_deps[v]) st.push_back(d);
+    }
+    return out;
+  };
+  const bool flat = drop.find('f') != std::string::npos;
+  std::vector<std::string> all_streams;  // every stream the file names, for 'f'
+  {
+    std::ifstream pre(argv[1]);
+    std::string l2;
+    std::set<std::string> seen;
+    while (std::getline(pre, l2)) {
+      std::istringstream ls(l2);
+      std::string op, x, y;
+      ls >> op >> x >> y;
+      const std::string st = op == "R" ? y : (op == "W" || op == "M" || op == "K" || op == "B" || op == "E") ? x : "";
+      if (!st.empty() && seen.insert(st).second) all_streams.push_back(st);
+    }
+  }
   std::string line;
   int n = 0;
   while (std::getline(in, line)) {
@@ -75,19 +159,63 @@ int main(int argc, char** argv) {
     }
     if (op == "B") {
       origin = x;
+      scap[x] = true;
+      sdeps[x].clear();
       CK(hipStreamBeginCapture(S(x), hipStreamCaptureModeRelaxed));
+      if (flat) {
+        hipEvent_t root;
+        CK(hipEventCreateWithFlags(&root, hipEventDisableTiming));
+        CK(hipEventRecord(root, S(x)));
+        int forked = 0;
+        for (const std::string& st : all_streams)
+          if (st != x) {
+            CK(hipStreamWaitEvent(S(st), root, 0));
+            scap[st] = true;
+            ++forked;
+          }
+        fprintf(stderr, "replay: %d streams forked from the origin at capture begin\n", forked);
+      }
     }
-    else if (op == "R") CK(hipEventRecord(E(x), S(y)));
-    else if (op == "W") CK(hipStreamWaitEvent(S(x), E(y), 0));
-    else if (op == "M") CK(hipMemcpyAsync(b, a, 256, hipMemcpyDeviceToDevice, S(x)));
-    else if (op == "K") touch<<<1, 64, 0, S(x)>>>(a);
+    else if (op == "R") {
+      edeps[x] = sdeps[y];
+      ecap[x] = scap[y];
+      CK(hipEventRecord(E(x), S(y)));
+    }
+    else if (op == "W") {
+      if (ecap[y] && !scap[x]) {  // the fork: the stream joins the capture
+        scap[x] = true;
+        sdeps[x] = edeps[y];
+      } else if (ecap[y]) {
+        const std::set<int> have = closure(sdeps[x]);
+        bool adds = false;
+        for (int v : edeps[y]) adds = adds || !have.count(v);
+        if (prune && !adds) {
+          ++pruned;
+          fprintf(stderr, "replay: pruned op %d (W %s %s: adds nothing)\n", n, x.c_str(), y.c_str());
+          ++n;
+          continue;
+        }
+        for (int v : edeps[y]) sdeps[x].insert(v);
+      }
+      ++kept_waits;
+      CK(hipStreamWaitEvent(S(x), E(y), 0));
+      leaf_removed += leaf_reduce(S(x), x);
+    }
+    else if (op == "M" || op == "K") {
+      node_deps.push_back(sdeps[x]);
+      sdeps[x] = {(int)node_deps.size() - 1};
+      if (op == "M") CK(hipMemcpyAsync(b, a, 256, hipMemcpyDeviceToDevice, S(x)));
+      else touch<<<1, 64, 0, S(x)>>>(a);
+    }
     else if (op == "E") {
       hipGraph_t g;
-      fprintf(stderr, "replay: %d ops, ending the capture\n", n);
+      fprintf(stderr, "replay: %d ops, %d waits kept, %d pruned as redundant, %d ancestor dependencies removed; "
+              "ending the capture\n", n, kept_waits, pruned, leaf_removed);
       CK(hipStreamEndCapture(S(x), &g));
       size_t nodes = 0;
       CK(hipGraphGetNodes(g, nullptr, &nodes));
-      printf("replay ok: %zu nodes (dropped '%s')\n", nodes, drop.c_str());
+      printf("replay ok: %zu nodes (mode '%s'; %d waits kept, %d pruned, %d ancestor dependencies removed)\n", nodes,
+             drop.c_str(), kept_waits, pruned, leaf_removed);
       return 0;
     }
     ++n;
