@@ -482,12 +482,20 @@ def bench_distributed(a):
         sys.stderr.write(f"[bench rank {rank}] watchdog: {budget:.0f}s exceeded in phase {state['phase']}\n")
         import faulthandler
         faulthandler.dump_traceback(file=sys.stderr, all_threads=True)   # where every thread of this rank is
+        cut = dict(stage_t, **({state["major"][0] + " (cut)": round(time.time() - state["major"][1], 2)}
+                                if state.get("major") else {}))
         if state["line"] is not None:
             res = dict(state["line"])
             res["watchdog"] = f"run cut at {budget:.0f}s in phase '{state['phase']}'; headline = last complete measurement"
-            res["stage_wall_s"] = dict(stage_t, **({state["major"][0] + " (cut)": round(time.time() - state["major"][1], 2)}
-                                                   if state.get("major") else {}))
+            res["stage_wall_s"] = cut
             emit(res)
+        else:   # nothing measured yet: still one line, saying where every stage's time went
+            emit({"metric": "fp32 bucket reduce-sum GB/s (device-resident) at 1/2/4/8 MI355X", "value": None,
+                  "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": None,
+                  "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+                  "data": "synthetic", "config": {"workload": f"{world}xMI355X FlexTree AllReduce over xGMI"},
+                  "watchdog": f"run cut at {budget:.0f}s in phase '{state['phase']}' before any measurement",
+                  "stage_wall_s": cut, "rccl_error_by_rank": state.get("rccl_ranks")})
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(0 if state["line"] is not None else 3)
@@ -535,6 +543,7 @@ def bench_distributed(a):
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank takes the same path
         if not ok.item():
             rccl_ranks = all_errors(rccl_error)
+            state["rccl_ranks"] = rccl_ranks
             # RCCL could not come up on some rank: the peer forms over a gloo-bootstrapped communicator still
             # move the data over xGMI (IPC), so the run keeps a measured line
             if comm is not None:
@@ -555,18 +564,49 @@ def bench_distributed(a):
     y = torch.empty_like(x)
     stream = torch.cuda.current_stream()
     bucket = n * esz
+    # after an RCCL call that never completed (preflight below), a device-wide synchronize would wait on it
+    # forever: from then on only the bench stream is synchronised (every ftar call joins it at its end)
+    sync_state = {"device": True}
+
+    def sync():
+        if sync_state["device"]:
+            torch.cuda.synchronize()
+        else:
+            stream.synchronize()
+
+    def preflight(timeout_s):
+        """First contact of RCCL p2p between the ranks: one small call of the default configuration, waited
+        for with a deadline (an event polled from the host), so a transfer that never completes becomes the
+        IPC fallback below instead of a run the watchdog cuts with nothing measured.  Returns "" or why not."""
+        npf = min(n, 1 << 20)
+        try:
+            comm.chunk_bytes = default_chunk
+            comm.peer_direct, comm.allgather, comm.reduce_scatter = 0, "direct", "direct"
+            comm.allreduce(x[:npf], y[:npf], npf, a.dtype, "sum", topo_=default_topo, stream=stream)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            t_end = time.time() + timeout_s
+            if os.environ.get("FTAR_BENCH_PREFLIGHT_HANG"):   # rehearses the hang path (nothing hangs)
+                return f"RCCL preflight ({npf} elements) not complete after {timeout_s:.0f}s (simulated)"
+            while not ev.query():
+                if time.time() > t_end:
+                    return f"RCCL preflight ({npf} elements) not complete after {timeout_s:.0f}s"
+                time.sleep(0.005)
+            return ""
+        except Exception as e:  # noqa: BLE001
+            return f"RCCL preflight failed: {str(e)[:180]}"
 
     def timed(fn, steps, warmup):
         """barrier + sync on both sides of `steps` calls; max over ranks (ms per call)."""
         for _ in range(warmup):
             fn()
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             fn()
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
         t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -602,7 +642,7 @@ def bench_distributed(a):
         forms then read / write the peers' buffers in place, with no local pass."""
         if not reg:
             reg["x"], reg["y"] = x.clone(), torch.empty_like(y)
-            torch.cuda.synchronize()
+            sync()
             reg["ids"] = [comm.register(reg["x"], bucket), comm.register(reg["y"], bucket)]
         return reg["x"], reg["y"]
 
@@ -649,7 +689,7 @@ def bench_distributed(a):
         proves the call read this call's data (no stale copies) over the whole bucket.  Returns (ok, what
         failed on any rank: "" | "sample" | "ranks differ" | "negation")."""
         x, y = fn.xin, fn.yout
-        torch.cuda.synchronize()
+        sync()
         mine = y[idx].float().cpu()
         ally = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(ally, mine)
@@ -662,7 +702,7 @@ def bench_distributed(a):
         x.neg_()
         try:
             fn()
-            torch.cuda.synchronize()
+            sync()
         finally:
             x.neg_()   # the inputs stay intact for the next configuration, whatever happened
         if not torch.equal(y, y1.neg_()):
@@ -745,7 +785,7 @@ def bench_distributed(a):
             comm.allreduce_host(hx, hy, n, a.dtype, "sum", topo_=default_topo, stream=stream)
         msh = timed(fnh, min(a.steps, 5), 1)
         fn_default()   # the device path on the same inputs: y
-        torch.cuda.synchronize()
+        sync()
         ic = idx.cpu()
         same = torch.tensor([1 if torch.equal(hy[ic], y[idx].cpu()) else 0], dtype=torch.int32)
         dist.all_reduce(same, op=dist.ReduceOp.MIN)
@@ -800,7 +840,19 @@ def bench_distributed(a):
         default_topo = ftar.topo_from_env(world, bucket)
     default_chunk = a.chunk_bytes or comm.chunk_bytes
     err = ""
+    hung = False
+    if not a.host_comm:
+        phase("rccl preflight")
+        err = preflight(float(os.environ.get("FTAR_BENCH_PREFLIGHT_S", "60")))
+        hung = "not complete" in err
+        flag = torch.tensor([1 if hung else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item():   # some rank's RCCL work may never finish: never wait on the whole device again
+            sync_state["device"] = False
+        phase("default")
     try:
+        if err:
+            raise RuntimeError(err)
         if os.environ.get("FTAR_BENCH_FAIL_DEFAULT") and not a.host_comm:   # rehearses the fallback below
             raise RuntimeError("FTAR_BENCH_FAIL_DEFAULT set")
         fn_default = run_with(default_topo, default_chunk, base_form)
@@ -817,6 +869,7 @@ def bench_distributed(a):
         # communicator still move the data over xGMI, so the run keeps a measured line (the broken RCCL
         # communicator is left alone: destroying it could block)
         rccl_ranks = all_errors(err)
+        state["rccl_ranks"] = rccl_ranks
         rccl_error = f"default configuration over RCCL failed: {err or 'on another rank'}"
         sys.stderr.write(f"[bench rank {rank}] {rccl_error}; falling back to the host-bootstrapped peer forms\n")
         a.host_comm = True
@@ -971,7 +1024,7 @@ def bench_distributed(a):
         for label, t, ch, form in configs:
             fn = run_with(t, ch, form)
             fn()
-            torch.cuda.synchronize()
+            sync()
             phases[label] = {"topology": str(t), "chunk_bytes": ch, "form": form, "phases_ms": comm.last_phases()}
         comm.phase_timing(False)
         state["line"]["phases_rank0"] = phases
@@ -1039,6 +1092,12 @@ def bench_distributed(a):
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
     state["done"] = True
+    if not sync_state["device"]:
+        # an RCCL kernel that never completed is still on the device: tearing the runtime down would wait
+        # for it, so the line printed above is this process's last act
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     for i in reg.get("ids", []):
         comm.deregister(i)
     comm.destroy()

@@ -14,6 +14,19 @@ for p in (PKG, os.path.join(ROOT, "tests"), ROOT):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "capture_runtime_limit: a graph-capture shape the HIP runtime crashes on "
+                                       "(SIGSEGV in hipStreamEndCapture, DESIGN §4); runs only with "
+                                       "FTAR_RUN_CAPTURE_LIMITS=1")
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("FTAR_RUN_CAPTURE_LIMITS") == "1":
+        return
+    skip = pytest.mark.skip(reason="HIP runtime capture limit: opt in with FTAR_RUN_CAPTURE_LIMITS=1 "
+                                   "(the child process crashes in hipStreamEndCapture)")
+    for item in items:
+        if "capture_runtime_limit" in item.keywords:
+            item.add_marker(skip)
 
 
 @pytest.fixture(scope="session")

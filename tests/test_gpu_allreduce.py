@@ -478,9 +478,10 @@ def test_allreduce_group_captures_into_a_hip_graph(topo):
     assert p.returncode == 0 and "group capture ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-3000:])
 
 
+@pytest.mark.capture_runtime_limit
 @pytest.mark.xfail(reason="HIP runtime: hipStreamEndCapture recurses without end on these capture graphs (also "
                           "the torch-bundled 7.0 runtime on the 2-rank shape); a single-threaded event-only "
-                          "reproducer is in profiles/r02/capture/ (tools/capture/replay.cpp), DESIGN §4",
+                          "reproducer is in profiles/r03/capture/ (tools/capture/replay.cpp), DESIGN §4",
                    strict=False)
 @pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 0, True),
                                                        (2, "1", "direct", "direct", 4096, False),

@@ -25,6 +25,13 @@
 // on by all), so no stream joins the capture through another forked stream;
 // the file's own fork waits then become ordinary cross-stream waits and the
 // dependencies stay the same (the begin event carries none).
+// drop kind 'a' (acyclic; diagnostic, changes the dependencies): skip every
+// cross-stream wait that would close a cycle in the relation "stream W waited
+// on an event recorded on stream R" (edge R -> W) -- e.g. the comm and reduce
+// streams waiting on each other in turn.  Forks (a stream's first wait) and
+// joins (a stream waiting on a stream it forked, directly or not) are kept.
+// A capture that then ends says the runtime cannot end captures whose
+// streams waited on each other both ways.
 #include <hip/hip_runtime.h>
 
 #include <set>
@@ -119,7 +126,30 @@ int main(int argc, char** argv) {
     }
     return out;
   };
-  const bool flat = drop.find('f') != std::string::npos;
+  const bool flat = drop.find('f') != std::string::npos, acyclic = drop.find('a') != std::string::npos;
+  std::map<std::string, std::string> erec;                 // event -> stream it was recorded on
+  std::map<std::string, std::set<std::string>> waited_by;  // R -> {W}: W waited on an event of R
+  int cyc = 0;
+  std::map<std::string, std::string> fork_parent;  // stream -> the stream whose event brought it into the capture
+  auto forked_from = [&](const std::string& s, std::string r) {  // is s an ancestor of r in the fork tree
+    while (fork_parent.count(r)) {
+      r = fork_parent[r];
+      if (r == s) return true;
+    }
+    return false;
+  };
+  auto reaches = [&](const std::string& from, const std::string& to) {
+    std::set<std::string> seen;
+    std::vector<std::string> st{from};
+    while (!st.empty()) {
+      std::string v = st.back();
+      st.pop_back();
+      if (v == to) return true;
+      if (!seen.insert(v).second) continue;
+      for (const std::string& w : waited_by[v]) st.push_back(w);
+    }
+    return false;
+  };
   std::vector<std::string> all_streams;  // every stream the file names, for 'f'
   {
     std::ifstream pre(argv[1]);
@@ -177,11 +207,23 @@ int main(int argc, char** argv) {
       }
     }
     else if (op == "R") {
+      erec[x] = y;
       edeps[x] = sdeps[y];
       ecap[x] = scap[y];
       CK(hipEventRecord(E(x), S(y)));
     }
     else if (op == "W") {
+      const std::string rec = erec[y];
+      const bool fork = ecap[y] && !scap[x], join = forked_from(x, rec);
+      if (fork) fork_parent[x] = rec;
+      if (acyclic && !fork && !join && !rec.empty() && rec != x && reaches(x, rec)) {
+        ++cyc;
+        fprintf(stderr, "replay: skipped op %d (W %s on an event of %s: closes a wait cycle)\n", n, x.c_str(),
+                rec.c_str());
+        ++n;
+        continue;
+      }
+      if (!rec.empty() && rec != x) waited_by[rec].insert(x);
       if (ecap[y] && !scap[x]) {  // the fork: the stream joins the capture
         scap[x] = true;
         sdeps[x] = edeps[y];
@@ -209,8 +251,8 @@ int main(int argc, char** argv) {
     }
     else if (op == "E") {
       hipGraph_t g;
-      fprintf(stderr, "replay: %d ops, %d waits kept, %d pruned as redundant, %d ancestor dependencies removed; "
-              "ending the capture\n", n, kept_waits, pruned, leaf_removed);
+      fprintf(stderr, "replay: %d ops, %d waits kept, %d pruned as redundant, %d ancestor dependencies removed, "
+              "%d cycle-closing waits skipped; ending the capture\n", n, kept_waits, pruned, leaf_removed, cyc);
       CK(hipStreamEndCapture(S(x), &g));
       size_t nodes = 0;
       CK(hipGraphGetNodes(g, nullptr, &nodes));
