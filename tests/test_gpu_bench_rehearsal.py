@@ -21,11 +21,11 @@ def _port():
         return s.getsockname()[1]
 
 
-def _bench(ranks, extra):
+def _bench(ranks, extra, env_extra=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
            "--steps", "2", "--warmup", "1", "--elements", str(5 << 24), "--elements-c5", str(1 << 22)] + extra
-    env = dict(os.environ, FTAR_BENCH_BUDGET_S="100", FTAR_BENCH_SWEEP_S="60")
+    env = dict(os.environ, FTAR_BENCH_BUDGET_S="100", FTAR_BENCH_SWEEP_S="60", **(env_extra or {}))
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
@@ -42,5 +42,21 @@ def test_bench_n_gt_1_rehearsal(ranks, extra):
     assert d["c5_bf16"]["check"] == "ok", d["c5_bf16"]
     assert "ms" in d["bucket_256MiB"], d["bucket_256MiB"]
     assert d["xgmi_probe_GBps"]["read_all_peers"][0] > 0
+    assert set(d["stage_wall_s"]) >= {"init", "default", "sweep", "headline", "C5 bf16", "host e2e"}, d["stage_wall_s"]
     if not extra:   # RCCL refused the shared GPU on every rank and every rank fell back
         assert "rccl_init_error" in d
+        assert [e["rank"] for e in d["rccl_error_by_rank"]] == list(range(ranks)), d["rccl_error_by_rank"]
+
+
+@pytest.mark.parametrize("env_extra,why", [({"FTAR_BENCH_PREFLIGHT_HANG": "1"}, "not complete"),
+                                           ({"FTAR_BENCH_FAIL_DEFAULT": "1"}, "FTAR_BENCH_FAIL_DEFAULT")])
+def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
+    """The first-contact failure paths of the 8-GPU run, at world size 1 over a real RCCL communicator: an RCCL
+    call that never completes (simulated: the preflight takes the path without anything hanging) or fails makes
+    every rank fall back to the IPC peer forms; the line names every rank's error and the stage times, and
+    rccl_p2p_best is absent because no RCCL configuration was measured."""
+    d = _bench(1, ["--force-dist", "--no-cpu-baseline"], env_extra)
+    assert d["check"] == "ok" and d["config"]["form"].startswith("peer-"), d["config"]
+    assert why in d["rccl_init_error"], d["rccl_init_error"]
+    assert len(d["rccl_error_by_rank"]) == 1 and why in d["rccl_error_by_rank"][0]["error"]
+    assert "default" in d["stage_wall_s"] and d.get("rccl_p2p_best") is None
