@@ -171,6 +171,8 @@ ftar_status_t grow_events(ftar_comm* c, size_t n) {
 }
 }  // namespace
 
+ftar_status_t agree_settings(ftar_comm* c);
+
 ftar_status_t comm_setup(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
@@ -197,6 +199,39 @@ ftar_status_t comm_setup(ftar_comm* c) {
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
   if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
+  return agree_settings(c);
+}
+
+// The environment-derived settings that shape the messages every rank posts (piece sizes, data-movement
+// forms) and the topology choice (FT_TOPO / FT_LONELY, the cost model and its constants) must be alike on
+// every rank: a rank pieced differently from its peers posts transfers they do not match.  Compared once
+// at bring-up (collective), so a mismatched launch fails every rank's init instead of hanging a call.
+// Setters (ftar_comm_set_*, ftar_cost_set_params) must likewise be called alike, as RCCL's own
+// configuration must.
+ftar_status_t agree_settings(ftar_comm* c) {
+  if (c->nranks <= 1) return FTAR_SUCCESS;
+  auto h = [](const char* v) {  // FNV-1a of an environment string ("" = unset)
+    uint64_t x = 1469598103934665603ull;
+    for (const char* p = v ? v : ""; *p; ++p) x = (x ^ (unsigned char)*p) * 1099511628211ull;
+    return x;
+  };
+  double alpha = 0, link = 0, hbm = 0;
+  ftar_cost_get_params(&alpha, &link, &hbm);
+  uint64_t cfg[12] = {(uint64_t)c->chunk_bytes, (uint64_t)c->host_chunk_bytes, (uint64_t)c->peer_direct,
+                      (uint64_t)c->host_peer_pipeline, (uint64_t)c->reduce_scatter, (uint64_t)c->allgather,
+                      h(getenv("FT_TOPO")), h(getenv("FT_LONELY")), h(getenv("FTAR_COST_MODEL")), 0, 0, 0};
+  memcpy(&cfg[9], &alpha, 8);
+  memcpy(&cfg[10], &link, 8);
+  memcpy(&cfg[11], &hbm, 8);
+  bool same = true;
+  FTAR_RETURN_IF(c->tp->agree(cfg, sizeof cfg, &same));
+  if (!same) {
+    set_error("ranks disagree on FTAR_CHUNK_BYTES / FTAR_HOST_CHUNK_BYTES / FTAR_PEER_DIRECT / "
+              "FTAR_HOST_PEER_PIPELINE / FTAR_REDUCE_SCATTER / FTAR_ALLGATHER / FT_TOPO / FT_LONELY / the cost "
+              "model: launch every rank with the same environment",
+              __FILE__, __LINE__);
+    return FTAR_ERR_INVALID_ARG;
+  }
   return FTAR_SUCCESS;
 }
 

@@ -364,6 +364,29 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
 
+  // every rank's bytes through one ncclAllGather on a private stream (host-blocking; communicator
+  // bring-up only)
+  ftar_status_t agree(const void* mine, size_t bytes, bool* same) override {
+    char* dev = nullptr;
+    FTAR_CHECK_ALLOC(hipMalloc(&dev, (size_t)(nranks_ + 1) * bytes));
+    std::vector<char> all((size_t)nranks_ * bytes);
+    hipStream_t s = nullptr;
+    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+              hipMemcpyAsync(dev, mine, bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
+              ncclAllGather(dev, dev + bytes, bytes, ncclUint8, comm_, s) == ncclSuccess &&
+              hipMemcpyAsync(all.data(), dev + bytes, all.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
+              hipStreamSynchronize(s) == hipSuccess;
+    if (s) hip_ignore(hipStreamDestroy(s));
+    hip_ignore(hipFree(dev));
+    if (!ok) {
+      set_error("settings agreement: the all-gather failed", __FILE__, __LINE__);
+      return FTAR_ERR_RCCL;
+    }
+    *same = true;
+    for (int q = 0; q < nranks_; ++q) *same = *same && !memcmp(all.data() + (size_t)q * bytes, mine, bytes);
+    return FTAR_SUCCESS;
+  }
+
  private:
   // sum of every rank's `mine` (host-blocking, on a private stream)
   ftar_status_t agree_failures(int mine, int* total) {

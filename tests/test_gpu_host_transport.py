@@ -418,3 +418,55 @@ def test_host_path_settings_must_agree_across_ranks():
     ref = oracle_lib.allreduce([fi.fill("f32", 41, r, n) for r in range(world)], "1")
     for r in range(world):
         assert res[r]["after"] == ref[r].tobytes(), r
+
+
+def _init_mismatch_worker(rank, world, port, q):
+    """Ranks launched with different environments (FTAR_CHUNK_BYTES, FT_TOPO): communicator bring-up compares
+    the settings that shape every rank's messages and fails on every rank, instead of a later call hanging."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import ftar
+    import ftar.dist
+    out = {}
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        for var, vals in (("FTAR_CHUNK_BYTES", ("1048576", "4194304")), ("FT_TOPO", ("1", "2"))):
+            os.environ[var] = vals[rank % 2]
+            try:
+                comm = ftar.dist.init_host_comm(device=0)
+                comm.destroy()
+                out[var] = "initialised"
+            except ftar.FtarError as e:
+                out[var] = (e.status, "disagree" in str(e))
+            del os.environ[var]
+            dist.barrier()
+        comm = ftar.dist.init_host_comm(device=0)   # alike again: fine
+        comm.destroy()
+        out["after"] = "ok"
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        import traceback
+        out["error"] = traceback.format_exc()
+    q.put((rank, out))
+
+
+def test_mismatched_environments_fail_bring_up_on_every_rank():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_init_mismatch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in res[r], res[r].get("error")
+        assert res[r]["FTAR_CHUNK_BYTES"] == (1, True) and res[r]["FT_TOPO"] == (1, True), res[r]
+        assert res[r]["after"] == "ok"
