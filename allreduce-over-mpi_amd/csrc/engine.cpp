@@ -69,6 +69,7 @@ struct ftar_comm {
   // what they parsed to are kept, so an unchanged environment costs two getenv
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
+  bool settings_agreed = false;  // agree_settings ran (engine.cpp comm_setup / the first call)
   bool env_seen = false;
   std::string env_topo, env_lonely;  // the strings last parsed ("" = unset)
   ftar_status_t env_status = FTAR_SUCCESS;
@@ -199,17 +200,24 @@ ftar_status_t comm_setup(ftar_comm* c) {
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
   if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
-  return agree_settings(c);
+  // a host-bootstrapped communicator compares its settings now (its host collective cannot hang on a
+  // rank whose bring-up failed: that rank reports through it too); an RCCL one at its first call, so a
+  // rank whose RCCL bring-up failed leaves no peer waiting in a collective inside ftar_comm_init_rank
+  if (!c->tp->async_p2p()) {
+    FTAR_RETURN_IF(agree_settings(c));
+    c->settings_agreed = true;
+  }
+  return FTAR_SUCCESS;
 }
 
 // The environment-derived settings that shape the messages every rank posts (piece sizes, data-movement
 // forms) and the topology choice (FT_TOPO / FT_LONELY, the cost model and its constants) must be alike on
 // every rank: a rank pieced differently from its peers posts transfers they do not match.  Compared once
-// at bring-up (collective), so a mismatched launch fails every rank's init instead of hanging a call.
+// (collective: at bring-up, or an RCCL communicator's first call), so a mismatched launch fails every rank
+// instead of hanging a call.
 // Setters (ftar_comm_set_*, ftar_cost_set_params) must likewise be called alike, as RCCL's own
 // configuration must.
 ftar_status_t agree_settings(ftar_comm* c) {
-  if (c->nranks <= 1) return FTAR_SUCCESS;
   auto h = [](const char* v) {  // FNV-1a of an environment string ("" = unset)
     uint64_t x = 1469598103934665603ull;
     for (const char* p = v ? v : ""; *p; ++p) x = (x ^ (unsigned char)*p) * 1099511628211ull;
@@ -937,6 +945,10 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     Topology t;
     bool is_auto = false;
     FTAR_RETURN_IF(topo ? to_topology(topo, c->nranks, &t) : env_topology(c, &is_auto, &t));
+  }
+  if (!c->settings_agreed && !c->capturing) {  // an RCCL communicator's first call (see comm_setup); a
+    FTAR_RETURN_IF(agree_settings(c));          // 1-rank one too, which exercises the same all-gather
+    c->settings_agreed = true;
   }
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
     if (sendbuf && count && host)
