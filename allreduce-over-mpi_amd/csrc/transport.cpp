@@ -192,11 +192,17 @@ ftar_status_t ipc_import(const IpcRef& ref, void** base, char** p) {
 // ---------------------------------------------------------------------------
 namespace {
 
+// ncclGetLastError(NULL) adds RCCL's own detail of the failure (which peer, which transport) to the
+// status string: one driver record of a failed first RCCL contact then says why (bench.py gathers every
+// rank's ftar_last_error)
 #define FTAR_CHECK_NCCL(expr)                                                                       \
   do {                                                                                              \
     ncclResult_t _r = (expr);                                                                       \
     if (_r != ncclSuccess) {                                                                        \
-      ::ftar::set_error(std::string(#expr) + ": " + ncclGetErrorString(_r), __FILE__, __LINE__);    \
+      const char* _d = ncclGetLastError(nullptr);                                                   \
+      ::ftar::set_error(std::string(#expr) + ": " + ncclGetErrorString(_r) +                        \
+                            (_d && *_d ? std::string(" (") + _d + ")" : std::string()),             \
+                        __FILE__, __LINE__);                                                        \
       return FTAR_ERR_RCCL;                                                                         \
     }                                                                                               \
   } while (0)
@@ -424,7 +430,10 @@ std::unique_ptr<Transport> make_rccl_transport(int nranks, const ftar_unique_id_
   ncclComm_t c = nullptr;
   ncclResult_t r = ncclCommInitRank(&c, nranks, uid, rank);
   if (r != ncclSuccess) {
-    set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r), __FILE__, __LINE__);
+    const char* d = ncclGetLastError(nullptr);
+    set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r) +
+                  (d && *d ? std::string(" (") + d + ")" : std::string()),
+              __FILE__, __LINE__);
     *st = FTAR_ERR_RCCL;
     return nullptr;
   }

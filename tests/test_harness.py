@@ -218,3 +218,29 @@ def test_harness_matches_oracle_on_odd_shapes(tmp_path, ranks, topo, n, device):
     for r in range(ranks):
         got = np.fromfile(os.path.join(tmp_path, f"out.{r}.bin"), dtype=np.float32)
         assert got.tobytes() == ref[r].tobytes(), (ranks, topo, n, r)
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n,device", [(2, "1", 1 << 26, False), (2, "2", 1 << 26, True),
+                                                 (8, "8", 1 << 24, False), (4, "2,2", 1 << 24, False)])
+def test_harness_baseline_sizes_match_oracle(tmp_path, ranks, topo, n, device):
+    """MPI_Allreduce_FT across real MPI processes at BASELINE sizes: C3's 256 MiB fp32 bucket with 2 ranks (the
+    ring and tree(2); host buffers and device-resident), and 8 ranks (C4/C5's width-8 tree) and a 2,2 tree on
+    64 MiB, on benchmark.cpp's own workload (data[i] = i * 0.1f on every rank, one call in place).  Every
+    rank's whole buffer equals the pinned oracle's result bit for bit (compared by sha256).  All ranks share
+    the box's one GPU, so the data moves through the ipc transport's IPC-mapped buffers, not RCCL."""
+    import hashlib
+
+    import numpy as np
+    import oracle_lib
+    args = ["--size", str(n), "--repeat", "1", "--dump", "out"] + (["--device"] if device else [])
+    p = subprocess.run([MPIEXEC, "-n", str(ranks), BIN] + args, cwd=tmp_path,
+                       env=dict(os.environ, FT_TOPO=topo), capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    x = (np.arange(n, dtype=np.float64).astype(np.float32) * np.float32(0.1)).astype(np.float32)
+    ref = oracle_lib.allreduce([x] * ranks, topo)
+    for r in range(ranks):
+        with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
+            got = hashlib.sha256(f.read()).hexdigest()
+        assert got == hashlib.sha256(ref[r].tobytes()).hexdigest(), (ranks, topo, n, r)
