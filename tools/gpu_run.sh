@@ -31,6 +31,7 @@ for s in "${steps[@]}"; do
     final) python3 -c "import json, bench; json.dump({'commit': '${FTAR_COMMIT:-unknown}', 'kernel_sources_sha': bench.kernel_source_digest()}, open('gpurun_out/pmc_meta.json', 'w'))" &&
            run bench 600 python bench.py --steps 20 --warmup 5 &&
            run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline &&
+           python3 tools/trace_split.py gpurun_out/prof/run_kernel_trace.csv --out gpurun_out/kernel_phases.json > /dev/null &&
            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
