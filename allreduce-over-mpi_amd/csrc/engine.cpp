@@ -64,12 +64,12 @@ struct ftar_comm {
   };
   std::map<int, Reg> regs;
   int next_reg = 1;
-  // FT_TOPO / FT_LONELY are read on every call with topo == NULL, as the
-  // reference's get_stages is (mpi_mod.hpp:1732); the last strings seen and
-  // what they parsed to are kept, so an unchanged environment costs two getenv
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
   bool settings_agreed = false;  // agree_settings ran (engine.cpp comm_setup / the first call)
+  // FT_TOPO / FT_LONELY are read on every call with topo == NULL, as the
+  // reference's get_stages is (mpi_mod.hpp:1732); the last strings seen and
+  // what they parsed to are kept, so an unchanged environment costs two getenv
   bool env_seen = false;
   std::string env_topo, env_lonely;  // the strings last parsed ("" = unset)
   ftar_status_t env_status = FTAR_SUCCESS;
