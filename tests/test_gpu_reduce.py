@@ -120,6 +120,31 @@ def test_reduce_bf16_matches_fp32_reference_within_one_rounding():
     assert np.all(np.abs(got - f32) <= ulp)
 
 
+@pytest.mark.parametrize("k", [2, 3, 8, 16])
+def test_reduce_bf16_is_torch_fp32_fold_rounded_once(k):
+    """bf16 has no reference (mpi_mod.hpp handles no 16-bit float), so its semantics are pinned against an
+    independent implementation instead of our own oracle: PyTorch, folding the sources left to right in fp32
+    (torch's own adds) and converting once with torch's round-to-nearest-even float -> bfloat16.  The GPU
+    kernel must give the same bits on every element, NaN and infinity inputs included."""
+    import torch
+    n = 50_001
+    ins = [fi.fill("bf16", 11, j, n) for j in range(k)]
+    ins[0][::97] = 0x7FC1       # NaN
+    ins[1][5::89] = 0x7F80      # +inf
+    ins[-1][7::83] = 0xFF80     # -inf
+    ins[1][11::79] = 0x0001     # bf16 denormal
+    got = run_reduce(ins, "bf16", "sum").view(np.uint16)
+    t = [torch.from_numpy(x.view(np.int16).copy()).view(torch.bfloat16) for x in ins]
+    acc = t[0].float()
+    for x in t[1:]:
+        acc = acc + x.float()
+    ref = acc.to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+    nan_g = (got & 0x7FFF) > 0x7F80
+    nan_r = (ref & 0x7FFF) > 0x7F80
+    assert np.array_equal(nan_g, nan_r)                     # NaN exactly where torch has NaN (DESIGN §5)
+    assert np.array_equal(got[~nan_r], ref[~nan_r])
+
+
 def test_reduce_beyond_int32_index():
     """2^31 + 77 elements (the reference kernel indexes with `int`, vector_add/reduce_sum_gpu.h:8):
     u8 sums wrap, checked on a head, a window across the 2^31 boundary and the tail."""
