@@ -61,12 +61,17 @@ struct ftar_comm {
     char* ptr;
     size_t bytes;
     std::vector<char*> peers;
+    void* rccl = nullptr;  // ncclCommRegister handle (RCCL communicators), or nullptr
   };
   std::map<int, Reg> regs;
   int next_reg = 1;
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
   bool settings_agreed = false;  // agree_settings ran (engine.cpp comm_setup / the first call)
+  // the scratch buffer registered with RCCL (ncclCommRegister), so p2p receives may land in it without
+  // RCCL's staging copies (FTAR_RCCL_REGISTER=1 / ftar_debug_set_rccl_register; bench.py sweeps it)
+  bool rccl_reg = false;
+  void* scratch_rccl = nullptr;
   // FT_TOPO / FT_LONELY are read on every call with topo == NULL, as the
   // reference's get_stages is (mpi_mod.hpp:1732); the last strings seen and
   // what they parsed to are kept, so an unchanged environment costs two getenv
@@ -188,6 +193,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
                      : std::max(0, std::min(2, atoi(pd)));
   }
   if (const char* hp = getenv("FTAR_HOST_PEER_PIPELINE")) c->host_peer_pipeline = atoi(hp) != 0;
+  if (const char* rr = getenv("FTAR_RCCL_REGISTER")) c->rccl_reg = atoi(rr) != 0;
   const char* hcb = getenv("FTAR_HOST_CHUNK_BYTES");
   c->host_chunk_bytes = hcb ? strtoull(hcb, nullptr, 0) : kDefaultHostChunkBytes;
   if (c->host_chunk_bytes && c->host_chunk_bytes < 256) c->host_chunk_bytes = 256;
@@ -284,7 +290,12 @@ void comm_teardown(ftar_comm* c) {
     if (st) hip_ignore(hipStreamSynchronize(st));
   if (c->tp) {
     c->tp->unmap_peers(&c->xpeers, c->rank);
-    for (auto& r : c->regs) c->tp->unmap_peers(&r.second.peers, c->rank);
+    for (auto& r : c->regs) {
+      c->tp->unmap_peers(&r.second.peers, c->rank);
+      c->tp->rccl_deregister(r.second.rccl);
+    }
+    if (c->scratch_rccl) c->tp->rccl_deregister(c->scratch_rccl);
+    c->scratch_rccl = nullptr;
   }
   c->regs.clear();
   if (c->xbuf) {
@@ -1048,8 +1059,18 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   const bool skew = host != nullptr;
   std::vector<long> delta(nst, 0);
   const size_t scratch_elems = skew ? per_stage_scratch(plan, &delta) : 2 * plan.scratch_half;
-  if (scratch_elems * esz > c->scratch_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the scratch buffer"));
+  if (scratch_elems * esz > c->scratch_bytes) {
+    FTAR_RETURN_IF(refuse_growth_under_capture(c, "the scratch buffer"));
+    if (c->scratch_rccl) {  // the old scratch is about to be freed: drop its RCCL registration first
+      FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
+      FTAR_CHECK_HIP(hipStreamSynchronize(c->red_s));
+      c->tp->rccl_deregister(c->scratch_rccl);
+      c->scratch_rccl = nullptr;
+    }
+  }
   FTAR_RETURN_IF(ensure_buffer(&c->scratch, &c->scratch_bytes, scratch_elems * esz, {c->comm_s, c->red_s}));
+  if (c->rccl_reg && !c->scratch_rccl && c->scratch && !c->capturing)
+    c->scratch_rccl = c->tp->rccl_register(c->scratch, c->scratch_bytes);
   const std::vector<std::pair<size_t, size_t>> order = step_order(nst, nchunks, skew);
 
   FTAR_RETURN_IF(grow_events(c, 2 * nst * nchunks + 2 * nchunks + 5));
@@ -1366,6 +1387,21 @@ ftar_status_t ftar_debug_set_peer_tuning(ftar_comm_t comm, int nt, int lds) {
   return FTAR_SUCCESS;
 }
 // Test/tuning hook (not in ftar.h): the peer forms' cross-GPU copies by the DMA engines.
+// RCCL registration of the comm's scratch buffer (FTAR_RCCL_REGISTER); off drops it at once.
+ftar_status_t ftar_debug_set_rccl_register(ftar_comm_t comm, int on) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->rccl_reg = on != 0;
+  if (!comm->rccl_reg && comm->scratch_rccl) {
+    FTAR_CHECK_HIP(hipSetDevice(comm->device));
+    FTAR_CHECK_HIP(hipStreamSynchronize(comm->comm_s));
+    FTAR_CHECK_HIP(hipStreamSynchronize(comm->red_s));
+    comm->tp->rccl_deregister(comm->scratch_rccl);
+    comm->scratch_rccl = nullptr;
+  }
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t ftar_debug_set_peer_dma(ftar_comm_t comm, int dma) {
   if (!comm) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
@@ -1385,6 +1421,7 @@ ftar_status_t ftar_comm_register(ftar_comm_t comm, void* buf, size_t bytes, int*
   FTAR_CHECK_HIP(hipSetDevice(comm->device));
   ftar_comm::Reg r{static_cast<char*>(buf), bytes, {}};
   FTAR_RETURN_IF(comm->tp->map_peers(buf, comm->rank, comm->nranks, &r.peers));
+  r.rccl = comm->tp->rccl_register(buf, bytes);  // RCCL's own registration too (local; nullptr if refused)
   *reg = comm->next_reg++;
   comm->regs.emplace(*reg, std::move(r));
   return FTAR_SUCCESS;
@@ -1399,6 +1436,7 @@ ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg) {
   FTAR_CHECK_HIP(hipStreamSynchronize(comm->comm_s));  // its last call ended in a barrier: no peer touches it
   FTAR_CHECK_HIP(hipStreamSynchronize(comm->red_s));
   comm->tp->unmap_peers(&it->second.peers, comm->rank);
+  comm->tp->rccl_deregister(it->second.rccl);
   comm->regs.erase(it);
   return FTAR_SUCCESS;
 }

@@ -195,6 +195,15 @@ class Transport {
     *same = true;
     return FTAR_SUCCESS;
   }
+  // RCCL user-buffer registration (ncclCommRegister, a local call): lets RCCL move p2p data straight
+  // between registered buffers where it can.  Returns a handle, or nullptr where the transport has no
+  // such registration or RCCL refused it (the transfers then take RCCL's staging path, same bytes).
+  virtual void* rccl_register(void* buf, size_t bytes) {
+    (void)buf;
+    (void)bytes;
+    return nullptr;
+  }
+  virtual void rccl_deregister(void* handle) { (void)handle; }
   virtual ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) = 0;
   virtual void unmap_peers(std::vector<char*>* peers, int rank) { (void)rank; peers->clear(); }
   // map_peers exports and opens IPC handles (false: one address space)

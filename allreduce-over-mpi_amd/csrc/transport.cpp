@@ -370,6 +370,17 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
 
+  void* rccl_register(void* buf, size_t bytes) override {
+    void* h = nullptr;
+    if (ncclCommRegister(comm_, buf, bytes, &h) != ncclSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    return h;
+  }
+  void rccl_deregister(void* handle) override {
+    if (handle) (void)ncclCommDeregister(comm_, handle);
+  }
   // every rank's bytes through one ncclAllGather on a private stream (host-blocking; communicator
   // bring-up only)
   ftar_status_t agree(const void* mine, size_t bytes, bool* same) override {

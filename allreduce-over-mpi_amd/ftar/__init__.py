@@ -120,6 +120,7 @@ _lib.ftar_allreduce_host_group.argtypes = [ctypes.POINTER(_vp), ctypes.POINTER(_
 _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
 _lib.ftar_debug_set_peer_dma.argtypes = [_vp, _int]
+_lib.ftar_debug_set_rccl_register.argtypes = [_vp, _int]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
@@ -446,6 +447,17 @@ class Comm:
     @peer_direct.setter
     def peer_direct(self, mode):
         _check(_lib.ftar_comm_set_peer_direct(self.handle, _peer_mode(mode)), "peer_direct")
+
+    @property
+    def rccl_register(self):
+        return getattr(self, "_rccl_register", False)
+
+    @rccl_register.setter
+    def rccl_register(self, on):
+        """RCCL registration (ncclCommRegister) of the comm's scratch buffer (FTAR_RCCL_REGISTER); buffers
+        passed to register() are always registered with RCCL too, where RCCL accepts them."""
+        _check(_lib.ftar_debug_set_rccl_register(self.handle, 1 if on else 0), "rccl_register")
+        self._rccl_register = bool(on)
 
     def peer_tuning(self, nt=True, lds=True, dma=False):
         """Peer forms: nontemporal copies (nt), the LDS-staged fold (lds; False = register kernel), and the

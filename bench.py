@@ -619,6 +619,9 @@ def bench_distributed(a):
         comm.peer_tuning(nt=tune != "plain", lds=tune != "vec", dma=tune == "dma")
         # ":cusN": the reduce stream on N CUs, the rest left to RCCL's p2p kernels (DESIGN §4 co-scheduling)
         comm.reduce_cus = int(tune[3:]) if tune.startswith("cus") else 0
+        # ":ncclreg": RCCL p2p between buffers registered with RCCL (ncclCommRegister): the comm's scratch
+        # and registered copies of x and y, so RCCL may skip its staging copies where it supports that
+        comm.rccl_register = tune == "ncclreg"
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
         rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
         kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
@@ -628,7 +631,7 @@ def bench_distributed(a):
         comm.peer_direct = form.split("-")[1] if peer else 0
         comm.allgather = "direct" if peer else form
         comm.reduce_scatter = "stages" if form == "stages" else "direct"
-        xin, yout = (reg_bufs() if form.endswith("-reg") else (x, y))
+        xin, yout = (reg_bufs() if form.endswith("-reg") or tune == "ncclreg" else (x, y))
 
         def fn():
             comm.allreduce(xin, yout, n, a.dtype, "sum", topo_=topo, stream=stream)
@@ -722,6 +725,7 @@ def bench_distributed(a):
         yb = torch.empty_like(xb)
         t5 = ftar.topo(a.topo, a.lonely, nranks=world) if a.topo else ftar.topo_from_env(world, nb * 2)
         comm.chunk_bytes = default_chunk
+        comm.rccl_register = False
         comm.peer_direct = "read" if a.host_comm else 0
         comm.allgather = "direct"
         comm.reduce_scatter = "direct"
@@ -780,6 +784,7 @@ def bench_distributed(a):
         comm.reduce_scatter = "direct"
         comm.peer_tuning()
         comm.reduce_cus = 0   # the sweep's last configuration may have left the reduce stream on a CU subset
+        comm.rccl_register = False
 
         def fnh():
             comm.allreduce_host(hx, hy, n, a.dtype, "sum", topo_=default_topo, stream=stream)
@@ -904,6 +909,7 @@ def bench_distributed(a):
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
                 plan.append((t, default_chunk, "direct:cus224"))
+                plan.append((t, default_chunk, "direct:ncclreg"))
             if form == "stages" and t.ring:
                 chunks = {default_chunk}  # the reference's ring rounds: one point is enough
             plan += [(t, chunk, form) for chunk in sorted(chunks)]

@@ -546,6 +546,30 @@ def test_reduce_stream_cu_mask_same_bits(cus):
         g.set_reduce_cus(0)
 
 
+def test_rccl_buffer_registration_single_rank():
+    """ncclCommRegister of registered buffers and of the comm's scratch (FTAR_RCCL_REGISTER / the bench's
+    direct:ncclreg entry) on a 1-rank RCCL communicator: register, call, toggle, deregister and destroy all
+    succeed and the call still copies (P <= 1, mpi_mod.hpp:1739)."""
+    import torch
+    import ftar
+    comm = ftar.Comm.init_rank(1, ftar.get_unique_id(), 0, 0)
+    try:
+        n = 1 << 20
+        x = torch.rand(n, device="cuda")
+        y = torch.empty_like(x)
+        ids = [comm.register(x, n * 4), comm.register(y, n * 4)]
+        for on in (True, False, True):
+            comm.rccl_register = on
+            y.zero_()
+            comm.allreduce(x, y, n, "f32", "sum", stream=torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            assert torch.equal(x, y)
+        for i in ids:
+            comm.deregister(i)
+    finally:
+        comm.destroy()
+
+
 def test_rccl_single_rank_allreduce_captures_into_a_hip_graph():
     """The product's process model (one rank per process over RCCL) under stream capture: a 1-rank RCCL
     communicator's ftar_allreduce (the reference's P <= 1 copy, mpi_mod.hpp:1739) captured with torch.cuda.graph
