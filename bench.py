@@ -311,8 +311,12 @@ def reference_mpi_path(world, n=1 << 24, repeat=20, seconds=150):
         p = subprocess.run([mpiexec, "-n", str(world), ref, "arbench", "--n", str(n), "--repeat", str(repeat)],
                            capture_output=True, text=True, timeout=seconds, env=env)
         d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+        hc = host_cores()
+        d["cores"] = world * 14   # 14 OpenMP threads per rank, hard-coded (mpi_mod.hpp:820)
+        d["cores_available"] = hc
         d["sample"] = (f"{world} MPI ranks on the host, ring (FT_TOPO=1), {n} fp32 per rank, best of {repeat} "
-                       "timed calls (benchmark.cpp timing: Barrier + Wtime, max over ranks)")
+                       f"timed calls (benchmark.cpp timing: Barrier + Wtime, max over ranks); {world} x 14 OpenMP "
+                       f"threads on {hc['available_cpus']} available CPUs")
         return d
     except Exception as e:  # noqa: BLE001  a baseline must not cost the run its line
         return {"error": str(e)[:200]}
