@@ -49,6 +49,9 @@ struct ftar_comm {
   // peer_dma: the xGMI copies of the peer forms (gather, scatter, push) by the DMA engines, one
   // hipMemcpyAsync per peer on its own stream forked from and joined back into comm_s
   bool peer_dma = false;
+  // workgroups per segment of the cross-GPU copy kernels (gather, scatter, push); 0 = as many as the
+  // segment fills (ftar_debug_set_peer_wg_cap; bench.py tries the xGMI probe's best cap when it beats that)
+  size_t peer_wg_cap = 0;
   std::vector<hipStream_t> dma_s;
   std::vector<hipEvent_t> dma_ev;
   hipEvent_t dma_fork = nullptr;
@@ -467,7 +470,7 @@ namespace {
 // the peer forms' cross-GPU copies: one copy-kernel launch over every segment (every link at once), or with
 // peer_dma one DMA copy per segment, each on its own stream, all joined back into comm_s
 ftar_status_t peer_copy(ftar_comm* c, const std::vector<Segment>& segs) {
-  if (!c->peer_dma) return launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt);
+  if (!c->peer_dma) return launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt, c->peer_wg_cap);
   if (!c->dma_fork) FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->dma_fork, hipEventDisableTiming));
   while (c->dma_s.size() < segs.size()) {
     hipStream_t t;
@@ -1387,6 +1390,13 @@ ftar_status_t ftar_debug_set_peer_tuning(ftar_comm_t comm, int nt, int lds) {
   return FTAR_SUCCESS;
 }
 // Test/tuning hook (not in ftar.h): the peer forms' cross-GPU copies by the DMA engines.
+ftar_status_t ftar_debug_set_peer_wg_cap(ftar_comm_t comm, size_t wg_per_segment) {
+  if (!comm) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->peer_wg_cap = wg_per_segment;
+  return FTAR_SUCCESS;
+}
+
 // RCCL registration of the comm's scratch buffer (FTAR_RCCL_REGISTER); off drops it at once.
 ftar_status_t ftar_debug_set_rccl_register(ftar_comm_t comm, int on) {
   if (!comm) return FTAR_ERR_INVALID_ARG;

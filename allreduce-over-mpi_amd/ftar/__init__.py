@@ -121,6 +121,7 @@ _lib.ftar_comm_set_peer_direct.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
 _lib.ftar_debug_set_peer_dma.argtypes = [_vp, _int]
 _lib.ftar_debug_set_rccl_register.argtypes = [_vp, _int]
+_lib.ftar_debug_set_peer_wg_cap.argtypes = [_vp, _sz]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
@@ -458,6 +459,16 @@ class Comm:
         passed to register() are always registered with RCCL too, where RCCL accepts them."""
         _check(_lib.ftar_debug_set_rccl_register(self.handle, 1 if on else 0), "rccl_register")
         self._rccl_register = bool(on)
+
+    @property
+    def peer_wg_cap(self):
+        return getattr(self, "_peer_wg_cap", 0)
+
+    @peer_wg_cap.setter
+    def peer_wg_cap(self, n):
+        """Workgroups per segment of the peer forms' cross-GPU copies (0 = as many as a segment fills)."""
+        _check(_lib.ftar_debug_set_peer_wg_cap(self.handle, int(n)), "peer_wg_cap")
+        self._peer_wg_cap = int(n)
 
     def peer_tuning(self, nt=True, lds=True, dma=False):
         """Peer forms: nontemporal copies (nt), the LDS-staged fold (lds; False = register kernel), and the

@@ -408,6 +408,24 @@ def links_driven(world, topology, form):
     return min(XGMI_LINKS, max(widths) - 1)
 
 
+def probe_cap_entries(probe, by_cap, gain=1.10):
+    """Sweep entries for the peer forms' copy-kernel cap: ftar_xgmi_probe measured read/write from all peers
+    uncapped ([min, max] over ranks) and at 4..64 workgroups per peer (min over ranks).  For each direction
+    whose best capped rate beats the uncapped minimum by `gain`, the registered peer form of that direction
+    with that cap ("peer-read-reg:wgN" / "peer-write-reg:wgN")."""
+    out = []
+    for key, form in (("read_all_peers", "peer-read-reg"), ("write_all_peers", "peer-write-reg")):
+        base = probe.get(key)
+        base = base[0] if isinstance(base, (list, tuple)) else base
+        rates = {int(w): v.get(key, 0) for w, v in (by_cap or {}).items()}
+        if not base or not rates:
+            continue
+        w, r = max(rates.items(), key=lambda kv: kv[1])
+        if r > gain * base:
+            out.append(f"{form}:wg{w}")
+    return out
+
+
 RCCL_P2P_FORMS = ("direct", "stages")   # ncclSend/ncclRecv both ways ("collective" ends in ncclAllGather)
 
 
@@ -626,6 +644,8 @@ def bench_distributed(a):
         # ":ncclreg": RCCL p2p between buffers registered with RCCL (ncclCommRegister): the comm's scratch
         # and registered copies of x and y, so RCCL may skip its staging copies where it supports that
         comm.rccl_register = tune == "ncclreg"
+        # ":wgN": the peer forms' cross-GPU copies capped at N workgroups per segment (the probe's best cap)
+        comm.peer_wg_cap = int(tune[2:]) if tune.startswith("wg") else 0
         """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
         rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
         kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
@@ -937,7 +957,10 @@ def bench_distributed(a):
     plan.sort(key=tier)
     sweep_t0 = time.time()
     probed = False
-    for t, chunk, form in plan:
+    i_plan = 0
+    while i_plan < len(plan):
+        t, chunk, form = plan[i_plan]
+        i_plan += 1
         if form.startswith("peer-") and not probed and world > 1:
             # xGMI calibration before the first peer configuration: link rates by copy kernels (read/write,
             # one peer / all peers), every rank at once; min/max over ranks
@@ -961,6 +984,10 @@ def bench_distributed(a):
                     dist.all_reduce(v, op=dist.ReduceOp.MIN)
                     by_cap[w] = {"read_all_peers": round(v[0].item(), 1), "write_all_peers": round(v[1].item(), 1)}
                 state["line"]["xgmi_probe_GBps"]["by_workgroups_per_peer"] = by_cap
+                # where a capped copy beat the uncapped one by > 10 % on every rank, the peer forms get a
+                # sweep entry with that cap next (the same decision on every rank: the rates are MIN-reduced)
+                extra = probe_cap_entries(state["line"]["xgmi_probe_GBps"], by_cap)
+                plan[i_plan:i_plan] = [(t, default_chunk, f) for f in extra]
             except Exception as e:  # noqa: BLE001
                 state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
             try:

@@ -180,3 +180,17 @@ def test_reference_mpi_path_runs_the_reference_on_the_host():
     assert "error" not in d, d
     assert d["kind"] == "reference" and d["P"] == 2 and d["n"] == 1 << 16 and d["topo"] == "1"
     assert 0 < d["min_s"] <= d["first_s"] and d["algbw_GBps_min"] > 0
+
+
+def test_probe_cap_entries_only_where_a_cap_wins():
+    """The peer forms' copy cap is tried only where the xGMI probe saw a capped copy beat the uncapped one by
+    more than 10 % (rates: min over ranks), per direction."""
+    import bench
+    probe = {"read_all_peers": [300.0, 310.0], "write_all_peers": [400.0, 405.0]}
+    by_cap = {4: {"read_all_peers": 200.0, "write_all_peers": 300.0},
+              16: {"read_all_peers": 350.0, "write_all_peers": 420.0},
+              64: {"read_all_peers": 320.0, "write_all_peers": 410.0}}
+    assert bench.probe_cap_entries(probe, by_cap) == ["peer-read-reg:wg16"]
+    assert bench.probe_cap_entries(probe, {8: {"read_all_peers": 100.0, "write_all_peers": 100.0}}) == []
+    assert bench.probe_cap_entries({"error": "x"}, by_cap) == []
+    assert bench.probe_cap_entries(probe, {}) == []

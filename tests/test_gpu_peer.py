@@ -338,6 +338,26 @@ def test_peer_tuning_same_bits(mode, nt, lds, dma, P, topo, dt):
         assert np.array_equal(got[r].view(np.uint8), ref[r].view(np.uint8)), (r, mode, nt, lds)
 
 
+@pytest.mark.parametrize("cap", [1, 4, 64])
+@pytest.mark.parametrize("mode,registered", [("read", True), ("write", True), ("read", False), ("write", False)])
+def test_peer_copy_cap_same_bits(cap, mode, registered):
+    """bench.py's ":wgN" entries cap the peer forms' cross-GPU copies at N workgroups per segment (grid-stride
+    beyond): same bytes, same bits."""
+    P, topo, n = 4, "4", 300_007
+    ins = [fi.fill("f32", 93, r, n) for r in range(P)]
+    g = group(P)
+    for c in g.comms:
+        c.peer_wg_cap = cap
+    try:
+        got = run_peer(ins, topo, dtype=6, mode=mode, registered=registered, outofplace=True)
+    finally:
+        for c in g.comms:
+            c.peer_wg_cap = 0
+    ref = oracle_lib.allreduce(ins, topo, dtype=6, outofplace=True)
+    for r in range(P):
+        assert np.array_equal(got[r].view(np.uint8), ref[r].view(np.uint8)), (r, mode, cap)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_random_soak_registered_subranges(seed):
     """Seeded random calls on SUB-RANGES of registered buffers (ftar_comm_register over a larger allocation,
