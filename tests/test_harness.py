@@ -244,3 +244,29 @@ def test_harness_baseline_sizes_match_oracle(tmp_path, ranks, topo, n, device):
         with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
             got = hashlib.sha256(f.read()).hexdigest()
         assert got == hashlib.sha256(ref[r].tobytes()).hexdigest(), (ranks, topo, n, r)
+
+
+@needs
+def test_harness_exact_mode_single_rank(tmp_path):
+    """--exact at one rank (CPU): the fold of one input is the input, for every repeat."""
+    for rep in (1, 3):
+        p = subprocess.run([MPIEXEC, "-n", "1", BIN, "--size", "100003", "--repeat", str(rep), "--exact"], cwd=tmp_path,
+                           capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0 and "EXACT 0: 100003 elements bit-exact" in p.stdout, p.stdout + p.stderr
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n,repeat,extra", [(8, "1", 1 << 28, 1, []), (8, "8", 1 << 28, 1, []),
+                                                       (2, "1", 1 << 26, 3, ["--device"])])
+def test_harness_whole_bucket_exact_at_c4_size(tmp_path, ranks, topo, n, repeat, extra):
+    """BASELINE configs[3]'s whole 1 GiB fp32 bucket per rank through MPI_Allreduce_FT across 8 MPI processes
+    (the ring and the width-8 tree; host buffers, pinned by MPI_Allreduce_FT_register), and C3's 256 MiB over 3
+    repeated device-resident calls: every element of every rank's buffer is compared bit for bit with the
+    reference's fold of the P identical benchmark.cpp inputs (--exact; no sampling).  The ranks share the box's
+    one GPU (the ipc transport), so this is the drop-in's parity at full size, not an xGMI measurement."""
+    p = subprocess.run([MPIEXEC, "-n", str(ranks), BIN, "--size", str(n), "--repeat", str(repeat), "--exact"] + extra,
+                       cwd=tmp_path, env=dict(os.environ, FT_TOPO=topo), capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(ranks):
+        assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
