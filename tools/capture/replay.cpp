@@ -25,6 +25,10 @@
 // on by all), so no stream joins the capture through another forked stream;
 // the file's own fork waits then become ordinary cross-stream waits and the
 // dependencies stay the same (the begin event carries none).
+// drop kind 'n' (node first): right after the capture begins, one tiny kernel
+// node on the origin stream, so no event of the capture is recorded before the
+// graph has a node (forks from an empty capture are the one shape every
+// crashing log shares).
 // drop kind 'a' (acyclic; diagnostic, changes the dependencies): skip every
 // cross-stream wait that would close a cycle in the relation "stream W waited
 // on an event recorded on stream R" (edge R -> W) -- e.g. the comm and reduce
@@ -192,6 +196,12 @@ int main(int argc, char** argv) {
       scap[x] = true;
       sdeps[x].clear();
       CK(hipStreamBeginCapture(S(x), hipStreamCaptureModeRelaxed));
+      if (drop.find('n') != std::string::npos) {
+        touch<<<1, 64, 0, S(x)>>>(a);
+        node_deps.push_back(sdeps[x]);
+        sdeps[x] = {(int)node_deps.size() - 1};
+        fprintf(stderr, "replay: a kernel node on the origin before any record\n");
+      }
       if (flat) {
         hipEvent_t root;
         CK(hipEventCreateWithFlags(&root, hipEventDisableTiming));
