@@ -535,7 +535,7 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   } else if (!write) {
     const Segment whole{in, X, bytes};
-    FTAR_RETURN_IF(launch_gather(&whole, 1, c->comm_s, c->peer_nt));
+    FTAR_RETURN_IF(c->peer_nt ? launch_copy(in, X, bytes, c->comm_s) : launch_gather(&whole, 1, c->comm_s, false));
     FTAR_RETURN_IF(mark(c, "copy-in", c->comm_s));
     FTAR_RETURN_IF(tp->barrier(c->comm_s));
     FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
@@ -577,7 +577,11 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     if (!zc) {
       segs.clear();
       for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
-      FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt));
+      if (c->peer_nt) {
+        for (const Segment& g : segs) FTAR_RETURN_IF(launch_copy(g.src, g.dst, g.bytes, c->comm_s));
+      } else {
+        FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, false));
+      }
       FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
     }
   }
@@ -967,10 +971,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
     if (sendbuf && count && host)
       FTAR_CHECK_HIP(hipMemcpyAsync(recvbuf, sendbuf, count * esz, hipMemcpyHostToHost, stream));
-    if (sendbuf && count && !host) {
-      const Segment whole{sendbuf, recvbuf, count * esz};
-      return launch_gather(&whole, 1, stream);
-    }
+    if (sendbuf && count && !host) return launch_copy(sendbuf, recvbuf, count * esz, stream);
     return FTAR_SUCCESS;
   }
   if (count == 0) return FTAR_SUCCESS;

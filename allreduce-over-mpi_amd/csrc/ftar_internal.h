@@ -145,7 +145,10 @@ struct Segment {
 // nt: nontemporal loads and stores (the default: cold copies, data not
 // re-read soon); false keeps both in the caches.
 ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true,
-                            size_t max_wg_per_seg = 0);  // 0: enough workgroups for one pass
+                            size_t max_wg_per_seg = 0);
+// One local device copy (k = 1 reduces, the P = 1 AllReduce, the peer forms' local copy-in/out): the
+// LDS-staged kernel when source and destination share their 16-byte alignment, else the copy kernel.
+ftar_status_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);  // 0: enough workgroups for one pass
 size_t dtype_size(ftar_dtype_t dt);
 
 // ---------------------------------------------------------------------------

@@ -62,6 +62,26 @@ hipError_t tr(bool lds, const void* const* srcs, int k, void* dst, size_t count,
 }
 }  // namespace
 
+// The LDS-staged kernel with K = 1 on one-wave workgroups of one tile (U = 1, W = 1; byte traits, so any
+// dtype): 6,530 vs 6,012 GB/s for the multi-segment copy kernel on cold 256 MiB buffers, the best of 17
+// (U, W) shapes (tools/kbench_cold.py --ks 1, profiles/r03/kbench_copy.log).  Sources and destinations
+// whose 16-byte alignments differ take the copy kernel, which handles any alignment.
+ftar_status_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t s) {
+  if (!bytes || src == dst) return FTAR_SUCCESS;
+  const uintptr_t mis = reinterpret_cast<uintptr_t>(dst) & 15;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) != mis) {
+    const Segment seg{src, dst, bytes};
+    return launch_gather(&seg, 1, s);
+  }
+  size_t head = mis ? 16 - mis : 0;
+  if (head > bytes) head = bytes;
+  const size_t nvec = (bytes - head) / 16;
+  const int tail = (int)(bytes - head - nvec * 16);
+  const void* srcs[1] = {src};
+  FTAR_CHECK_HIP((launch_lds<U8Sum, 1, 1, 1>(srcs, dst, nvec, s, (int)head, tail)));
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t count, ftar_dtype_t dt, ftar_op_t op,
                             hipStream_t s, bool round_each, const int* shape, int nlevels, bool lds) {
   if (k < 1 || k > FTAR_MAX_K || !srcs || !dst) return FTAR_ERR_INVALID_ARG;
@@ -69,11 +89,8 @@ ftar_status_t launch_reduce(const void* const* srcs, int k, void* dst, size_t co
   if (count == 0) return FTAR_SUCCESS;
   for (int j = 0; j < k; ++j)
     if (!srcs[j]) return FTAR_ERR_INVALID_ARG;
-  if (k == 1) {  // vector_add/reduce_sum.h:36-47: a copy (streaming copy kernel, not the DMA blit)
-    if (srcs[0] == dst) return FTAR_SUCCESS;
-    const Segment seg{srcs[0], dst, count * dtype_size(dt)};
-    return launch_gather(&seg, 1, s);
-  }
+  if (k == 1)  // vector_add/reduce_sum.h:36-47: a copy (a streaming kernel, not the DMA blit)
+    return launch_copy(srcs[0], dst, count * dtype_size(dt), s);
   hipError_t e = hipErrorInvalidValue;
   if (nlevels > 1 && op == FTAR_SUM && (dt == FTAR_FLOAT32 || dt == FTAR_FLOAT64 || dt == FTAR_BFLOAT16)) {
     TreeCode tc;

@@ -82,9 +82,21 @@ hipError_t variant_k(int v, const void* const* srcs, int k, void* dst, size_t nv
   }
   return variant_prog<Tr, K>(v, srcs, dst, nvec, s);
 }
+// k = 1 (a copy, vector_add/reduce_sum.h:36-47): variant 90 = production (the streaming copy kernel,
+// launch_gather), 40-62 = the LDS-DMA-staged kernel with K = 1 (load to LDS, store from LDS)
+template <class Tr>
+hipError_t variant_copy(int v, const void* const* srcs, void* dst, size_t nvec, hipStream_t s) {
+  if (v == 90) {
+    const Segment seg{srcs[0], dst, nvec * 16};
+    return launch_gather(&seg, 1, s) == FTAR_SUCCESS ? hipSuccess : hipErrorInvalidValue;
+  }
+  return variant_prog<Tr, 1>(v, srcs, dst, nvec, s);
+}
+
 template <class Tr>
 hipError_t variant_tr(int v, const void* const* srcs, int k, void* dst, size_t nvec, hipStream_t s) {
   switch (k) {
+    case 1: return variant_copy<Tr>(v, srcs, dst, nvec, s);
     case 2: return variant_k<Tr, 2>(v, srcs, k, dst, nvec, s);
     case 3: return variant_k<Tr, 3>(v, srcs, k, dst, nvec, s);
     case 4: return variant_k<Tr, 4>(v, srcs, k, dst, nvec, s);
