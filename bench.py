@@ -55,6 +55,10 @@ def parse():
     ap.add_argument("--host-comm", action="store_true",
                     help="N>1 rehearsal on fewer GPUs than ranks: communicator bootstrapped over gloo "
                          "(ftar_comm_init_host, no RCCL), ranks may share a GPU, peer-direct forms only")
+    ap.add_argument("--rccl-loopback", action="store_true",
+                    help="N>1 rehearsal on fewer GPUs than ranks over RCCL itself: every rank gets its own "
+                         "NCCL_HOSTID, so RCCL accepts ranks sharing a GPU and moves ncclSend/ncclRecv over "
+                         "loopback sockets (every RCCL form runs; timings are not xGMI numbers)")
     return ap.parse_args()
 
 
@@ -556,6 +560,12 @@ def bench_distributed(a):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm, rccl_error, rccl_ranks = None, None, None
+    if a.rccl_loopback and not a.host_comm:
+        # one "host" per rank for RCCL: its duplicate-GPU check compares (host hash, bus id), and ranks on
+        # different hosts talk through the network transport (sockets on lo), never IPC or xGMI
+        os.environ["NCCL_HOSTID"] = f"ftar-loopback-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     if not a.host_comm:
         try:
             comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
@@ -848,6 +858,9 @@ def bench_distributed(a):
                        "chunk_bytes": chunk, "form": form, "xgmi_links": links, "parallelism": f"dp{world}"
                        + (f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), host-bootstrapped "
                           "communicator; not an xGMI measurement)" if a.host_comm and world > torch.cuda.device_count()
+                          else f" (rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s), RCCL over loopback "
+                          "sockets, one NCCL_HOSTID per rank; not an xGMI measurement)"
+                          if a.rccl_loopback and world > torch.cuda.device_count()
                           else " (host-bootstrapped communicator: RCCL unavailable, see rccl_init_error)" if a.host_comm else "")},
             "algbw_GBps_per_rank": round(algbw, 2), "busbw_GBps_per_rank": round(busbw, 2),
             "roofline": roof,

@@ -1,0 +1,179 @@
+"""One rank of an RCCL communicator whose ranks share the box's one GPU (run under torchrun).
+
+RCCL refuses two ranks of one communicator on the same device ("Duplicate GPU detected") only when their
+host hashes are equal; NCCL_HOSTID gives every rank its own, so RCCL takes each rank for a separate node and
+carries ncclSend/ncclRecv over its network transport (sockets on the loopback interface).  That is the
+product's RcclTransport -- the replacement of handle_send/handle_recv (mpi_mod.hpp:1254-1305) -- executing
+between ranks, on one GPU: the same plans, streams, pieces and kernels as over xGMI, only the wire differs.
+
+Checks, per rank (written as one JSON line "LOOPBACK {...}"):
+  * every golden case of this world size, all dtypes/ops/lonely layouts, in the three all-gather forms
+    (direct, the reference's stages, collective): the reference's output bits (sha256 per rank);
+  * a larger ragged bucket against the pinned oracle (ring and the widest tree), device and host buffers;
+  * bf16 and RCCL's own ncclAllReduce on the same communicator.
+FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and replays it (capture()).
+"""
+import json
+import os
+import sys
+import traceback
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "allreduce-over-mpi_amd"))
+
+
+def loopback_env(rank):
+    """RCCL settings that let ranks on one GPU form a communicator (every rank its own 'host')."""
+    os.environ["NCCL_HOSTID"] = f"ftar-loopback-{rank}"
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    loopback_env(rank)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import ftar
+    import ftar.dist as fdist
+    import ftar_inputs as fi
+    import golden_cases as gc
+    import oracle_lib
+    from gpu_util import filled_dev, from_dev, to_dev
+
+    max_n = int(os.environ.get("FTAR_LOOPBACK_MAX_N", "70000"))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    res = {"rank": rank, "world": world, "golden": 0, "oracle": 0, "fail": []}
+    comm = fdist.init_comm(device=0)
+    res["rccl"] = True
+
+    def run(x, topo, lonely, dtype, op, outofplace, repeat=1, host=False):
+        n = x.size
+        if host:
+            send = torch.from_numpy(x.copy()).pin_memory() if outofplace else None
+            recv = torch.from_numpy(x.copy()).pin_memory() if not outofplace else torch.empty_like(
+                torch.from_numpy(x)).pin_memory()
+            for _ in range(repeat):
+                comm.allreduce_host(send.data_ptr() if send is not None else None, recv.data_ptr(), n, dtype, op,
+                                    topo_=topo, lonely=lonely)
+            torch.cuda.synchronize()
+            return recv.numpy().copy()
+        s_t, s_p = to_dev(x)
+        if outofplace:
+            r_t, r_p = filled_dev(x.nbytes)
+        else:
+            r_t, r_p = s_t, s_p
+        for it in range(repeat):
+            comm.allreduce(s_p if outofplace else None, r_p, n, dtype, op, topo_=topo, lonely=lonely)
+            if outofplace and it + 1 < repeat:
+                (s_t, s_p), (r_t, r_p) = (r_t, r_p), (s_t, s_p)
+        return from_dev(r_t, x.dtype, n)
+
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "capture":
+        capture(comm, res, world, rank)
+        return finish(comm, res)
+
+    forms = os.environ.get("FTAR_LOOPBACK_FORMS", "direct,stages,collective").split(",")
+    for ag in forms:
+        comm.allgather = ag
+        comm.reduce_scatter = "stages" if ag == "stages" else "direct"
+        for c in gc.allreduce_cases(max_n=max_n, filt=lambda c: c["P"] == world):
+            x = gc.case_inputs(c)[rank]
+            try:
+                out = run(x, c["topo"], c["lonely"], c["dtype"], c["op"], c["outofplace"], c["repeat"])
+                gc.check_output(c, rank, out)
+                res["golden"] += 1
+            except Exception as e:  # noqa: BLE001  reported per case
+                res["fail"].append(f"{ag} {c['id']}: {str(e)[:300]}")
+
+    comm.allgather, comm.reduce_scatter = "direct", "direct"
+    n = (1 << 20) + 13
+    for topo, dt, host in (("1", "f32", False), (str(world), "f32", False), ("1", "f32", True),
+                           (str(world), "bf16", False)):
+        ins = [fi.fill(dt, 77, r, n) for r in range(world)]
+        try:
+            out = run(ins[rank], topo, 0, fi.BY_NAME[dt], 0, True, host=host)
+            ref = oracle_lib.allreduce(ins, topo, 0, dtype=fi.BY_NAME[dt])[rank]
+            np.testing.assert_array_equal(out.view(np.uint8), ref.view(np.uint8))
+            res["oracle"] += 1
+        except Exception as e:  # noqa: BLE001
+            res["fail"].append(f"oracle topo={topo} {dt} host={host}: {str(e)[:300]}")
+
+    # RCCL's own collective on the same communicator (yardstick path of bench.py)
+    try:
+        x = fi.fill("i32", 5, rank, 4099)
+        s_t, s_p = to_dev(x)
+        r_t, r_p = filled_dev(x.nbytes)
+        comm.rccl_allreduce(s_p, r_p, x.size, fi.BY_NAME["i32"], 0)
+        want = np.sum([fi.fill("i32", 5, r, 4099).astype(np.int64) for r in range(world)], axis=0)
+        np.testing.assert_array_equal(from_dev(r_t, np.int32, x.size), want.astype(np.int32))
+        res["nccl_allreduce"] = "ok"
+    except Exception as e:  # noqa: BLE001
+        res["fail"].append(f"ncclAllReduce: {str(e)[:300]}")
+
+    return finish(comm, res)
+
+
+def finish(comm, res):
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    comm.destroy()
+    print("LOOPBACK " + json.dumps(res), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0 if not res["fail"] else 1
+
+
+def capture(comm, res, world, rank):
+    """The product's process model under stream capture at P > 1: one rank per process over an RCCL
+    communicator, ftar_allreduce (ring and the width-P tree, direct and staged forms) captured with
+    torch.cuda.graph and replayed on new inputs; every replay equals the oracle's fold of that replay's
+    inputs.  ncclSend/ncclRecv are captured as graph nodes, as a training step's gradient AllReduce would be."""
+    import numpy as np
+    import torch
+
+    import ftar_inputs as fi
+    import oracle_lib
+    n = (1 << 18) + 7
+    res["captured"] = 0
+    for topo, ag in (("1", "direct"), (str(world), "direct"), ("1", "stages")):
+        try:
+            comm.allgather = ag
+            comm.reduce_scatter = "stages" if ag == "stages" else "direct"
+            x = torch.empty(n, device="cuda")
+            y = torch.empty_like(x)
+            x.copy_(torch.from_numpy(fi.fill("f32", 1, rank, n)))
+            comm.allreduce(x, y, n, "f32", "sum", topo_=topo, stream=torch.cuda.current_stream())   # warm-up
+            torch.cuda.synchronize()
+            s0 = torch.cuda.Stream()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s0):
+                comm.allreduce(x, y, n, "f32", "sum", topo_=topo, stream=s0)
+            for it in range(3):
+                ins = [fi.fill("f32", 100 + it, r, n) for r in range(world)]
+                x.copy_(torch.from_numpy(ins[rank]))
+                y.zero_()
+                torch.cuda.synchronize()
+                g.replay()
+                torch.cuda.synchronize()
+                ref = oracle_lib.allreduce(ins, topo)[rank]
+                np.testing.assert_array_equal(y.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+            del g
+            res["captured"] += 1
+        except Exception as e:  # noqa: BLE001
+            res["fail"].append(f"capture topo={topo} {ag}: {str(e)[:300]}")
+
+
+if __name__ == "__main__":
+    try:
+        sys.exit(main())
+    except Exception:  # noqa: BLE001
+        traceback.print_exc()
+        print("LOOPBACK " + json.dumps({"rank": int(os.environ.get("RANK", -1)), "error": traceback.format_exc()[-1500:]}),
+              flush=True)
+        sys.exit(1)

@@ -25,7 +25,8 @@ def _bench(ranks, extra, env_extra=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
            "--steps", "2", "--warmup", "1", "--elements", str(5 << 24), "--elements-c5", str(1 << 22)] + extra
-    env = dict(os.environ, FTAR_BENCH_BUDGET_S="100", FTAR_BENCH_SWEEP_S="60", **(env_extra or {}))
+    env = dict(os.environ, FTAR_BENCH_BUDGET_S="100", FTAR_BENCH_SWEEP_S="60")
+    env.update(env_extra or {})
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
@@ -60,3 +61,22 @@ def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
     assert why in d["rccl_init_error"], d["rccl_init_error"]
     assert len(d["rccl_error_by_rank"]) == 1 and why in d["rccl_error_by_rank"][0]["error"]
     assert "default" in d["stage_wall_s"] and d.get("rccl_p2p_best") is None
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
+    """The same N > 1 run with RCCL itself carrying the default configuration and every RCCL form of the sweep
+    (--rccl-loopback: one NCCL_HOSTID per rank, ncclSend/ncclRecv over loopback sockets, the ranks sharing the
+    box's GPU): no fallback is taken, the default configuration is RCCL p2p and validates, and rccl_p2p_best is
+    in the line with a validated entry -- the fields the driver's 8-GPU run reports, produced by a real
+    multi-rank RCCL communicator."""
+    d = _bench(ranks, ["--rccl-loopback", "--no-cpu-baseline"], {"FTAR_BENCH_BUDGET_S": "160"})
+    assert d["n_gpus"] == ranks and d["check"] == "ok" and "watchdog" not in d, d
+    assert "rccl_init_error" not in d and "rccl_error_by_rank" not in d, d.get("rccl_init_error")
+    assert d["default_config"]["form"] == "direct" and d["default_config"]["check"] == "ok", d["default_config"]
+    best = d["rccl_p2p_best"]
+    assert best and best["form"].split(":")[0] in ("direct", "stages") and best["ms"] > 0, best
+    rccl_ok = [r for r in d["sweep"] if r.get("check") == "ok" and r["form"].split(":")[0] in ("direct", "stages",
+                                                                                                "collective")]
+    assert rccl_ok and not [r for r in d["sweep"] if r.get("check") == "MISMATCH"], d["sweep"]
+    assert "RCCL over loopback" in d["config"]["parallelism"], d["config"]

@@ -1,0 +1,55 @@
+"""RCCL point-to-point between ranks, on the box's one GPU (tests/rccl_loopback_child.py under torchrun).
+
+The product's RcclTransport (ncclSend/ncclRecv in ncclGroupStart/End; the replacement of the reference's
+handle_send/handle_recv, mpi_mod.hpp:1254-1305) has otherwise only ever run on a 1-rank communicator here,
+because RCCL refuses two ranks of one communicator on the same device.  Giving every rank its own
+NCCL_HOSTID makes RCCL treat them as separate nodes, so its socket transport over the loopback interface
+carries the bytes: every golden case of the world size (per-rank reference bits) in the direct, staged and
+collective forms, plus ragged 2^20 buckets against the oracle through device and host buffers.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_loopback(world, env_extra=None, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(HERE, "rccl_loopback_child.py")]
+    env = dict(os.environ, **(env_extra or {}))
+    p = subprocess.run(cmd, cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True, timeout=timeout)
+    res = [json.loads(ln.split(" ", 1)[1]) for ln in p.stdout.splitlines() if ln.startswith("LOOPBACK ")]
+    return p, sorted(res, key=lambda r: r["rank"])
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_rccl_p2p_between_ranks_matches_reference(world):
+    p, res = run_loopback(world)
+    assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
+    for r in res:
+        assert not r["fail"], r["fail"][:10]
+        assert r["golden"] > 0 and r["oracle"] == 4 and r["nccl_allreduce"] == "ok", r
+    assert len({r["golden"] for r in res}) == 1
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
+    """One rank per process over RCCL (the product's process model), P > 1, under torch.cuda.graph: the
+    ring and the width-P tree in the direct form and the ring in the reference's staged rounds, each captured
+    once and replayed on three new input sets, bit-exact against the oracle on every rank."""
+    p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "capture"})
+    assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
+    for r in res:
+        assert not r["fail"] and r["captured"] == 3, r

@@ -270,3 +270,57 @@ def test_harness_whole_bucket_exact_at_c4_size(tmp_path, ranks, topo, n, repeat,
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(ranks):
         assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
+
+
+def _loopback_mpmd(ranks, args):
+    """mpiexec's MPMD form with one NCCL_HOSTID per rank: RCCL then takes every rank (all on the box's one
+    GPU) for its own node and carries ncclSend/ncclRecv over sockets on the loopback interface, so the drop-in
+    runs its RCCL transport between real MPI processes (tests/rccl_loopback_child.py explains the setting)."""
+    cmd = [MPIEXEC]
+    for r in range(ranks):
+        cmd += ([":"] if r else []) + ["-n", "1", "-env", "NCCL_HOSTID", f"ftar-loopback-{r}", BIN] + args
+    return cmd
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
+@pytest.mark.parametrize("case_id", ["ar_P2_t1_l0_f32_op0_n1048576_lin", "ar_P8_t8_l0_f32_op0_n65536_lin"])
+def test_harness_rccl_transport_reproduces_reference_output(tmp_path, case_id, device):
+    """benchmark.cpp's workload (C1 and the 8-rank width-8 tree) through MPI_Allreduce_FT with
+    FTAR_MPI_TRANSPORT=rccl: the communicator is RCCL's and every block moves by ncclSend/ncclRecv between
+    the MPI processes.  Every rank's buffer has the sha256 of the unmodified reference's output."""
+    import hashlib
+
+    import golden_cases as gc
+    case = next(c for c in gc.manifest()["cases"] if c["id"] == case_id)
+    args = ["--size", str(case["n"]), "--repeat", "1", "--check", "--dump", "out"] + (["--device"] if device else [])
+    env = dict(os.environ, FT_TOPO=case["topo"], FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo",
+               NCCL_IB_DISABLE="1")
+    p = subprocess.run(_loopback_mpmd(case["P"], args), cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(case["P"]):
+        with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == case["sha256"][r], f"{case_id} rank {r}"
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n", [(2, "1", 1 << 24), (4, "2,2", (1 << 22) + 5), (3, "3", 300_007)])
+def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
+    """The same RCCL transport between MPI processes on larger and ragged buckets (host buffers, the
+    piece-pipelined host path over RCCL), each rank's whole buffer against the pinned oracle."""
+    import hashlib
+
+    import numpy as np
+    import oracle_lib
+    env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    p = subprocess.run(_loopback_mpmd(ranks, ["--size", str(n), "--repeat", "2", "--dump", "out"]), cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    x = (np.arange(n, dtype=np.float64).astype(np.float32) * np.float32(0.1)).astype(np.float32)
+    ref = oracle_lib.allreduce(oracle_lib.allreduce([x] * ranks, topo), topo)   # two calls in place
+    for r in range(ranks):
+        with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == hashlib.sha256(ref[r].tobytes()).hexdigest(), r
