@@ -33,6 +33,11 @@
 // identical operands every fold order of the ring, :1689-1703, and of a
 // single-stage tree, :1316-1358, gives these partial sums).  Needs no dump,
 // so it checks whole BASELINE-sized buckets (1 GiB per rank) in place.
+// --graph (with --device): one MPI_Allreduce_FT_device call is captured into a
+// HIP graph on a stream of its own (after one uncaptured call that brings the
+// communicator and its buffers up, inputs restarted), and every warm-up and
+// timed call replays the graph (hipGraphLaunch + hipStreamSynchronize): the
+// same in-place AllReduce, so --check / --exact / --dump apply unchanged.
 #include <hip/hip_runtime_api.h>
 
 #include <chrono>
@@ -91,6 +96,7 @@ int main(int argc, char** argv) {
   size_t data_len = 35;
   int repeat = 1, warmup = 0, comm_cycle = 0, comm_threads = 0;
   bool to_file = false, check = false, device = false, do_register = true, register_check = false, exact = false;
+  bool graph = false;
   std::string tag, comm_type = "flextree", dump;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -107,6 +113,7 @@ int main(int argc, char** argv) {
     else if (a == "--check") check = true;
     else if (a == "--exact") exact = true;
     else if (a == "--device") device = true;
+    else if (a == "--graph") graph = true;
     else if (a == "--dump") dump = next();
     else if (a == "--no-register") do_register = false;
     else if (a == "--comm-cycle") comm_cycle = atoi(next().c_str());
@@ -121,6 +128,7 @@ int main(int argc, char** argv) {
   if (comm_type == "ftar") comm_type = "flextree";
   if (comm_type != "flextree" && comm_type != "mpi") die(rank, "unknown comm type: " + comm_type);
   if (device && comm_type == "mpi") die(rank, "--device needs --comm-type flextree");
+  if (graph && !device) die(rank, "--graph needs --device");
 
   std::vector<float> data(data_len);
   const float base = 0.1f;
@@ -154,11 +162,35 @@ int main(int argc, char** argv) {
     fflush(stdout);
   }
 
+  hipStream_t gstream = nullptr;
+  hipGraphExec_t gexec = nullptr;
   auto one_call = [&]() -> int {
     if (comm_type == "mpi") return MPI_Allreduce(MPI_IN_PLACE, data.data(), (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
+    if (gexec) return hipGraphLaunch(gexec, gstream) == hipSuccess && hipStreamSynchronize(gstream) == hipSuccess
+                          ? MPI_SUCCESS : MPI_ERR_OTHER;
     if (device) return MPI_Allreduce_FT_device(MPI_IN_PLACE, dptr, (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD, nullptr);
     return MPI_Allreduce_FT(MPI_IN_PLACE, data.data(), (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD);
   };
+  if (graph) {  // prime uncaptured (bring-up, settings agreement, scratch growth), restart, capture one call
+    if (int rc = one_call()) call_failed(rank, P, "graph priming call", rc);
+    if (hipMemcpy(dptr, data.data(), data_len * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+      die(rank, "hipMemcpy failed");
+    hipGraph_t g = nullptr;
+    if (hipStreamCreateWithFlags(&gstream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamBeginCapture(gstream, hipStreamCaptureModeRelaxed) != hipSuccess)
+      die(rank, "hipStreamBeginCapture failed");
+    const int rc = MPI_Allreduce_FT_device(MPI_IN_PLACE, dptr, (int)data_len, MPI_FLOAT, MPI_SUM, MPI_COMM_WORLD,
+                                           gstream);
+    const hipError_t ec = hipStreamEndCapture(gstream, &g);
+    if (rc != MPI_SUCCESS) call_failed(rank, P, "captured call", rc);
+    if (ec != hipSuccess || hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0) != hipSuccess)
+      die(rank, std::string("graph capture failed: ") + hipGetErrorString(ec));
+    size_t nodes = 0;
+    (void)hipGraphGetNodes(g, nullptr, &nodes);
+    (void)hipGraphDestroy(g);
+    printf("GRAPH %d: captured %zu nodes\n", rank, nodes);
+    fflush(stdout);
+  }
 
   // warm-up calls change the data (in place, x P each); restart from i*0.1 afterwards
   for (int i = 0; i < warmup; ++i)
@@ -337,6 +369,8 @@ int main(int argc, char** argv) {
   int lifecycle_bad_all = 0;
   MPI_Allreduce(&lifecycle_bad, &lifecycle_bad_all, 1, MPI_INT, MPI_SUM, MPI_COMM_WORLD);
 
+  if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (gstream) (void)hipStreamDestroy(gstream);
   if (device) (void)hipFree(dptr);
   if (registered) MPI_Allreduce_FT_unregister(data.data());
   MPI_Allreduce_FT_finalize();

@@ -31,6 +31,8 @@ def loopback_env(rank):
 
 
 def main():
+    import faulthandler
+    faulthandler.enable()   # a crash inside the runtime still names the Python line it came from
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     loopback_env(rank)
     import numpy as np
@@ -152,8 +154,11 @@ def capture(comm, res, world, rank):
             torch.cuda.synchronize()
             s0 = torch.cuda.Stream()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s0):
+            sys.stderr.write(f"[rank {rank}] capture topo={topo} {ag}: begin\n")
+            with torch.cuda.graph(g, stream=s0,
+                                  capture_error_mode=os.environ.get("FTAR_LOOPBACK_CAPTURE_MODE", "global")):
                 comm.allreduce(x, y, n, "f32", "sum", topo_=topo, stream=s0)
+            sys.stderr.write(f"[rank {rank}] capture topo={topo} {ag}: captured\n")
             for it in range(3):
                 ins = [fi.fill("f32", 100 + it, r, n) for r in range(world)]
                 x.copy_(torch.from_numpy(ins[rank]))

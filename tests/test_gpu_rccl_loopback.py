@@ -44,6 +44,11 @@ def test_rccl_p2p_between_ranks_matches_reference(world):
     assert len({r["golden"] for r in res}) == 1
 
 
+@pytest.mark.capture_runtime_limit
+@pytest.mark.xfail(reason="torch's bundled HIP 7.0 runtime: SIGSEGV inside hipStreamEndCapture (torch capture_end, "
+                          "global and relaxed modes; profiles/r03/loopback/capture_py*.log); the same capture "
+                          "from C++ on /opt/rocm 7.2 passes (test_harness_rccl_allreduce_captured_in_a_hip_graph)",
+                   strict=False)
 @pytest.mark.parametrize("world", [2, 4])
 def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
     """One rank per process over RCCL (the product's process model), P > 1, under torch.cuda.graph: the

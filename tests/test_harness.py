@@ -324,3 +324,22 @@ def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
     for r in range(ranks):
         with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
             assert hashlib.sha256(f.read()).hexdigest() == hashlib.sha256(ref[r].tobytes()).hexdigest(), r
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n", [(2, "1", (1 << 20) + 3), (2, "2", 65537), (4, "1", 100_003),
+                                          (4, "4", 100_003), (4, "2,2", 4099)])
+def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n):
+    """The product's process model under stream capture at P > 1: one MPI process per rank over an RCCL
+    communicator (FTAR_MPI_TRANSPORT=rccl, loopback sockets), MPI_Allreduce_FT_device captured once into a
+    HIP graph from plain C++ on /opt/rocm's runtime (ftar_benchmark --graph), then 3 replays in place: every
+    element bit-exact against the reference's fold of the P identical inputs (--exact) on every rank."""
+    env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    args = ["--size", str(n), "--repeat", "3", "--device", "--graph", "--exact"]
+    p = subprocess.run(_loopback_mpmd(ranks, args), cwd=tmp_path, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(ranks):
+        assert re.search(rf"GRAPH {r}: captured \d+ nodes", p.stdout), p.stdout[-3000:]
+        assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
