@@ -343,3 +343,19 @@ def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n
     for r in range(ranks):
         assert re.search(rf"GRAPH {r}: captured \d+ nodes", p.stdout), p.stdout[-3000:]
         assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("ranks,topo,n,extra", [(2, "1", 1 << 26, ["--device"]), (8, "8", 1 << 28, []),
+                                                (8, "1", 1 << 28, [])])
+def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, extra):
+    """BASELINE sizes through the RCCL transport between MPI processes (loopback sockets): C3's 256 MiB
+    device-resident with 2 ranks, and C4's whole 1 GiB host bucket per rank with 8 ranks on the width-8 tree
+    and on the ring (many pipeline pieces per block); every element of every rank bit-exact (--exact)."""
+    env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    p = subprocess.run(_loopback_mpmd(ranks, ["--size", str(n), "--repeat", "1", "--exact"] + extra), cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
+    for r in range(ranks):
+        assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
