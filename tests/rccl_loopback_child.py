@@ -11,7 +11,8 @@ Checks, per rank (written as one JSON line "LOOPBACK {...}"):
     (direct, the reference's stages, collective): the reference's output bits (sha256 per rank);
   * a larger ragged bucket against the pinned oracle (ring and the widest tree), device and host buffers;
   * bf16 and RCCL's own ncclAllReduce on the same communicator.
-FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and replays it (capture()).
+FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and replays it (capture());
+FTAR_LOOPBACK_MODE=soak runs seeded random cases with random per-call settings (soak()).
 """
 import json
 import os
@@ -78,6 +79,9 @@ def main():
     if os.environ.get("FTAR_LOOPBACK_MODE") == "capture":
         capture(comm, res, world, rank)
         return finish(comm, res)
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "soak":
+        soak(comm, res, world, rank, run, int(os.environ.get("FTAR_LOOPBACK_SOAK", "40")))
+        return finish(comm, res)
 
     forms = os.environ.get("FTAR_LOOPBACK_FORMS", "direct,stages,collective").split(",")
     for ag in forms:
@@ -129,6 +133,42 @@ def finish(comm, res):
     dist.barrier()
     dist.destroy_process_group()
     return 0 if not res["fail"] else 1
+
+
+def soak(comm, res, world, rank, run, count):
+    """Seeded random cases of this world size (tests/random_cases.py: ring, trees, lonely layouts, every dtype,
+    SUM and BAND, ragged sizes down to 0 and 1 element, in place or out of place) over RCCL, each with a random
+    pipeline piece size, data-movement form and device or pinned-host buffers; every rank against the oracle.
+    Every rank draws the same sequence, so the per-call settings agree across ranks."""
+    import random
+
+    import ftar_inputs as fi
+    import random_cases
+    rng = random.Random(4242 + world)
+    res["soak"] = 0
+    seed = 900 + world
+    while res["soak"] < count:
+        for c in random_cases.cases(seed=seed, count=60, max_p=world):
+            if c["P"] != world or res["soak"] >= count:
+                continue
+            form = rng.choice(["direct", "stages", "collective"])
+            chunk = rng.choice([0, 256, 4096, 1 << 16])
+            host = rng.random() < 0.4
+            try:
+                comm.allgather = form
+                comm.reduce_scatter = "stages" if form == "stages" else "direct"
+                comm.chunk_bytes = chunk
+                comm.host_chunk_bytes = chunk
+                out = run(c["ins"][rank], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]],
+                          0 if c["op"] == "sum" else 1, c["oop"], host=host)
+                if out.tobytes() != c["ref"][rank].tobytes():
+                    raise AssertionError("differs from the oracle")
+                res["soak"] += 1
+            except Exception as e:  # noqa: BLE001
+                res["fail"].append(f"soak P={world} topo={c['topo']}+{c['lonely']} n={c['n']} {c['dtype']} "
+                                   f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host}: {str(e)[:200]}")
+                return
+        seed += 1000
 
 
 def capture(comm, res, world, rank):
