@@ -101,6 +101,7 @@ struct ftar_comm {
   // (peer_allreduce_host); FTAR_HOST_PEER_PIPELINE=0 takes the whole-bucket path instead (A/B)
   bool host_peer_pipeline = true;
   bool capturing = false;  // the current call's stream is being captured: no allocation, no host sync
+  bool serial = false;     // ... and every internal stream is the caller's (serial_capture)
   // events handed to captured calls: each captured call records a fresh set
   // (an event is never re-recorded inside one capture), kept until teardown
   std::vector<hipEvent_t> captured_events;
@@ -471,6 +472,11 @@ namespace {
 // peer_dma one DMA copy per segment, each on its own stream, all joined back into comm_s
 ftar_status_t peer_copy(ftar_comm* c, const std::vector<Segment>& segs) {
   if (!c->peer_dma) return launch_gather(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt, c->peer_wg_cap);
+  if (c->serial) {  // a serial capture: the DMA copies in turn on the one stream
+    for (const Segment& g : segs)
+      if (g.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(g.dst, g.src, g.bytes, hipMemcpyDeviceToDevice, c->comm_s));
+    return FTAR_SUCCESS;
+  }
   if (!c->dma_fork) FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->dma_fork, hipEventDisableTiming));
   while (c->dma_s.size() < segs.size()) {
     hipStream_t t;
@@ -922,6 +928,20 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
 // previous call's first waits for that call's completion marker (recorded on
 // its stream after every internal stream joined it), so its transfers cannot
 // overwrite scratch the previous call's reduces are still reading.
+// Serial capture: a captured call issues everything on the caller's stream (FTAR_CAPTURE_SERIAL=1 / 0;
+// default on when the loaded HIP runtime is older than 7.2).  torch 2.10 bundles HIP 7.0, whose
+// hipStreamEndCapture dies (SIGSEGV, unbounded recursion) on the graph the forked comm/reduce streams and
+// their per-piece cross waits leave, while 7.2 captures it; a chain in issue order keeps every
+// dependency and gives up only the comm/reduce overlap inside the graph.
+bool serial_capture() {
+  static const bool on = [] {
+    if (const char* e = getenv("FTAR_CAPTURE_SERIAL")) return *e != '0';
+    int v = 0;
+    return hipRuntimeGetVersion(&v) != hipSuccess || v < 70200000;  // major*1e7 + minor*1e5 + patch
+  }();
+  return on;
+}
+
 ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
                         const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr) {
   if (!c) return FTAR_ERR_INVALID_ARG;
@@ -945,7 +965,16 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   if (!capturing && c->done_recorded && c->done_stream != stream)
     FTAR_CHECK_HIP(hipStreamWaitEvent(stream, c->done_ev, 0));
   c->capturing = capturing;
+  // serial capture: every internal stream is the caller's for this call, so the captured graph is one
+  // chain in issue order (every wait refers to an event recorded earlier in that order, so the chain keeps
+  // every dependency; the comm/reduce overlap is given up inside the graph)
+  const bool serial = capturing && serial_capture();
+  hipStream_t saved[4] = {c->comm_s, c->red_s, c->h2d_s, c->d2h_s};
+  if (serial) c->comm_s = c->red_s = c->h2d_s = c->d2h_s = stream;
+  c->serial = serial;
   const ftar_status_t st = allreduce_locked(sendbuf, recvbuf, count, dt, op, topo, c, stream, host);
+  if (serial) c->comm_s = saved[0], c->red_s = saved[1], c->h2d_s = saved[2], c->d2h_s = saved[3];
+  c->serial = false;
   c->capturing = false;
   if (st == FTAR_SUCCESS && !capturing) {
     FTAR_CHECK_HIP(hipEventRecord(c->done_ev, stream));

@@ -59,6 +59,15 @@ static void die(int rank, const std::string& msg) {
   MPI_Abort(MPI_COMM_WORLD, 1);
 }
 
+// A bad command line: every rank parses the same arguments, so every rank ends here and the job ends
+// cleanly (MPI_Finalize, exit code 1).  MPI_Abort could kill the job before mpiexec forwarded the message.
+[[noreturn]] static void usage_error(int rank, const std::string& msg) {
+  fprintf(stderr, "[rank %d] %s\n", rank, msg.c_str());
+  fflush(stderr);
+  MPI_Finalize();
+  exit(1);
+}
+
 // A failed MPI_Allreduce_FT.  The reference exit(1)s inside the call (an
 // invalid FT_TOPO, mpi_mod.hpp:1471-1475); here the call returned an MPI error
 // class.  An argument error fails every rank at the same call, so the ranks
@@ -101,7 +110,7 @@ int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
-      if (i + 1 >= argc) die(rank, "missing value for " + a);
+      if (i + 1 >= argc) usage_error(rank, "missing value for " + a);
       return argv[++i];
     };
     if (a == "--size") data_len = strtoull(next().c_str(), nullptr, 0);
@@ -123,12 +132,12 @@ int main(int argc, char** argv) {
       if (rank == 0) printf("ftar_benchmark: %s\n", ftar_version());
       MPI_Finalize();
       return 0;
-    } else die(rank, "unknown parameter: " + a);
+    } else usage_error(rank, "unknown parameter: " + a);
   }
   if (comm_type == "ftar") comm_type = "flextree";
-  if (comm_type != "flextree" && comm_type != "mpi") die(rank, "unknown comm type: " + comm_type);
-  if (device && comm_type == "mpi") die(rank, "--device needs --comm-type flextree");
-  if (graph && !device) die(rank, "--graph needs --device");
+  if (comm_type != "flextree" && comm_type != "mpi") usage_error(rank, "unknown comm type: " + comm_type);
+  if (device && comm_type == "mpi") usage_error(rank, "--device needs --comm-type flextree");
+  if (graph && !device) usage_error(rank, "--graph needs --device");
 
   std::vector<float> data(data_len);
   const float base = 0.1f;

@@ -478,18 +478,27 @@ def test_allreduce_group_captures_into_a_hip_graph(topo):
     assert p.returncode == 0 and "group capture ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-3000:])
 
 
+@pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 0, True),
+                                                       (4, "2,2", "stages", "stages", 4096, True)])
+def test_allreduce_group_captures_on_the_torch_runtime(tmp_path, P, topo, rs, ag, chunk, shared):
+    """In-process groups on the capture stream through torch.cuda.graph (torch's bundled HIP 7.0 runtime), in a
+    child process: 2 ranks one piece per block, and 4 ranks of a (2,2) tree in the staged rounds with 4 KiB
+    pieces.  On that runtime every captured call issues serially on its stream (serial_capture, engine.cpp):
+    the forked comm/reduce streams crashed hipStreamEndCapture there (rounds 1-3)."""
+    _capture_in_child(tmp_path, P, topo, rs, ag, chunk, shared)
+
+
 @pytest.mark.capture_runtime_limit
-@pytest.mark.xfail(reason="HIP runtime: hipStreamEndCapture recurses without end on these capture graphs (also "
-                          "the torch-bundled 7.0 runtime on the 2-rank shape); a single-threaded event-only "
+@pytest.mark.xfail(reason="HIP 7.0 runtime (torch): hipStreamEndCapture recurses without end once the caller "
+                          "forks one stream per rank from the capture stream; a single-threaded event-only "
                           "reproducer is in profiles/r03/capture/ (tools/capture/replay.cpp), DESIGN §4",
                    strict=False)
-@pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 0, True),
-                                                       (2, "1", "direct", "direct", 4096, False),
-                                                       (4, "2,2", "stages", "stages", 4096, True)])
+@pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 4096, False)])
 def test_allreduce_group_capture_runtime_limits(tmp_path, P, topo, rs, ag, chunk, shared):
-    """The capture shapes the HIP runtime cannot end (torch's runtime, more ranks, several pieces, or a stream
-    forked per rank), through torch.cuda.graph in a child process: kept as expected failures so a runtime that
-    handles them shows up as XPASS."""
+    """The capture shape the torch runtime still cannot end (a stream forked per rank by the caller, each
+    rank's call serial on its own stream, the ranks' streams cross-waiting for their transfers), through
+    torch.cuda.graph in a child process: kept as an expected failure so a runtime that handles it shows up as
+    XPASS."""
     _capture_in_child(tmp_path, P, topo, rs, ag, chunk, shared)
 
 

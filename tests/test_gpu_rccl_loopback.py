@@ -44,16 +44,15 @@ def test_rccl_p2p_between_ranks_matches_reference(world):
     assert len({r["golden"] for r in res}) == 1
 
 
-@pytest.mark.capture_runtime_limit
-@pytest.mark.xfail(reason="torch's bundled HIP 7.0 runtime: SIGSEGV inside hipStreamEndCapture (torch capture_end, "
-                          "global and relaxed modes; profiles/r03/loopback/capture_py*.log); the same capture "
-                          "from C++ on /opt/rocm 7.2 passes (test_harness_rccl_allreduce_captured_in_a_hip_graph)",
-                   strict=False)
 @pytest.mark.parametrize("world", [2, 4])
 def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
     """One rank per process over RCCL (the product's process model), P > 1, under torch.cuda.graph: the
     ring and the width-P tree in the direct form and the ring in the reference's staged rounds, each captured
-    once and replayed on three new input sets, bit-exact against the oracle on every rank."""
+    once and replayed on three new input sets, bit-exact against the oracle on every rank.  torch's bundled HIP
+    7.0 runtime died in hipStreamEndCapture on the forked comm/reduce streams (profiles/r03/loopback/
+    capture_py_relaxed.log), so on runtimes before 7.2 a captured call issues serially on its stream
+    (serial_capture, engine.cpp); from C++ on 7.2 the forked form captures
+    (test_harness_rccl_allreduce_captured_in_a_hip_graph)."""
     p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "capture"})
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:

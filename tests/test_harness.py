@@ -328,14 +328,19 @@ def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("ranks,topo,n", [(2, "1", (1 << 20) + 3), (2, "2", 65537), (4, "1", 100_003),
-                                          (4, "4", 100_003), (4, "2,2", 4099)])
-def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n):
+@pytest.mark.parametrize("ranks,topo,n,serial", [(2, "1", (1 << 20) + 3, "0"), (2, "2", 65537, "0"),
+                                                 (4, "1", 100_003, "0"), (4, "4", 100_003, "0"),
+                                                 (4, "2,2", 4099, "0"), (2, "1", (1 << 20) + 3, "1"),
+                                                 (4, "2,2", 4099, "1")])
+def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n, serial):
     """The product's process model under stream capture at P > 1: one MPI process per rank over an RCCL
     communicator (FTAR_MPI_TRANSPORT=rccl, loopback sockets), MPI_Allreduce_FT_device captured once into a
     HIP graph from plain C++ on /opt/rocm's runtime (ftar_benchmark --graph), then 3 replays in place: every
-    element bit-exact against the reference's fold of the P identical inputs (--exact) on every rank."""
-    env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    element bit-exact against the reference's fold of the P identical inputs (--exact) on every rank.  Both
+    capture forms: the forked comm/reduce streams (7.2's default) and the serial one (FTAR_CAPTURE_SERIAL=1,
+    the default on older runtimes)."""
+    env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+               FTAR_CAPTURE_SERIAL=serial)
     args = ["--size", str(n), "--repeat", "3", "--device", "--graph", "--exact"]
     p = subprocess.run(_loopback_mpmd(ranks, args), cwd=tmp_path, env=env, capture_output=True, text=True,
                        timeout=240)
