@@ -30,12 +30,13 @@ def random_topology(rng, P):
     return rng.choice(opts)
 
 
-def cases(seed, count, max_p=12, max_n=40000):
+def cases(seed, count, max_p=12, max_n=40000, P_fixed=None):
+    """count cases; P uniform in 2..max_p, or P_fixed for every case."""
     import ftar_inputs as fi
     rng = random.Random(seed)
     out = []
     while len(out) < count:
-        P = rng.randint(2, max_p)
+        P = P_fixed or rng.randint(2, max_p)
         topo, lonely = random_topology(rng, P)
         n = rng.choice([0, 1, P - 1, P, P + 1, rng.randint(2, 200), rng.randint(200, max_n)])
         dt = rng.choice(["f32", "f32", "f32", "bf16", "f64", "i32", "u8", "i16", "i64", "bool"])

@@ -146,29 +146,24 @@ def soak(comm, res, world, rank, run, count):
     import random_cases
     rng = random.Random(4242 + world)
     res["soak"] = 0
-    seed = 900 + world
-    while res["soak"] < count:
-        for c in random_cases.cases(seed=seed, count=60, max_p=world):
-            if c["P"] != world or res["soak"] >= count:
-                continue
-            form = rng.choice(["direct", "stages", "collective"])
-            chunk = rng.choice([0, 256, 4096, 1 << 16])
-            host = rng.random() < 0.4
-            try:
-                comm.allgather = form
-                comm.reduce_scatter = "stages" if form == "stages" else "direct"
-                comm.chunk_bytes = chunk
-                comm.host_chunk_bytes = chunk
-                out = run(c["ins"][rank], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]],
-                          0 if c["op"] == "sum" else 1, c["oop"], host=host)
-                if out.tobytes() != c["ref"][rank].tobytes():
-                    raise AssertionError("differs from the oracle")
-                res["soak"] += 1
-            except Exception as e:  # noqa: BLE001
-                res["fail"].append(f"soak P={world} topo={c['topo']}+{c['lonely']} n={c['n']} {c['dtype']} "
-                                   f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host}: {str(e)[:200]}")
-                return
-        seed += 1000
+    for c in random_cases.cases(seed=900 + world, count=count, P_fixed=world):
+        form = rng.choice(["direct", "stages", "collective"])
+        chunk = rng.choice([0, 256, 4096, 1 << 16])
+        host = rng.random() < 0.4
+        try:
+            comm.allgather = form
+            comm.reduce_scatter = "stages" if form == "stages" else "direct"
+            comm.chunk_bytes = chunk
+            comm.host_chunk_bytes = chunk
+            out = run(c["ins"][rank], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]],
+                      0 if c["op"] == "sum" else 1, c["oop"], host=host)
+            if out.tobytes() != c["ref"][rank].tobytes():
+                raise AssertionError("differs from the oracle")
+            res["soak"] += 1
+        except Exception as e:  # noqa: BLE001
+            res["fail"].append(f"soak P={world} topo={c['topo']}+{c['lonely']} n={c['n']} {c['dtype']} "
+                               f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host}: {str(e)[:200]}")
+            return
 
 
 def capture(comm, res, world, rank):

@@ -59,10 +59,10 @@ def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
         assert not r["fail"] and r["captured"] == 3, r
 
 
-@pytest.mark.parametrize("world", [2, 3, 5, 6])
+@pytest.mark.parametrize("world", [2, 3, 5, 6, 7, 8])
 def test_rccl_p2p_random_soak(world):
-    """Seeded random cases of the world size over RCCL (lonely layouts at P = 3, 5, 6 included), each with its
-    own piece size, data-movement form and device or pinned-host buffers, bit-exact against the oracle."""
+    """Seeded random cases of the world size over RCCL, each with its own piece size, data-movement form and
+    device or pinned-host buffers, bit-exact against the oracle (lonely layouts at P = 5, 6, 7 and 8)."""
     p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "soak"})
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
