@@ -54,6 +54,10 @@ TOPOS = [
     (8, "8", 0), (8, "2,4", 0), (8, "4,2", 0), (8, "2,2,2", 0), (9, "3,3", 0),
     (5, "2,2", 1), (7, "2,3", 1), (7, "3,2", 1), (9, "2,4", 1), (6, "2,2", 2), (8, "3,2", 2),
     (9, "2,2,2", 1),
+    # round 3: node-scale layouts past one 8-GPU node (the reference cost model picks 2,5 at P = 10 and 2,6 at
+    # P = 12), four- and two-level trees of 16, and lonely ranks at P = 11, 13, 14
+    (10, "2,5", 0), (12, "2,6", 0), (12, "3,4", 0), (12, "2,2,3", 0), (16, "1", 0), (16, "16", 0),
+    (16, "4,4", 0), (16, "2,2,2,2", 0), (11, "2,5", 1), (13, "3,4", 1), (14, "2,3,2", 2),
 ]
 SIZES = [1, 3, 7, 17, 1003, 65541]
 
