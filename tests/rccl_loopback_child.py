@@ -124,12 +124,21 @@ def main():
     return finish(comm, res)
 
 
+def write_result(res):
+    """one file per rank (FTAR_LOOPBACK_OUT): ranks share stdout, where their lines can interleave"""
+    d = os.environ.get("FTAR_LOOPBACK_OUT")
+    if d:
+        with open(os.path.join(d, f"rank{res['rank']}.json"), "w") as f:
+            json.dump(res, f)
+
+
 def finish(comm, res):
     import torch
     import torch.distributed as dist
     torch.cuda.synchronize()
     comm.destroy()
     print("LOOPBACK " + json.dumps(res), flush=True)
+    write_result(res)
     dist.barrier()
     dist.destroy_process_group()
     return 0 if not res["fail"] else 1
@@ -214,6 +223,7 @@ if __name__ == "__main__":
         sys.exit(main())
     except Exception:  # noqa: BLE001
         traceback.print_exc()
-        print("LOOPBACK " + json.dumps({"rank": int(os.environ.get("RANK", -1)), "error": traceback.format_exc()[-1500:]}),
-              flush=True)
+        err = {"rank": int(os.environ.get("RANK", -1)), "error": traceback.format_exc()[-1500:]}
+        print("LOOPBACK " + json.dumps(err), flush=True)
+        write_result(err)
         sys.exit(1)

@@ -12,6 +12,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -26,12 +27,19 @@ def _port():
 
 
 def run_loopback(world, env_extra=None, timeout=300):
+    """(completed process, every rank's result dict, by rank); each rank writes its own result file"""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(HERE, "rccl_loopback_child.py")]
-    env = dict(os.environ, **(env_extra or {}))
-    p = subprocess.run(cmd, cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True, timeout=timeout)
-    res = [json.loads(ln.split(" ", 1)[1]) for ln in p.stdout.splitlines() if ln.startswith("LOOPBACK ")]
-    return p, sorted(res, key=lambda r: r["rank"])
+    with tempfile.TemporaryDirectory() as out:
+        env = dict(os.environ, FTAR_LOOPBACK_OUT=out, **(env_extra or {}))
+        p = subprocess.run(cmd, cwd=os.path.dirname(HERE), env=env, capture_output=True, text=True, timeout=timeout)
+        res = []
+        for r in range(world):
+            path = os.path.join(out, f"rank{r}.json")
+            if os.path.exists(path):
+                with open(path) as f:
+                    res.append(json.load(f))
+    return p, res
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
