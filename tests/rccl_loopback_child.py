@@ -12,7 +12,8 @@ Checks, per rank (written as one JSON line "LOOPBACK {...}"):
   * a larger ragged bucket against the pinned oracle (ring and the widest tree), device and host buffers;
   * bf16 and RCCL's own ncclAllReduce on the same communicator.
 FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and replays it (capture());
-FTAR_LOOPBACK_MODE=soak runs seeded random cases with random per-call settings (soak()).
+FTAR_LOOPBACK_MODE=soak runs seeded random cases with random per-call settings (soak());
+FTAR_LOOPBACK_MODE=ddp trains through DistributedDataParallel with ftar's comm hook (ddp()).
 """
 import json
 import os
@@ -78,6 +79,9 @@ def main():
 
     if os.environ.get("FTAR_LOOPBACK_MODE") == "capture":
         capture(comm, res, world, rank)
+        return finish(comm, res)
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "ddp":
+        ddp(comm, res, world, rank)
         return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "soak":
         soak(comm, res, world, rank, run, int(os.environ.get("FTAR_LOOPBACK_SOAK", "40")))
@@ -173,6 +177,58 @@ def soak(comm, res, world, rank, run, count):
             res["fail"].append(f"soak P={world} topo={c['topo']}+{c['lonely']} n={c['n']} {c['dtype']} "
                                f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host}: {str(e)[:200]}")
             return
+
+
+def ddp(comm, res, world, rank):
+    """DistributedDataParallel with ftar as its gradient AllReduce (ftar.ddp.allreduce_hook) against DDP's own
+    gloo AllReduce: the same model, the same per-rank batches, 3 SGD steps, small buckets (several per step).
+    At P = 2 the gradients are bit-identical (one rounded add either way, / 2 exact); at P = 4 the two sum in
+    different orders, so they agree to a relative 1e-5 of each tensor's largest gradient."""
+    import copy
+
+    import torch
+    import torch.distributed as dist
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    import ftar.ddp
+    torch.manual_seed(1234)
+    net = torch.nn.Sequential(torch.nn.Linear(256, 1024), torch.nn.ReLU(), torch.nn.Linear(1024, 1000),
+                              torch.nn.ReLU(), torch.nn.Linear(1000, 10)).cuda()
+    a = DDP(copy.deepcopy(net), device_ids=[0], bucket_cap_mb=1)
+    b = DDP(copy.deepcopy(net), device_ids=[0], bucket_cap_mb=1)
+    state = ftar.ddp.HookState(comm)
+    a.register_comm_hook(state, ftar.ddp.allreduce_hook)
+    oa = torch.optim.SGD(a.parameters(), lr=0.05)
+    ob = torch.optim.SGD(b.parameters(), lr=0.05)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(99 + rank)
+    worst = 0.0
+    for step in range(3):
+        x = torch.randn(64, 256, device="cuda", generator=g)
+        y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        for pa, pb in zip(a.parameters(), b.parameters()):
+            if world == 2:   # a + b is one rounding either way, and / 2 is exact: identical bits
+                if not torch.equal(pa.grad, pb.grad):
+                    res["fail"].append(f"ddp step {step}: gradient differs from DDP's own AllReduce")
+                    return
+            else:
+                worst = max(worst, ((pa.grad - pb.grad).abs().max() / pb.grad.abs().max().clamp_min(1e-30)).item())
+        oa.step()
+        ob.step()
+    res["ddp_hook_calls"] = state.calls
+    res["ddp_worst_rel"] = worst
+    if world != 2 and worst > 1e-5:
+        res["fail"].append(f"ddp: gradients differ by {worst:.3g} (relative) from DDP's own AllReduce")
+    # every rank ends with the same parameters
+    flat = torch.cat([p.detach().reshape(-1) for p in a.parameters()])
+    first = flat.clone()
+    dist.broadcast(first, 0)
+    if not torch.equal(first, flat):
+        res["fail"].append("ddp: ranks' parameters differ after 3 steps")
 
 
 def capture(comm, res, world, rank):
