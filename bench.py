@@ -566,6 +566,9 @@ def bench_distributed(a):
         os.environ["NCCL_HOSTID"] = f"ftar-loopback-{rank}"
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
+        if rank == 0 and world <= torch.cuda.device_count():
+            sys.stderr.write("[bench] --rccl-loopback with a GPU per rank: RCCL moves the data over sockets, "
+                             "not xGMI; drop the flag to measure the node\n")
     if not a.host_comm:
         try:
             comm = ftar.dist.init_comm(device=local)   # RCCL unique id over the gloo group
