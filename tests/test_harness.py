@@ -364,3 +364,20 @@ def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, ext
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(ranks):
         assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
+
+
+@needs
+@pytest.mark.gpu
+def test_harness_rccl_communicator_lifecycle_two_ranks(tmp_path):
+    """Communicator lifecycle over real RCCL communicators between MPI processes (loopback sockets): 6
+    duplicates and singleton splits of MPI_COMM_WORLD created and freed in turn (an RCCL communicator brought
+    up and destroyed with each), then 2 threads driving 2 communicators at once, exact sums throughout."""
+    env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    args = ["--size", "65536", "--repeat", "2", "--check", "--comm-cycle", "6", "--comm-threads", "2"]
+    p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-4000:]
+    assert p.stdout.count("(test passed)") == 2, out[-4000:]
+    for r in range(2):
+        assert re.search(rf"COMM_CYCLE {r}: cycles=6 handles_reused=\d+ ok", p.stdout), out[-4000:]
+        assert f"COMM_THREADS {r}: threads=2 ok" in p.stdout or "COMM_THREADS skipped" in p.stdout, out[-4000:]
