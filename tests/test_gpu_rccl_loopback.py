@@ -77,12 +77,13 @@ def test_rccl_p2p_random_soak(world):
         assert not r["fail"] and r["soak"] == 40, r
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_ddp_comm_hook_over_rccl(world):
+def test_ddp_comm_hook_over_rccl(world, dtype):
     """torch DistributedDataParallel with ftar as the gradient AllReduce (ftar.ddp.allreduce_hook, one rank
-    per process over RCCL) against DDP's own AllReduce on the same model and batches: bit-identical gradients
-    at P = 2, within 1e-5 relative at P = 4, every rank with the same parameters after 3 SGD steps."""
-    p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "ddp"})
+    per process over RCCL) against DDP's own AllReduce on the same model and batches, fp32 and bf16 models:
+    bit-identical gradients at P = 2, close at P = 4, every rank with the same parameters after 3 SGD steps."""
+    p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "ddp", "FTAR_LOOPBACK_DDP_DTYPE": dtype})
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
         assert not r["fail"] and r["ddp_hook_calls"] >= 3, r   # at least one bucket per step
