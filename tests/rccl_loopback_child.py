@@ -222,6 +222,9 @@ def ddp(comm, res, world, rank):
                 worst = max(worst, d.item())
         oa.step()
         ob.step()
+        with torch.no_grad():   # the next step compares gradients of the same parameters
+            for pa, pb in zip(a.parameters(), b.parameters()):
+                pb.copy_(pa)
     res["ddp_hook_calls"] = state.calls
     res["ddp_worst_rel"] = worst
     if world != 2 and worst > (1e-5 if dt == torch.float32 else 2e-2):
