@@ -392,3 +392,29 @@ def test_allreduce_special_values_vs_oracle(topo, form, dt):
             assert_bits_equal_nan_as_nan(bufs[r].cpu().numpy().view(view), ref[r].view(view), dt)
     finally:
         group.destroy()
+
+
+def test_reduce_reference_gpu_test_size_k1_to_16():
+    """The reference's own GPU test (vector_add.cu:139-150, :182-187): k = 1..16 sources of n = 150e6 fp32
+    uniform [0, 1) values (rand()/RAND_MAX there), GPU reduce against the CPU reduce_sum within 1e-5.  Here:
+    ftar_reduce against torch's fp32 adds folded left to right (reduce_sum's order, mpi_mod.hpp:856-863;
+    reduce_sum.h:36-222), every element bit for bit, at the reference's size; a 1-element offset copy of the
+    sources (the unaligned head/tail path) at k = 3 and 16."""
+    import torch
+
+    import ftar
+    n, kmax = 150_000_000, 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(150)
+    srcs = [torch.rand(n + 1, device="cuda", generator=g) for _ in range(kmax)]
+    dst = torch.empty(n + 1, device="cuda")
+    acc = torch.empty(n, device="cuda")
+    for k in range(1, kmax + 1):
+        for off in ((0, 1) if k in (3, 16) else (0,)):
+            acc.copy_(srcs[0][off:off + n])
+            for j in range(1, k):
+                acc.add_(srcs[j][off:off + n])
+            dst.fill_(float("nan"))
+            ftar.reduce([s[off:] for s in srcs[:k]], dst[off:], n, "f32", "sum")
+            torch.cuda.synchronize()
+            assert torch.equal(dst[off:off + n].view(torch.int32), acc.view(torch.int32)), (k, off)
