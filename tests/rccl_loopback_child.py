@@ -55,12 +55,12 @@ def main():
     comm = fdist.init_comm(device=0)
     res["rccl"] = True
 
-    def run(x, topo, lonely, dtype, op, outofplace, repeat=1, host=False):
+    def run(x, topo, lonely, dtype, op, outofplace, repeat=1, host=False, pinned=True):
         n = x.size
         if host:
-            send = torch.from_numpy(x.copy()).pin_memory() if outofplace else None
-            recv = torch.from_numpy(x.copy()).pin_memory() if not outofplace else torch.empty_like(
-                torch.from_numpy(x)).pin_memory()
+            pin = (lambda t: t.pin_memory()) if pinned else (lambda t: t)
+            send = pin(torch.from_numpy(x.copy())) if outofplace else None
+            recv = pin(torch.from_numpy(x.copy())) if not outofplace else pin(torch.empty_like(torch.from_numpy(x)))
             for _ in range(repeat):
                 comm.allreduce_host(send.data_ptr() if send is not None else None, recv.data_ptr(), n, dtype, op,
                                     topo_=topo, lonely=lonely)
@@ -151,7 +151,8 @@ def finish(comm, res):
 def soak(comm, res, world, rank, run, count):
     """Seeded random cases of this world size (tests/random_cases.py: ring, trees, lonely layouts, every dtype,
     SUM and BAND, ragged sizes down to 0 and 1 element, in place or out of place) over RCCL, each with a random
-    pipeline piece size, data-movement form and device or pinned-host buffers; every rank against the oracle.
+    pipeline piece size, data-movement form and device, pinned-host or pageable-host buffers; every rank
+    against the oracle.
     Every rank draws the same sequence, so the per-call settings agree across ranks."""
     import random
 
@@ -163,19 +164,21 @@ def soak(comm, res, world, rank, run, count):
         form = rng.choice(["direct", "stages", "collective"])
         chunk = rng.choice([0, 256, 4096, 1 << 16])
         host = rng.random() < 0.4
+        pinned = rng.random() < 0.7
         try:
             comm.allgather = form
             comm.reduce_scatter = "stages" if form == "stages" else "direct"
             comm.chunk_bytes = chunk
             comm.host_chunk_bytes = chunk
             out = run(c["ins"][rank], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]],
-                      0 if c["op"] == "sum" else 1, c["oop"], host=host)
+                      0 if c["op"] == "sum" else 1, c["oop"], host=host, pinned=pinned)
             if out.tobytes() != c["ref"][rank].tobytes():
                 raise AssertionError("differs from the oracle")
             res["soak"] += 1
         except Exception as e:  # noqa: BLE001
             res["fail"].append(f"soak P={world} topo={c['topo']}+{c['lonely']} n={c['n']} {c['dtype']} "
-                               f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host}: {str(e)[:200]}")
+                               f"{c['op']} oop={c['oop']} {form} chunk={chunk} host={host} pinned={pinned}: "
+                               f"{str(e)[:200]}")
             return
 
 

@@ -70,7 +70,7 @@ def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
 @pytest.mark.parametrize("world", [2, 3, 5, 6, 7, 8])
 def test_rccl_p2p_random_soak(world):
     """Seeded random cases of the world size over RCCL, each with its own piece size, data-movement form and
-    device or pinned-host buffers, bit-exact against the oracle (lonely layouts at P = 5, 6, 7 and 8)."""
+    device, pinned or pageable host buffers, bit-exact against the oracle (lonely layouts at P = 5, 6, 7 and 8)."""
     p, res = run_loopback(world, {"FTAR_LOOPBACK_MODE": "soak"})
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
