@@ -26,7 +26,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def run_loopback(world, env_extra=None, timeout=300):
+def run_loopback(world, env_extra=None, timeout=170):
     """(completed process, every rank's result dict, by rank); each rank writes its own result file"""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(HERE, "rccl_loopback_child.py")]

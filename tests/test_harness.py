@@ -298,7 +298,7 @@ def test_harness_rccl_transport_reproduces_reference_output(tmp_path, case_id, d
     env = dict(os.environ, FT_TOPO=case["topo"], FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo",
                NCCL_IB_DISABLE="1")
     p = subprocess.run(_loopback_mpmd(case["P"], args), cwd=tmp_path, env=env, capture_output=True, text=True,
-                       timeout=240)
+                       timeout=170)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(case["P"]):
         with open(os.path.join(tmp_path, f"out.{r}.bin"), "rb") as f:
@@ -317,7 +317,7 @@ def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
     import oracle_lib
     env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     p = subprocess.run(_loopback_mpmd(ranks, ["--size", str(n), "--repeat", "2", "--dump", "out"]), cwd=tmp_path,
-                       env=env, capture_output=True, text=True, timeout=300)
+                       env=env, capture_output=True, text=True, timeout=170)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     x = (np.arange(n, dtype=np.float64).astype(np.float32) * np.float32(0.1)).astype(np.float32)
     ref = oracle_lib.allreduce(oracle_lib.allreduce([x] * ranks, topo), topo)   # two calls in place
@@ -343,7 +343,7 @@ def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n
                FTAR_CAPTURE_SERIAL=serial)
     args = ["--size", str(n), "--repeat", "3", "--device", "--graph", "--exact"]
     p = subprocess.run(_loopback_mpmd(ranks, args), cwd=tmp_path, env=env, capture_output=True, text=True,
-                       timeout=240)
+                       timeout=170)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(ranks):
         assert re.search(rf"GRAPH {r}: captured \d+ nodes", p.stdout), p.stdout[-3000:]
@@ -360,7 +360,7 @@ def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, ext
     and on the ring (many pipeline pieces per block); every element of every rank bit-exact (--exact)."""
     env = dict(os.environ, FT_TOPO=topo, FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     p = subprocess.run(_loopback_mpmd(ranks, ["--size", str(n), "--repeat", "1", "--exact"] + extra), cwd=tmp_path,
-                       env=env, capture_output=True, text=True, timeout=600)
+                       env=env, capture_output=True, text=True, timeout=170)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     for r in range(ranks):
         assert f"EXACT {r}: {n} elements bit-exact" in p.stdout, p.stdout[-3000:]
@@ -371,13 +371,14 @@ def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, ext
 def test_harness_rccl_communicator_lifecycle_two_ranks(tmp_path):
     """Communicator lifecycle over real RCCL communicators between MPI processes (loopback sockets): 6
     duplicates and singleton splits of MPI_COMM_WORLD created and freed in turn (an RCCL communicator brought
-    up and destroyed with each), then 2 threads driving 2 communicators at once, exact sums throughout."""
+    up and destroyed with each), exact sums throughout.  (Not --comm-threads: collectives on two RCCL
+    communicators issued concurrently from two threads may be ordered differently on the two ranks, and RCCL
+    then deadlocks, as NCCL documents for concurrent communicators; that check runs on the ipc transport.)"""
     env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
-    args = ["--size", "65536", "--repeat", "2", "--check", "--comm-cycle", "6", "--comm-threads", "2"]
-    p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=240)
+    args = ["--size", "65536", "--repeat", "2", "--check", "--comm-cycle", "6"]
+    p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
     out = p.stdout + p.stderr
     assert p.returncode == 0, out[-4000:]
     assert p.stdout.count("(test passed)") == 2, out[-4000:]
     for r in range(2):
         assert re.search(rf"COMM_CYCLE {r}: cycles=6 handles_reused=\d+ ok", p.stdout), out[-4000:]
-        assert f"COMM_THREADS {r}: threads=2 ok" in p.stdout or "COMM_THREADS skipped" in p.stdout, out[-4000:]
