@@ -42,7 +42,7 @@ def run_loopback(world, env_extra=None, timeout=170):
     return p, res
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 8, 12])
 def test_rccl_p2p_between_ranks_matches_reference(world):
     p, res = run_loopback(world)
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
