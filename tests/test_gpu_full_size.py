@@ -163,3 +163,34 @@ def test_host_allreduce_full_size_properties(P, n, dt, topo):
         hs.clear()
         orig.clear()
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("topo", ["1", "2"])
+def test_allreduce_at_mpi_max_count_fp32(topo):
+    """The largest bucket MPI_Allreduce_FT's `int count` can name (mpi_mod.hpp:1724): 2^31 - 1 fp32 elements
+    (8 GiB) per rank, 2 ranks, ring and tree(2), out of place: block 1 starts 4 GiB into the bucket, so byte
+    offsets pass 2^32.  With two ranks every element is one fp32 add, the same in either order, so the whole
+    output is checked bit for bit against torch's x0 + x1."""
+    import torch
+
+    import ftar
+    P, n = 2, (1 << 31) - 1
+    dev = torch.device("cuda", 0)
+    g = ftar.Comm.init_local(P)
+    xs, ys = [], []
+    try:
+        for r in range(P):
+            gen = torch.Generator(device=dev)
+            gen.manual_seed(31 + r)
+            xs.append(torch.rand(n, generator=gen, device=dev) * 2 - 1)
+            ys.append(torch.empty(n, device=dev))
+        g.allreduce(xs, ys, n, "f32", "sum", topo_=topo)
+        torch.cuda.synchronize()
+        exp = xs[0] + xs[1]
+        for r in range(P):
+            assert torch.equal(ys[r].view(torch.int32), exp.view(torch.int32)), r
+    finally:
+        g.destroy()
+        xs.clear()
+        ys.clear()
+        torch.cuda.empty_cache()
