@@ -13,7 +13,8 @@ Checks, per rank (written as one JSON line "LOOPBACK {...}"):
   * bf16 and RCCL's own ncclAllReduce on the same communicator.
 FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and replays it (capture());
 FTAR_LOOPBACK_MODE=soak runs seeded random cases with random per-call settings (soak());
-FTAR_LOOPBACK_MODE=ddp trains through DistributedDataParallel with ftar's comm hook (ddp()).
+FTAR_LOOPBACK_MODE=ddp trains through DistributedDataParallel with ftar's comm hook (ddp());
+FTAR_LOOPBACK_MODE=full runs BASELINE's C4 and C5 buckets (full_size()).
 """
 import json
 import os
@@ -82,6 +83,9 @@ def main():
         return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "ddp":
         ddp(comm, res, world, rank)
+        return finish(comm, res)
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "full":
+        full_size(comm, res, world, rank)
         return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "soak":
         soak(comm, res, world, rank, run, int(os.environ.get("FTAR_LOOPBACK_SOAK", "40")))
@@ -238,6 +242,52 @@ def ddp(comm, res, world, rank):
     dist.broadcast(first, 0)
     if not torch.equal(first, flat):
         res["fail"].append("ddp: ranks' parameters differ after 3 steps")
+
+
+def full_size(comm, res, world, rank):
+    """BASELINE's full buckets over RCCL at P = world (8 for C4/C5): C4 = 2^28 fp32 on the ring (direct and
+    the reference's staged rounds), C5 = 2^29 bf16 on the width-P tree; out of place, device-resident.  Each
+    rank's whole output must equal every other rank's (a checksum of its bits, all-gathered), and 65,536
+    sampled elements plus every block boundary must equal the reference's fold of the P inputs there
+    (tests/sample_fold.py, pinned to the oracle by tests/test_sample_fold.py)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import sample_fold
+    res["full"] = []
+    for n, dt, topo, form in (((1 << 28), "f32", "1", "direct"), ((1 << 28), "f32", "1", "stages"),
+                              ((1 << 29), "bf16", str(world), "direct")):
+        tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
+        comm.allgather = form
+        comm.reduce_scatter = "stages" if form == "stages" else "direct"
+        g = torch.Generator(device="cuda")
+        g.manual_seed(2024 + rank)
+        x = (torch.rand(n, generator=g, device="cuda") * 2 - 1).to(tdt)
+        y = torch.empty_like(x)
+        comm.allreduce(x, y, n, dt, "sum", topo_=topo, stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        split = -(-n // world)
+        rng = np.random.default_rng(7)
+        idx = np.unique(np.concatenate([rng.integers(0, n, 65536), np.arange(world) * split,
+                                        np.minimum(np.arange(1, world + 1) * split, n) - 1]))
+        it = torch.from_numpy(idx).cuda()
+        mine = x[it].float().cpu()
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        exp = sample_fold.fold(np.stack([a.numpy() for a in allv]), idx, n, "ring" if topo == "1" else "tree",
+                               bf16=dt == "bf16")
+        got = y[it].float().cpu().numpy()
+        bits = y.view(torch.int16 if dt == "bf16" else torch.int32).to(torch.int64)
+        h = torch.tensor([int((bits * (torch.arange(n, device="cuda") % 65521 + 1)).sum().item())])
+        hs = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        ok = np.array_equal(got.view(np.uint32), exp.view(np.uint32)) and len({int(v) for v in hs}) == 1
+        res["full"].append(f"{dt} n={n} topo={topo} {form}: {'ok' if ok else 'MISMATCH'}")
+        if not ok:
+            res["fail"].append(res["full"][-1])
+        del x, y, bits
+        torch.cuda.empty_cache()
 
 
 def capture(comm, res, world, rank):

@@ -87,3 +87,13 @@ def test_ddp_comm_hook_over_rccl(world, dtype):
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
         assert not r["fail"] and r["ddp_hook_calls"] >= 3, r   # at least one bucket per step
+
+
+def test_rccl_p2p_baseline_c4_c5_full_size():
+    """BASELINE configs[3] (8 ranks x 2^28 fp32, the ring, direct and staged) and configs[4] (8 ranks x 2^29
+    bf16, the width-8 tree) over RCCL between 8 processes: every rank's whole output identical across ranks,
+    and 65,536 sampled elements plus the block boundaries equal the reference's fold (sample_fold)."""
+    p, res = run_loopback(8, {"FTAR_LOOPBACK_MODE": "full"})
+    assert p.returncode == 0 and len(res) == 8, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
+    for r in res:
+        assert not r["fail"] and len(r["full"]) == 3, r
