@@ -17,16 +17,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "capture_runtime_limit: a graph-capture shape the HIP runtime crashes on "
                                        "(SIGSEGV in hipStreamEndCapture, DESIGN §4); runs only with "
                                        "FTAR_RUN_CAPTURE_LIMITS=1")
+    config.addinivalue_line("markers", "wide: further world sizes / dtypes of the multi-process RCCL rehearsals "
+                                       "(several minutes together); the default GPU suite keeps one or two per "
+                                       "kind; runs only with FTAR_RUN_WIDE=1 (logs: profiles/r03/loopback/)")
 
 
 def pytest_collection_modifyitems(config, items):
-    if os.environ.get("FTAR_RUN_CAPTURE_LIMITS") == "1":
-        return
-    skip = pytest.mark.skip(reason="HIP runtime capture limit: opt in with FTAR_RUN_CAPTURE_LIMITS=1 "
-                                   "(the child process crashes in hipStreamEndCapture)")
+    skips = []
+    if os.environ.get("FTAR_RUN_CAPTURE_LIMITS") != "1":
+        skips.append(("capture_runtime_limit", pytest.mark.skip(
+            reason="HIP runtime capture limit: opt in with FTAR_RUN_CAPTURE_LIMITS=1 (the child process crashes "
+                   "in hipStreamEndCapture)")))
+    if os.environ.get("FTAR_RUN_WIDE") != "1":
+        skips.append(("wide", pytest.mark.skip(reason="wide rehearsal: opt in with FTAR_RUN_WIDE=1")))
     for item in items:
-        if "capture_runtime_limit" in item.keywords:
-            item.add_marker(skip)
+        for kw, mark in skips:
+            if kw in item.keywords:
+                item.add_marker(mark)
 
 
 @pytest.fixture(scope="session")

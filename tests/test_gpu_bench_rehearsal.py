@@ -63,7 +63,7 @@ def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
     assert "default" in d["stage_wall_s"] and d.get("rccl_p2p_best") is None
 
 
-@pytest.mark.parametrize("ranks", [2, 4])
+@pytest.mark.parametrize("ranks", [2, pytest.param(4, marks=pytest.mark.wide)])
 def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
     """The same N > 1 run with RCCL itself carrying the default configuration and every RCCL form of the sweep
     (--rccl-loopback: one NCCL_HOSTID per rank, ncclSend/ncclRecv over loopback sockets, the ranks sharing the

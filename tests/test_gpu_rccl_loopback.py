@@ -42,7 +42,11 @@ def run_loopback(world, env_extra=None, timeout=170):
     return p, res
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8, 12])
+WIDE = pytest.mark.wide
+
+
+@pytest.mark.parametrize("world", [2, pytest.param(3, marks=WIDE), pytest.param(4, marks=WIDE), 8,
+                                   pytest.param(12, marks=WIDE)])
 def test_rccl_p2p_between_ranks_matches_reference(world):
     p, res = run_loopback(world)
     assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
@@ -52,7 +56,7 @@ def test_rccl_p2p_between_ranks_matches_reference(world):
     assert len({r["golden"] for r in res}) == 1
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, pytest.param(4, marks=WIDE)])
 def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
     """One rank per process over RCCL (the product's process model), P > 1, under torch.cuda.graph: the
     ring and the width-P tree in the direct form and the ring in the reference's staged rounds, each captured
@@ -67,7 +71,7 @@ def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
         assert not r["fail"] and r["captured"] == 3, r
 
 
-@pytest.mark.parametrize("world", [2, 3, 5, 6, 7, 8])
+@pytest.mark.parametrize("world", [pytest.param(w, marks=WIDE) if w != 5 else w for w in (2, 3, 5, 6, 7, 8)])
 def test_rccl_p2p_random_soak(world):
     """Seeded random cases of the world size over RCCL, each with its own piece size, data-movement form and
     device, pinned or pageable host buffers, bit-exact against the oracle (lonely layouts at P = 5, 6, 7 and 8)."""
@@ -77,8 +81,8 @@ def test_rccl_p2p_random_soak(world):
         assert not r["fail"] and r["soak"] == 40, r
 
 
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world,dtype", [(2, "bf16"), pytest.param(2, "f32", marks=WIDE),
+                                         pytest.param(4, "f32", marks=WIDE), pytest.param(4, "bf16", marks=WIDE)])
 def test_ddp_comm_hook_over_rccl(world, dtype):
     """torch DistributedDataParallel with ftar as the gradient AllReduce (ftar.ddp.allreduce_hook, one rank
     per process over RCCL) against DDP's own AllReduce on the same model and batches, fp32 and bf16 models:

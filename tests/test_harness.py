@@ -328,9 +328,12 @@ def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("ranks,topo,n,serial", [(2, "1", (1 << 20) + 3, "0"), (2, "2", 65537, "0"),
-                                                 (4, "1", 100_003, "0"), (4, "4", 100_003, "0"),
-                                                 (4, "2,2", 4099, "0"), (2, "1", (1 << 20) + 3, "1"),
+@pytest.mark.parametrize("ranks,topo,n,serial", [(2, "1", (1 << 20) + 3, "0"),
+                                                 pytest.param(2, "2", 65537, "0", marks=pytest.mark.wide),
+                                                 pytest.param(4, "1", 100_003, "0", marks=pytest.mark.wide),
+                                                 (4, "4", 100_003, "0"),
+                                                 pytest.param(4, "2,2", 4099, "0", marks=pytest.mark.wide),
+                                                 pytest.param(2, "1", (1 << 20) + 3, "1", marks=pytest.mark.wide),
                                                  (4, "2,2", 4099, "1")])
 def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n, serial):
     """The product's process model under stream capture at P > 1: one MPI process per rank over an RCCL
@@ -353,7 +356,7 @@ def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n
 @needs
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks,topo,n,extra", [(2, "1", 1 << 26, ["--device"]), (8, "8", 1 << 28, []),
-                                                (8, "1", 1 << 28, [])])
+                                                pytest.param(8, "1", 1 << 28, [], marks=pytest.mark.wide)])
 def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, extra):
     """BASELINE sizes through the RCCL transport between MPI processes (loopback sockets): C3's 256 MiB
     device-resident with 2 ranks, and C4's whole 1 GiB host bucket per rank with 8 ranks on the width-8 tree
