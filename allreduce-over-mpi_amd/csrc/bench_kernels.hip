@@ -1,6 +1,9 @@
-// A/B harness of the reduce kernels (tools/kbench_cold.py; not part of ftar.h): shape, cache-policy and
-// dtype variants of the production kernels in reduce_impl.h, built in their own translation unit so the
-// library compiles in parallel.
+// libftar_bench.so: the A/B harness of the reduce kernels and kernel-level test hooks, kept OUT of the
+// product library (libftar.so holds only the kernels launch_reduce / launch_tree / launch_copy /
+// launch_gather dispatch).  Not part of ftar.h; loaded by tools/kbench*.py and the bf16 conversion test
+// through ftar.bench_lib().  Shape, cache-policy and dtype variants of the production kernels in
+// reduce_impl.h are instantiated here from the same templates; launch_gather (variant 90) and
+// launch_reduce (the nested-fold A/B) are the product's own, linked from libftar.so.
 #include "reduce_impl.h"
 
 namespace ftar {
@@ -141,3 +144,57 @@ extern "C" ftar_status_t ftar_debug_reduce_variant(int variant, int dtype, const
   return e == hipSuccess ? FTAR_SUCCESS : FTAR_ERR_HIP;
 }
 
+// A/B of the nested fold: lds = 1 the LDS-staged kernel (production), 0 the
+// register kernel of round 1 (tools/kbench_cold.py --shapes).
+extern "C" ftar_status_t ftar_debug_reduce_nested_lds(int lds, const void* const* srcs, int k, void* dst, size_t count,
+                                                      int dtype, const int* shape, int nlevels, void* stream) {
+  return ftar::launch_reduce(srcs, k, dst, count, (ftar_dtype_t)dtype, FTAR_SUM, static_cast<hipStream_t>(stream),
+                             false, shape, nlevels, lds != 0);
+}
+
+namespace ftar {
+namespace {
+// every float bit pattern u (lo half) and u ^ 0x80000001 (hi half) through both bf16 conversions
+__global__ void __launch_bounds__(256) bf16_cvt_check_kernel(unsigned long long* bad, unsigned* first) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * 256;
+  unsigned long long mine = 0;
+  unsigned first_mine = 0xffffffffu;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < (1ull << 32); i += stride) {
+    const unsigned u = (unsigned)i, v = u ^ 0x80000001u;
+    const float lo = __uint_as_float(u), hi = __uint_as_float(v);
+    if (pack_bf16<true>(lo, hi) != pack_bf16<false>(lo, hi)) {
+      ++mine;
+      first_mine = first_mine < u ? first_mine : u;
+    }
+  }
+  if (mine) {
+    atomicAdd(bad, mine);
+    atomicMin(first, first_mine);
+  }
+}
+}  // namespace
+}  // namespace ftar
+
+// Test hook (not in ftar.h): how many of the 2^32 float bit patterns convert to different bf16 bits
+// through v_cvt_pk_bf16_f32 than through the bit-exact RNE (bf16_round_bits); the first such pattern.
+extern "C" ftar_status_t ftar_debug_bf16_cvt_check(unsigned long long* mismatches, unsigned* first) {
+  if (!mismatches || !first) return FTAR_ERR_INVALID_ARG;
+  unsigned long long* d_bad = nullptr;
+  unsigned* d_first = nullptr;
+  ftar_status_t st = FTAR_SUCCESS;  // both buffers are freed on every path below
+  if (hipMalloc(&d_bad, sizeof *d_bad) != hipSuccess || hipMalloc(&d_first, sizeof *d_first) != hipSuccess)
+    st = FTAR_ERR_NO_MEMORY;
+  if (st == FTAR_SUCCESS &&
+      (hipMemset(d_bad, 0, sizeof *d_bad) != hipSuccess || hipMemset(d_first, 0xff, sizeof *d_first) != hipSuccess))
+    st = FTAR_ERR_HIP;
+  if (st == FTAR_SUCCESS) {
+    hipLaunchKernelGGL(ftar::bf16_cvt_check_kernel, dim3(8192), dim3(256), 0, nullptr, d_bad, d_first);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(mismatches, d_bad, sizeof *d_bad, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(first, d_first, sizeof *d_first, hipMemcpyDeviceToHost) != hipSuccess)
+      st = FTAR_ERR_HIP;
+  }
+  ftar::hip_ignore(hipFree(d_bad));
+  ftar::hip_ignore(hipFree(d_first));
+  return st;
+}

@@ -1,6 +1,7 @@
 // C ABI: version/errors, the one-device reduce, topology parsing, the
-// re-fitted cost model and schedule introspection.  Communicator and
-// AllReduce entry points live in engine.cpp.
+// reference's cost model restated, and schedule introspection.  The xGMI
+// execution model lives in cost_model.cpp; communicator and AllReduce entry
+// points in engine.cpp.
 #include <rccl/rccl.h>
 
 #include <unistd.h>
@@ -43,45 +44,6 @@ void trace(const char* fmt, ...) {
 }
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// cost model.  The reference (cost_model/CostModel.h:1-80) scores a width list
-// with per-layer latency `lo`, memory steps `o` and (P-1)/P*s*bo for a
-// 16-host MPI cluster; it never sees that one tree stage of width w talks to
-// w-1 peers AT ONCE.  On an MI355X node every peer is its own xGMI link, so
-// here a stage of width w on data D moves D/w to each of w-1 peers in
-// parallel, then reduces w+1 streams through HBM:
-//   stage(w, D) = 2*alpha + 2*(D/w)/link + (w+1)*(D/w)/hbm,   D /= w per stage
-// That is the staged (reference) form.  The default direct forms run the ring
-// and every non-lonely tree of at most 4 stages as one gather-and-fold round
-// plus one all-gather round, i.e. exactly what tree(P) moves and folds, so
-// they cost stage(P, S); the ring's reference form would be
-// 2(P-1)*alpha + 2(P-1)*(S/P)/link.  ftar_topo_choose keeps the fewest stages
-// on a tie (the flat fold; bf16 rounds once).
-// alpha = one p2p group (launch + handshake), link = one peer's unidirectional
-// xGMI bandwidth, hbm = achieved reduce bandwidth.  Defaults are MI355X
-// figures (DESIGN.md §Cost model); FTAR_COST_{ALPHA_US,LINK_GBPS,HBM_GBPS}
-// override them.
-// ---------------------------------------------------------------------------
-// Process-wide constants set by ftar_cost_set_params (e.g. fitted from
-// ftar_xgmi_probe by bench.py); 0 = unset.  The environment overrides both.
-std::mutex g_cost_mu;
-double g_alpha = 0, g_link = 0, g_hbm = 0;
-
-struct CostConsts {
-  double alpha = 20e-6, link = 48e9, hbm = 6.3e12;  // hbm: measured k=2..8 reduce (profiles/r01/kbench3)
-  CostConsts() {
-    {
-      std::lock_guard<std::mutex> g(g_cost_mu);
-      if (g_alpha > 0) alpha = g_alpha;
-      if (g_link > 0) link = g_link;
-      if (g_hbm > 0) hbm = g_hbm;
-    }
-    if (const char* e = getenv("FTAR_COST_ALPHA_US")) alpha = atof(e) * 1e-6;
-    if (const char* e = getenv("FTAR_COST_LINK_GBPS")) link = atof(e) * 1e9;
-    if (const char* e = getenv("FTAR_COST_HBM_GBPS")) hbm = atof(e) * 1e9;
-  }
-};
 
 // ---------------------------------------------------------------------------
 // The reference's cost model, restated (cost_model/CostModel.h:1-120), for
@@ -132,44 +94,6 @@ double ref_cost(const std::vector<int>& tree, int total, double chunk) {
 
 // getWidth(P) (GetWidth.h:10-47): ordered factorizations, smallest first
 // factor first, the single factor [P] listed as [1,P], [P,1]
-std::vector<std::vector<int>> ref_getwidth(int P);
-
-double model_cost(const Topology& t, int P, size_t bytes) {
-  CostConsts k;
-  const double S = (double)bytes;
-  if (P <= 1) return 0.0;
-  const bool one_round = P <= FTAR_MAX_K && (t.ring || (t.lonely == 0 && t.widths.size() >= 2 &&
-                                                         t.widths.size() <= (size_t)kMaxFoldLevels));
-  if (one_round) {  // direct forms (the default): = tree(P), see schedule.cpp
-    Topology one;
-    one.widths = {(size_t)P};
-    return model_cost(one, P, bytes);
-  }
-  if (t.ring) return 2.0 * (P - 1) * (k.alpha + (S / P) / k.link) + (P - 1) * 3.0 * (S / P) / k.hbm;
-  double D = S, cost = 0.0;
-  for (size_t w : t.widths) {
-    const double piece = D / (double)w;
-    cost += 2.0 * k.alpha + 2.0 * piece / k.link + (double)(w + 1) * piece / k.hbm;
-    D = piece;
-  }
-  if (t.lonely) cost += 4.0 * k.alpha + 2.0 * (S / P) / k.link;  // lonely exchange stages
-  return cost;
-}
-
-// every ordered factorization of n into factors >= 2 (cost_model/GetWidth.h:10-47)
-void factorizations(size_t n, std::vector<size_t>& cur, std::vector<std::vector<size_t>>& out) {
-  if (n == 1) {
-    if (!cur.empty()) out.push_back(cur);
-    return;
-  }
-  for (size_t f = 2; f <= n; ++f)
-    if (n % f == 0) {
-      cur.push_back(f);
-      factorizations(n / f, cur, out);
-      cur.pop_back();
-    }
-}
-
 std::vector<std::vector<int>> ref_getwidth(int P) {
   std::vector<size_t> cur;
   std::vector<std::vector<size_t>> f;
@@ -247,22 +171,6 @@ int ftar_cost_reference_candidates(int nranks, int* widths, int max_widths, int*
     }
   }
   return (int)cands.size();
-}
-
-ftar_status_t ftar_cost_set_params(double alpha_us, double link_gbps, double hbm_gbps) {
-  std::lock_guard<std::mutex> g(ftar::g_cost_mu);
-  ftar::g_alpha = alpha_us > 0 ? alpha_us * 1e-6 : 0;
-  ftar::g_link = link_gbps > 0 ? link_gbps * 1e9 : 0;
-  ftar::g_hbm = hbm_gbps > 0 ? hbm_gbps * 1e9 : 0;
-  return FTAR_SUCCESS;
-}
-
-ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* hbm_gbps) {
-  ftar::CostConsts k;
-  if (alpha_us) *alpha_us = k.alpha * 1e6;
-  if (link_gbps) *link_gbps = k.link / 1e9;
-  if (hbm_gbps) *hbm_gbps = k.hbm / 1e9;
-  return FTAR_SUCCESS;
 }
 
 const char* ftar_version(void) {
@@ -356,49 +264,6 @@ ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nr
   return FTAR_SUCCESS;
 }
 
-ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out) {
-  if (!out || nranks <= 0) return FTAR_ERR_INVALID_ARG;
-  if (const char* m = getenv("FTAR_COST_MODEL")) {
-    if (!strcmp(m, "reference")) {  // the reference's own scores (CostModel.h), chunk = FTAR_COST_REF_CHUNK
-      const char* ch = getenv("FTAR_COST_REF_CHUNK");
-      return ftar_topo_choose_reference(nranks, ch ? atof(ch) : 100.0, out, nullptr);
-    }
-    if (*m && strcmp(m, "xgmi")) {
-      ftar::set_error(std::string("FTAR_COST_MODEL=") + m + ": expected xgmi or reference", __FILE__, __LINE__);
-      return FTAR_ERR_INVALID_ARG;
-    }
-  }
-  ftar::Topology ring;
-  ring.ring = true;
-  ring.widths = {1};
-  ftar::Topology best = ring;
-  if (nranks > 1) {
-    // trees first, the ring last; on a tie keep the tree with the fewest stages
-    // (the direct forms make the ring and multi-stage trees cost what tree(P)
-    // costs; its flat fold rounds bf16 once instead of once per hop / node)
-    double best_cost = 1e300;
-    std::vector<size_t> cur;
-    std::vector<std::vector<size_t>> cands;
-    ftar::factorizations((size_t)nranks, cur, cands);
-    for (auto& c : cands) {
-      if (c.size() > FTAR_MAX_STAGES) continue;
-      bool fits = true;  // one stage folds w sources: at most FTAR_MAX_K (engine.cpp)
-      for (size_t w : c) fits = fits && w <= FTAR_MAX_K;
-      if (!fits) continue;
-      ftar::Topology t;
-      t.widths = c;
-      double cost = ftar::model_cost(t, nranks, bytes);
-      if (cost < best_cost || (cost == best_cost && c.size() < best.widths.size())) {
-        best_cost = cost;
-        best = t;
-      }
-    }
-    if (ftar::model_cost(ring, nranks, bytes) < best_cost) best = ring;
-  }
-  ftar::from_topology(best, out);
-  return FTAR_SUCCESS;
-}
-
 int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out) {
   // the reference's getWidth(P) order (cost_model/GetWidth.h:10-47): ordered
   // factorizations, smallest first factor first; its {1,P}/{P,1} pair is the ring.
@@ -431,12 +296,6 @@ ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out) {
   const char* el = getenv("FT_LONELY");
   if ((!et || !*et) && (!el || !*el || !strcmp(el, "0"))) return ftar_topo_choose(nranks, bytes, out);
   return ftar_topo_parse(et, el, nranks, out);
-}
-
-double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes) {
-  ftar::Topology t;
-  if (ftar::to_topology(topo, nranks, &t) != FTAR_SUCCESS) return -1.0;
-  return ftar::model_cost(t, nranks, bytes);
 }
 
 int ftar_topo_format(const ftar_topo_t* topo, char* buf, size_t buflen) {

@@ -40,8 +40,14 @@ struct ftar_comm {
   size_t scratch_bytes = 0;
   void* staging = nullptr;  // host mode: the device copy of the bucket, grow-only
   size_t staging_bytes = 0;
-  size_t chunk_bytes = 0;
+  size_t chunk_bytes = 0;  // the fixed pipeline piece; 0 = the execution model's per call (chunk_auto)
   size_t host_chunk_bytes = 0;
+  // FTAR_FORM_AUTO: the execution model picks the form per call (cost_model.cpp); otherwise the form the
+  // explicit settings below (allgather, reduce_scatter, peer_direct) describe, or -2 for a mix
+  int form = FTAR_FORM_AUTO;
+  // choices of the model, cached per (bytes, flags, fixed topology/form/piece, constants' generation)
+  std::map<std::string, ftar::ExecChoice> exec_cache;
+  ftar_exec_t last_exec{};
   int peer_direct = 0;             // FTAR_PEER_DIRECT / ftar_comm_set_peer_direct: 0 off, 1 read, 2 write
   // peer-form tuning (ftar_debug_set_peer_tuning; bench.py sweeps both on a
   // real node): nontemporal copies, LDS-staged fold (false: register kernel)
@@ -111,7 +117,6 @@ struct ftar_comm {
 namespace ftar {
 
 namespace {
-constexpr size_t kDefaultChunkBytes = 16u << 20;
 // Host mode pieces (0 = auto): 16 MiB per block, at least split/64 (bounds the
 // number of copies for huge buckets).  4 MiB device->host copies run at only
 // ~33 GB/s; larger pieces lengthen the pipeline's fill and drain (one piece of
@@ -167,6 +172,39 @@ ftar_status_t set_reduce_cus(ftar_comm* c, int cus) {
   return FTAR_SUCCESS;
 }
 
+// The form the explicit settings describe (ftar_form_t), or -2 for a mix no form names.
+int form_of(const ftar_comm* c) {
+  if (c->peer_direct == FTAR_PEER_READ) return FTAR_FORM_PEER_READ;
+  if (c->peer_direct == FTAR_PEER_WRITE) return FTAR_FORM_PEER_WRITE;
+  if (c->reduce_scatter == FTAR_RS_STAGES) return c->allgather == FTAR_AG_STAGES ? FTAR_FORM_STAGES : -2;
+  if (c->allgather == FTAR_AG_DIRECT) return FTAR_FORM_DIRECT;
+  return c->allgather == FTAR_AG_COLLECTIVE ? FTAR_FORM_COLLECTIVE : -2;
+}
+
+// "auto" | "direct" | "stages" | "collective" | "peer-read" | "peer-write"; -3 = none of them
+int form_from_name(const std::string& m) {
+  if (m == "auto" || m.empty()) return FTAR_FORM_AUTO;
+  if (m == "direct") return FTAR_FORM_DIRECT;
+  if (m == "stages") return FTAR_FORM_STAGES;
+  if (m == "collective") return FTAR_FORM_COLLECTIVE;
+  if (m == "peer-read" || m == "read") return FTAR_FORM_PEER_READ;
+  if (m == "peer-write" || m == "write") return FTAR_FORM_PEER_WRITE;
+  return -3;
+}
+
+// The settings of one form (the engine's three knobs): all-gather, reduce-scatter, peer mode.
+void form_settings(int form, int* ag, int* rs, int* peer) {
+  *ag = form == FTAR_FORM_STAGES ? FTAR_AG_STAGES : form == FTAR_FORM_COLLECTIVE ? FTAR_AG_COLLECTIVE : FTAR_AG_DIRECT;
+  *rs = form == FTAR_FORM_STAGES ? FTAR_RS_STAGES : FTAR_RS_DIRECT;
+  *peer = form == FTAR_FORM_PEER_READ ? FTAR_PEER_READ : form == FTAR_FORM_PEER_WRITE ? FTAR_PEER_WRITE : FTAR_PEER_OFF;
+}
+
+void set_form(ftar_comm* c, int form) {
+  c->form = form;
+  if (form >= FTAR_FORM_DIRECT) form_settings(form, &c->allgather, &c->reduce_scatter, &c->peer_direct);
+  else if (form == FTAR_FORM_AUTO) c->peer_direct = FTAR_PEER_OFF;
+}
+
 ftar_status_t grow_events(ftar_comm* c, size_t n) {
   if (c->capturing) {  // a fresh set for this captured call; the uncaptured set stays as it is
     for (hipEvent_t e : c->events) c->captured_events.push_back(e);
@@ -207,9 +245,21 @@ ftar_status_t comm_setup(ftar_comm* c) {
     const std::string m(ag);
     c->allgather = m == "stages" ? FTAR_AG_STAGES : m == "collective" ? FTAR_AG_COLLECTIVE : FTAR_AG_DIRECT;
   }
+  // any explicit data-movement setting fixes the form; FTAR_FORM names one (or "auto") outright
+  if (getenv("FTAR_PEER_DIRECT") || getenv("FTAR_REDUCE_SCATTER") || getenv("FTAR_ALLGATHER")) c->form = form_of(c);
+  if (const char* fm = getenv("FTAR_FORM")) {
+    const int f = form_from_name(fm);
+    if (f == -3) {
+      set_error(std::string("FTAR_FORM=") + fm + ": expected auto, direct, stages, collective, peer-read or peer-write",
+                __FILE__, __LINE__);
+      return FTAR_ERR_INVALID_ARG;
+    }
+    set_form(c, f);
+  }
+  if (!c->tp->async_p2p()) c->form = form_of(c);  // a host-bootstrapped communicator keeps its peer form
   const char* cb = getenv("FTAR_CHUNK_BYTES");
-  c->chunk_bytes = cb ? strtoull(cb, nullptr, 0) : kDefaultChunkBytes;
-  if (c->chunk_bytes < 256) c->chunk_bytes = kDefaultChunkBytes;
+  const size_t cbv = cb ? strtoull(cb, nullptr, 0) : 0;
+  c->chunk_bytes = cbv ? std::max<size_t>(256, cbv & ~size_t(255)) : 0;
   // a host-bootstrapped communicator compares its settings now (its host collective cannot hang on a
   // rank whose bring-up failed: that rank reports through it too); an RCCL one at its first call, so a
   // rank whose RCCL bring-up failed leaves no peer waiting in a collective inside ftar_comm_init_rank
@@ -233,20 +283,20 @@ ftar_status_t agree_settings(ftar_comm* c) {
     for (const char* p = v ? v : ""; *p; ++p) x = (x ^ (unsigned char)*p) * 1099511628211ull;
     return x;
   };
-  double alpha = 0, link = 0, hbm = 0;
-  ftar_cost_get_params(&alpha, &link, &hbm);
-  uint64_t cfg[12] = {(uint64_t)c->chunk_bytes, (uint64_t)c->host_chunk_bytes, (uint64_t)c->peer_direct,
-                      (uint64_t)c->host_peer_pipeline, (uint64_t)c->reduce_scatter, (uint64_t)c->allgather,
-                      h(getenv("FT_TOPO")), h(getenv("FT_LONELY")), h(getenv("FTAR_COST_MODEL")), 0, 0, 0};
-  memcpy(&cfg[9], &alpha, 8);
-  memcpy(&cfg[10], &link, 8);
-  memcpy(&cfg[11], &hbm, 8);
+  ftar_cost_params_t k;
+  ftar_cost_get(&k);
+  uint64_t cfg[10 + sizeof k / 8] = {(uint64_t)c->chunk_bytes, (uint64_t)c->host_chunk_bytes,
+                                     (uint64_t)c->peer_direct, (uint64_t)c->host_peer_pipeline,
+                                     (uint64_t)c->reduce_scatter, (uint64_t)c->allgather, (uint64_t)(int64_t)c->form,
+                                     h(getenv("FT_TOPO")), h(getenv("FT_LONELY")), h(getenv("FTAR_COST_MODEL"))};
+  static_assert(sizeof k % 8 == 0, "cost params are doubles");
+  memcpy(&cfg[10], &k, sizeof k);
   bool same = true;
   FTAR_RETURN_IF(c->tp->agree(cfg, sizeof cfg, &same));
   if (!same) {
     set_error("ranks disagree on FTAR_CHUNK_BYTES / FTAR_HOST_CHUNK_BYTES / FTAR_PEER_DIRECT / "
-              "FTAR_HOST_PEER_PIPELINE / FTAR_REDUCE_SCATTER / FTAR_ALLGATHER / FT_TOPO / FT_LONELY / the cost "
-              "model: launch every rank with the same environment",
+              "FTAR_HOST_PEER_PIPELINE / FTAR_REDUCE_SCATTER / FTAR_ALLGATHER / FTAR_FORM / FT_TOPO / FT_LONELY / "
+              "the cost model or its constants: launch every rank with the same environment",
               __FILE__, __LINE__);
     return FTAR_ERR_INVALID_ARG;
   }
@@ -499,9 +549,9 @@ ftar_status_t peer_copy(ftar_comm* c, const std::vector<Segment>& segs) {
 }  // namespace
 
 ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
-                             const Plan& plan, ftar_comm* c, hipStream_t stream) {
+                             const Plan& plan, ftar_comm* c, hipStream_t stream, int mode) {
   const size_t esz = dtype_size(dt), bytes = count * esz;
-  const bool write = c->peer_direct == FTAR_PEER_WRITE;
+  const bool write = mode == FTAR_PEER_WRITE;
   const size_t slot_bytes = plan.split * esz, final_at = (size_t)plan.nranks * slot_bytes;
   char* out = static_cast<char*>(recvbuf);
   const char* in = static_cast<const char*>(sendbuf ? sendbuf : recvbuf);
@@ -808,22 +858,66 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
 
 namespace {
 
-// The call's topology (argument, FT_TOPO/FT_LONELY read at this call, or the
-// cost model) and its cached plan; check_world once per (topology, count, form).
-ftar_status_t resolve_plan(ftar_comm* c, const ftar_topo_t* topo, size_t count, size_t esz, const Form& form,
-                           const Plan** out) {
-  Topology t;
-  bool is_auto = false;
-  if (topo) {
-    FTAR_RETURN_IF(to_topology(topo, c->nranks, &t));
-  } else {
-    FTAR_RETURN_IF(env_topology(c, &is_auto, &t));
-  }
-  if (is_auto) {
+// The call's topology: the argument, or FT_TOPO/FT_LONELY read at this call; both unset: *is_auto (the
+// execution model chooses), or under FTAR_COST_MODEL=reference the reference's own model's width list.
+ftar_status_t call_topology(ftar_comm* c, const ftar_topo_t* topo, size_t bytes, Topology* t, bool* is_auto) {
+  *is_auto = false;
+  if (topo) return to_topology(topo, c->nranks, t);
+  FTAR_RETURN_IF(env_topology(c, is_auto, t));
+  const char* m = getenv("FTAR_COST_MODEL");
+  if (*is_auto && m && !strcmp(m, "reference")) {
     ftar_topo_t ch;
-    FTAR_RETURN_IF(ftar_topo_choose(c->nranks, count * esz, &ch));
-    FTAR_RETURN_IF(to_topology(&ch, c->nranks, &t));
+    FTAR_RETURN_IF(ftar_topo_choose(c->nranks, bytes, &ch));
+    FTAR_RETURN_IF(to_topology(&ch, c->nranks, t));
+    *is_auto = false;
   }
+  return FTAR_SUCCESS;
+}
+
+// What the call runs: the topology, form and piece the caller fixed, the rest from the execution model
+// (cost_model.cpp), cached per communicator.  The same inputs on every rank give the same choice: the
+// model's constants are compared across ranks at the first call (agree_settings).  Peer forms are
+// candidates only for device buffers outside stream capture, and only once their rates are set.
+ftar_status_t decide_exec(ftar_comm* c, Topology* t, bool topo_auto, size_t bytes, bool host, ExecChoice* out) {
+  int flags = 0;
+  if (topo_auto) flags |= FTAR_CHOOSE_TOPO;
+  if (c->form == FTAR_FORM_AUTO && c->tp->async_p2p()) {
+    flags |= FTAR_CHOOSE_FORM;
+    if (!host && !c->capturing && c->nranks > 1) flags |= FTAR_CHOOSE_PEER;
+  }
+  if (!c->chunk_bytes && !host) flags |= FTAR_CHOOSE_CHUNK;
+  // a fixed mix of settings no form names is priced as the form of its reduce-scatter
+  const int fixed_form = c->form >= FTAR_FORM_DIRECT ? c->form
+                         : c->reduce_scatter == FTAR_RS_STAGES ? FTAR_FORM_STAGES : FTAR_FORM_DIRECT;
+  const size_t fixed_chunk = host ? 0 : c->chunk_bytes;
+  const std::string key = std::to_string(bytes) + "/" + std::to_string(flags) + "/" + t->key() + "/" +
+                          std::to_string(fixed_form) + "/" + std::to_string(fixed_chunk) + "/" +
+                          std::to_string(cost_generation());
+  auto it = c->exec_cache.find(key);
+  if (it == c->exec_cache.end()) {
+    ExecChoice ch;
+    ftar_status_t st = choose_exec(c->nranks, bytes, flags, *t, fixed_form, fixed_chunk, &ch);
+    if (st != FTAR_SUCCESS) {  // nothing the model can price (e.g. P > FTAR_MAX_K one-round): as configured
+      ch.topo = *t;
+      ch.form = fixed_form;
+      ch.chunk = fixed_chunk;
+      ch.seconds = -1;
+      if (flags & FTAR_CHOOSE_TOPO) {  // the ring runs at any size
+        ch.topo = Topology();
+        ch.topo.ring = true;
+        ch.topo.widths = {1};
+      }
+    }
+    if (c->exec_cache.size() > 256) c->exec_cache.clear();
+    it = c->exec_cache.emplace(key, ch).first;
+  }
+  *out = it->second;
+  *t = out->topo;
+  return FTAR_SUCCESS;
+}
+
+// The call's cached plan; check_world once per (topology, count, form).
+ftar_status_t resolve_plan(ftar_comm* c, const Topology& t, size_t count, const Form& form, const Plan** out) {
   const std::string key = t.key() + "/" + std::to_string(count) + "/ag" + std::to_string(form.allgather) + "/rs" +
                           std::to_string(form.reduce_scatter);
   auto it = c->plans.find(key);
@@ -1005,20 +1099,32 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   }
   if (count == 0) return FTAR_SUCCESS;
 
+  Topology topology;
+  bool topo_auto = false;
+  FTAR_RETURN_IF(call_topology(c, topo, count * esz, &topology, &topo_auto));
+  ExecChoice ex;
+  FTAR_RETURN_IF(decide_exec(c, &topology, topo_auto, count * esz, host != nullptr, &ex));
   Form form;
   form.allgather = c->allgather;
   form.reduce_scatter = c->reduce_scatter;
+  int peer_mode = c->peer_direct;
+  if (c->form == FTAR_FORM_AUTO && c->tp->async_p2p())
+    form_settings(ex.form, &form.allgather, &form.reduce_scatter, &peer_mode);
   if (host && form.allgather == FTAR_AG_COLLECTIVE) form.allgather = FTAR_AG_DIRECT;  // D2H needs pieces
   const Plan* planp = nullptr;
-  FTAR_RETURN_IF(resolve_plan(c, topo, count, esz, form, &planp));
+  FTAR_RETURN_IF(resolve_plan(c, topology, count, form, &planp));
   const Plan& plan = *planp;
+  from_topology(topology, &c->last_exec.topo);
+  c->last_exec.form = ex.form;
+  c->last_exec.chunk_bytes = ex.chunk;
+  c->last_exec.seconds = ex.seconds;
   const size_t nst = plan.stages.size();
   if (!c->tp->async_p2p()) {
     // A host-bootstrapped communicator's paths differ in their host barriers (peer read: 3, write: 2,
     // host buffers pipelined: m + 2, whole bucket: 3), so every rank must take the same one with the same
     // pieces: the settings that choose it are compared first, and a mismatch fails the call on every rank
     //  instead of pairing barriers of different phases.
-    const uint64_t cfg[6] = {(uint64_t)c->peer_direct, (uint64_t)c->allgather, (uint64_t)c->reduce_scatter,
+    const uint64_t cfg[6] = {(uint64_t)peer_mode, (uint64_t)c->allgather, (uint64_t)c->reduce_scatter,
                              (uint64_t)(host != nullptr), host ? (uint64_t)c->host_peer_pipeline : 0,
                              host ? (uint64_t)host_peer_piece(c, plan.split, esz) : 0};
     bool same = true;
@@ -1030,11 +1136,11 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
       return FTAR_ERR_INVALID_ARG;
     }
   }
-  if (!host && c->peer_direct && peer_eligible(plan)) {
+  if (!host && peer_mode && peer_eligible(plan)) {
     FTAR_RETURN_IF(grow_events(c, 5));
-    return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream);
+    return peer_allreduce(sendbuf, recvbuf, count, dt, op, plan, c, stream, peer_mode);
   }
-  if (host && c->peer_direct == FTAR_PEER_READ && !c->tp->async_p2p() && peer_eligible(plan) &&
+  if (host && peer_mode == FTAR_PEER_READ && !c->tp->async_p2p() && peer_eligible(plan) &&
       c->host_peer_pipeline && host_peer_piece(c, plan.split, esz) < plan.split) {
     // host buffers on a transport without p2p (a communicator bootstrapped over MPI with no RCCL,
     // ftar_comm_init_host): the read form piece by piece, H2D / exchange / D2H overlapped.  A bucket
@@ -1043,7 +1149,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     FTAR_RETURN_IF(grow_events(c, 5));
     return peer_allreduce_host(*host, count, dt, op, plan, c, stream);
   }
-  if (host && c->peer_direct && !c->tp->async_p2p() && peer_eligible(plan)) {
+  if (host && peer_mode && !c->tp->async_p2p() && peer_eligible(plan)) {
     // the write form (or FTAR_HOST_PEER_PIPELINE=0): the whole bucket in, the peer exchange in HBM,
     // the whole bucket out -- same plan, same bits, not pipelined (transports with stream-ordered
     // p2p keep using the pipelined p2p path below for host buffers even in peer-direct mode)
@@ -1052,7 +1158,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, bytes, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     FTAR_CHECK_HIP(hipMemcpyAsync(c->staging, host->src, bytes, hipMemcpyHostToDevice, stream));
     FTAR_RETURN_IF(grow_events(c, 5));
-    FTAR_RETURN_IF(peer_allreduce(nullptr, c->staging, count, dt, op, plan, c, stream));
+    FTAR_RETURN_IF(peer_allreduce(nullptr, c->staging, count, dt, op, plan, c, stream, peer_mode));
     FTAR_CHECK_HIP(hipMemcpyAsync(host->dst, c->staging, bytes, hipMemcpyDeviceToHost, stream));
     return FTAR_SUCCESS;
   }
@@ -1070,7 +1176,8 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   // plan covers whole blocks from their start (tests/test_plan.py), so piece
   // k of every stage touches exactly piece k of each block: the same bytes,
   // the same partition, the same bits as the device path.
-  size_t chunk_bytes = c->chunk_bytes;
+  // the piece: fixed, or the model's (0 = whole blocks)
+  size_t chunk_bytes = c->chunk_bytes ? c->chunk_bytes : ex.chunk ? ex.chunk : plan.split * esz;
   if (host) {
     chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
     if (count * esz > c->staging_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the staging buffer"));
@@ -1331,10 +1438,46 @@ ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device) {
   *device = comm->device;
   return FTAR_SUCCESS;
 }
+// Introspection for tools/rccl_order/queue_probe.cpp (not in ftar.h): the communicator's internal streams
+// (comm, reduce, H2D, D2H; null where not created), so the probe can tell which of them share a hardware queue.
+extern "C" ftar_status_t ftar_debug_comm_streams(ftar_comm_t comm, void** streams4) {
+  if (!comm || !streams4) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  streams4[0] = comm->comm_s;
+  streams4[1] = comm->red_s;
+  streams4[2] = comm->h2d_s;
+  streams4[3] = comm->d2h_s;
+  return FTAR_SUCCESS;
+}
 ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes) {
   if (!comm) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
-  comm->chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : ftar::kDefaultChunkBytes;
+  comm->chunk_bytes = bytes ? std::max<size_t>(256, bytes & ~size_t(255)) : 0;  // 0: the model's piece
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_set_form(ftar_comm_t comm, int form) {
+  if (!comm || form < FTAR_FORM_AUTO || form > FTAR_FORM_PEER_WRITE) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  if (!comm->tp->async_p2p() && form != FTAR_FORM_PEER_READ && form != FTAR_FORM_PEER_WRITE) {
+    ftar::set_error("a host-bootstrapped communicator moves data by the peer forms only", __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
+  ftar::set_form(comm, form);
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_get_form(ftar_comm_t comm, int* form) {
+  if (!comm || !form) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  *form = comm->form;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_comm_last_exec(ftar_comm_t comm, ftar_exec_t* out) {
+  if (!comm || !out) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  *out = comm->last_exec;
   return FTAR_SUCCESS;
 }
 ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode) {
@@ -1342,6 +1485,7 @@ ftar_status_t ftar_comm_set_allgather(ftar_comm_t comm, ftar_allgather_t mode) {
     return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   comm->allgather = mode;
+  comm->form = ftar::form_of(comm);
   return FTAR_SUCCESS;
 }
 
@@ -1349,6 +1493,7 @@ ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter
   if (!comm || (mode != FTAR_RS_STAGES && mode != FTAR_RS_DIRECT)) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   comm->reduce_scatter = mode;
+  comm->form = ftar::form_of(comm);
   return FTAR_SUCCESS;
 }
 
@@ -1407,6 +1552,7 @@ ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode) {
   if (!comm || mode < FTAR_PEER_OFF || mode > FTAR_PEER_WRITE) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);
   comm->peer_direct = mode;
+  comm->form = ftar::form_of(comm);
   return FTAR_SUCCESS;
 }
 

@@ -69,6 +69,31 @@ ftar_status_t to_topology(const ftar_topo_t* t, int nranks, Topology* out);
 void from_topology(const Topology& t, ftar_topo_t* out);
 
 // ---------------------------------------------------------------------------
+// the xGMI execution model (cost_model.cpp)
+// ---------------------------------------------------------------------------
+struct CostParams {  // seconds and bytes per second
+  double alpha, link, hbm, issue, barrier, peer_read, peer_write, copy, coll;
+};
+CostParams cost_params();  // defaults <- ftar_cost_set <- FTAR_COST_* environment
+uint64_t cost_generation();  // changes whenever ftar_cost_set / _set_params is called (cached choices expire)
+// every ordered factorization of n into factors >= 2 (cost_model/GetWidth.h:10-47)
+void factorizations(size_t n, std::vector<size_t>& cur, std::vector<std::vector<size_t>>& out);
+// the direct forms run it as one gather-and-fold round plus one all-gather round (schedule.cpp)
+bool one_round_topology(const Topology& t, int P);
+// predicted seconds; < 0 where the form cannot run this topology or its rate is unmeasured
+double exec_cost(const Topology& t, int P, size_t bytes, int form, size_t chunk, bool registered,
+                 const CostParams& k);
+struct ExecChoice {
+  Topology topo;
+  int form = FTAR_FORM_DIRECT;
+  size_t chunk = 0;  // 0: whole blocks
+  double seconds = 0;
+};
+// argmin over what `flags` (FTAR_CHOOSE_*) leaves free; the rest is fixed_*
+ftar_status_t choose_exec(int P, size_t bytes, int flags, const Topology& fixed_topo, int fixed_form,
+                          size_t fixed_chunk, ExecChoice* out);
+
+// ---------------------------------------------------------------------------
 // schedule (mpi_mod.hpp:80-766) lowered to an executable plan
 // ---------------------------------------------------------------------------
 enum BufId : int { BUF_SRC = 0, BUF_DST = 1, BUF_SCRATCH = 2 };

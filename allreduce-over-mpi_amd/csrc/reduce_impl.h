@@ -28,9 +28,9 @@
 //       narrow integers wrap (promotion + truncating store == modular add),
 //       bool sum = OR of non-zero, bf16 (extension) = fp32 accumulate + one RNE.
 #pragma once
-// Internal: the reduce kernels, their traits and launchers (included by reduce_kernels.hip, the
-// production dispatch, and reduce_variants.hip, the A/B harness; anonymous namespace: each TU
-// instantiates what it uses).
+// Internal: the reduce kernels, their traits and launchers, included by reduce_kernels.hip (the
+// production dispatch, libftar.so) and bench_kernels.hip (the A/B harness, libftar_bench.so);
+// anonymous namespace: each TU instantiates what it uses.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -153,58 +153,3 @@ extern "C" long ftar_debug_last_kernel(char* buf, size_t buflen) {
   free(dem);
   return (long)need;
 }
-
-// A/B of the nested fold: lds = 1 the LDS-staged kernel (production), 0 the
-// register kernel of round 1 (tools/kbench_cold.py --shapes).
-extern "C" ftar_status_t ftar_debug_reduce_nested_lds(int lds, const void* const* srcs, int k, void* dst, size_t count,
-                                                      int dtype, const int* shape, int nlevels, void* stream) {
-  return ftar::launch_reduce(srcs, k, dst, count, (ftar_dtype_t)dtype, FTAR_SUM, static_cast<hipStream_t>(stream),
-                             false, shape, nlevels, lds != 0);
-}
-
-namespace ftar {
-namespace {
-// every float bit pattern u (lo half) and u ^ 0x80000001 (hi half) through both bf16 conversions
-__global__ void __launch_bounds__(256) bf16_cvt_check_kernel(unsigned long long* bad, unsigned* first) {
-  const unsigned long long stride = (unsigned long long)gridDim.x * 256;
-  unsigned long long mine = 0;
-  unsigned first_mine = 0xffffffffu;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < (1ull << 32); i += stride) {
-    const unsigned u = (unsigned)i, v = u ^ 0x80000001u;
-    const float lo = __uint_as_float(u), hi = __uint_as_float(v);
-    if (pack_bf16<true>(lo, hi) != pack_bf16<false>(lo, hi)) {
-      ++mine;
-      first_mine = first_mine < u ? first_mine : u;
-    }
-  }
-  if (mine) {
-    atomicAdd(bad, mine);
-    atomicMin(first, first_mine);
-  }
-}
-}  // namespace
-}  // namespace ftar
-
-// Test hook (not in ftar.h): how many of the 2^32 float bit patterns convert to different bf16 bits
-// through v_cvt_pk_bf16_f32 than through the bit-exact RNE (bf16_round_bits); the first such pattern.
-extern "C" ftar_status_t ftar_debug_bf16_cvt_check(unsigned long long* mismatches, unsigned* first) {
-  if (!mismatches || !first) return FTAR_ERR_INVALID_ARG;
-  unsigned long long* d_bad = nullptr;
-  unsigned* d_first = nullptr;
-  ftar_status_t st = FTAR_SUCCESS;  // both buffers are freed on every path below
-  if (hipMalloc(&d_bad, sizeof *d_bad) != hipSuccess || hipMalloc(&d_first, sizeof *d_first) != hipSuccess)
-    st = FTAR_ERR_NO_MEMORY;
-  if (st == FTAR_SUCCESS &&
-      (hipMemset(d_bad, 0, sizeof *d_bad) != hipSuccess || hipMemset(d_first, 0xff, sizeof *d_first) != hipSuccess))
-    st = FTAR_ERR_HIP;
-  if (st == FTAR_SUCCESS) {
-    hipLaunchKernelGGL(ftar::bf16_cvt_check_kernel, dim3(8192), dim3(256), 0, nullptr, d_bad, d_first);
-    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(mismatches, d_bad, sizeof *d_bad, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(first, d_first, sizeof *d_first, hipMemcpyDeviceToHost) != hipSuccess)
-      st = FTAR_ERR_HIP;
-  }
-  ftar::hip_ignore(hipFree(d_bad));
-  ftar::hip_ignore(hipFree(d_first));
-  return st;
-}

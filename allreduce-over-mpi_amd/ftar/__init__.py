@@ -79,6 +79,29 @@ class Topo(ctypes.Structure):
         return [self.stages[i] for i in range(self.nstages)]
 
 
+class CostParams(ctypes.Structure):
+    """ftar_cost_params_t: the xGMI execution model's constants (include/ftar.h)."""
+    _fields_ = [(n, ctypes.c_double) for n in ("alpha_us", "link_gbps", "hbm_gbps", "issue_us", "barrier_us",
+                                               "peer_read_gbps", "peer_write_gbps", "copy_gbps", "coll_gbps")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class Exec(ctypes.Structure):
+    """ftar_exec_t: what the execution model chose (topology, form, piece) and its predicted seconds."""
+    _fields_ = [("topo", Topo), ("form", ctypes.c_int), ("chunk_bytes", ctypes.c_size_t), ("seconds", ctypes.c_double)]
+
+    def as_dict(self):
+        return {"topology": str(self.topo), "form": FORM_NAME.get(self.form, self.form),
+                "chunk_bytes": self.chunk_bytes, "predicted_ms": self.seconds * 1e3 if self.seconds >= 0 else None}
+
+
+FORM = {"auto": -1, "direct": 0, "stages": 1, "collective": 2, "peer-read": 3, "peer-write": 4}   # ftar_form_t
+FORM_NAME = {v: k for k, v in FORM.items()}
+CHOOSE_TOPO, CHOOSE_FORM, CHOOSE_CHUNK, CHOOSE_PEER = 1, 2, 4, 8
+
+
 class UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
@@ -103,6 +126,14 @@ _lib.ftar_topo_choose_reference.argtypes = [_int, ctypes.c_double, ctypes.POINTE
 _lib.ftar_cost_reference_candidates.argtypes = [_int, ctypes.POINTER(_int), _int, ctypes.POINTER(_int), _int]
 _lib.ftar_cost_set_params.argtypes = [ctypes.c_double] * 3
 _lib.ftar_cost_get_params.argtypes = [ctypes.POINTER(ctypes.c_double)] * 3
+_lib.ftar_cost_set.argtypes = [ctypes.POINTER(CostParams)]
+_lib.ftar_cost_get.argtypes = [ctypes.POINTER(CostParams)]
+_lib.ftar_cost_predict.argtypes = [ctypes.POINTER(Topo), _int, _sz, _int, _sz, _int]
+_lib.ftar_cost_predict.restype = ctypes.c_double
+_lib.ftar_exec_choose.argtypes = [_int, _sz, _int, ctypes.POINTER(Exec)]
+_lib.ftar_comm_set_form.argtypes = [_vp, _int]
+_lib.ftar_comm_get_form.argtypes = [_vp, ctypes.POINTER(_int)]
+_lib.ftar_comm_last_exec.argtypes = [_vp, ctypes.POINTER(Exec)]
 _lib.ftar_topo_format.argtypes = [ctypes.POINTER(Topo), ctypes.c_char_p, _sz]
 _lib.ftar_get_unique_id.argtypes = [ctypes.POINTER(UniqueId)]
 _lib.ftar_comm_init_rank.argtypes = [ctypes.POINTER(_vp), _int, UniqueId, _int, _int]
@@ -159,6 +190,19 @@ _lib.ftar_debug_last_kernel.restype = ctypes.c_long
 
 def lib():
     return _lib
+
+
+_bench_lib = None
+
+
+def bench_lib():
+    """libftar_bench.so: the A/B kernel variants (ftar_debug_reduce_variant, ftar_debug_reduce_nested_lds) and
+    kernel test hooks (ftar_debug_bf16_cvt_check) that tools/kbench*.py and the tests load; kept out of the
+    product library, which holds only the kernels the engine dispatches."""
+    global _bench_lib
+    if _bench_lib is None:
+        _bench_lib = ctypes.CDLL(os.path.join(os.path.dirname(LIB_PATH), "libftar_bench.so"))
+    return _bench_lib
 
 
 def version():
@@ -341,6 +385,48 @@ def cost_params(alpha_us=None, link_gbps=None, hbm_gbps=None):
     return {"alpha_us": v[0].value, "link_GBps": v[1].value, "hbm_GBps": v[2].value}
 
 
+def cost_get():
+    """Every constant of the xGMI execution model (defaults <- cost_set <- FTAR_COST_* environment)."""
+    p = CostParams()
+    _check(_lib.ftar_cost_get(ctypes.byref(p)), "ftar_cost_get")
+    return p.as_dict()
+
+
+def cost_set(**kw):
+    """Set the execution model's constants (process-wide); names as in cost_get(); a field left out or <= 0
+    keeps (or restores) its default.  Returns cost_get()."""
+    p = CostParams(**{k: float(v or 0.0) for k, v in kw.items()})
+    _check(_lib.ftar_cost_set(ctypes.byref(p)), "ftar_cost_set")
+    return cost_get()
+
+
+def cost_predict(t, form, chunk_bytes, nranks, nbytes, registered=False):
+    """Predicted seconds of one AllReduce (ftar_cost_predict); None where it cannot run that way."""
+    v = _lib.ftar_cost_predict(ctypes.byref(topo(t)), FORM[form] if isinstance(form, str) else form, chunk_bytes,
+                               nranks, nbytes, int(registered))
+    return None if v < 0 else v
+
+
+def exec_choose(nranks, nbytes, topo_=None, form=None, chunk_bytes=None, peer=True):
+    """The execution model's choice (ftar_exec_choose): whatever is None is chosen; returns an Exec."""
+    e = Exec()
+    flags = 0
+    if topo_ is None:
+        flags |= CHOOSE_TOPO
+    else:
+        e.topo = topo(topo_)
+    if form is None:
+        flags |= CHOOSE_FORM | (CHOOSE_PEER if peer else 0)
+    else:
+        e.form = FORM[form] if isinstance(form, str) else form
+    if chunk_bytes is None:
+        flags |= CHOOSE_CHUNK
+    else:
+        e.chunk_bytes = chunk_bytes
+    _check(_lib.ftar_exec_choose(nranks, nbytes, flags, ctypes.byref(e)), "ftar_exec_choose")
+    return e
+
+
 def schedule_json(t, nranks, rank, count):
     t = topo(t)
     n = _lib.ftar_schedule_json(ctypes.byref(t), nranks, rank, count, None, 0)
@@ -423,6 +509,24 @@ class Comm:
     @chunk_bytes.setter
     def chunk_bytes(self, b):
         _check(_lib.ftar_comm_set_chunk_bytes(self.handle, b), "chunk_bytes")
+
+    @property
+    def form(self):
+        """The data-movement form: "auto" (the execution model chooses per call), a form name, or -2 (a mix of
+        all-gather / reduce-scatter settings no form names)."""
+        v = _int()
+        _check(_lib.ftar_comm_get_form(self.handle, ctypes.byref(v)), "form")
+        return FORM_NAME.get(v.value, v.value)
+
+    @form.setter
+    def form(self, f):
+        _check(_lib.ftar_comm_set_form(self.handle, FORM[f] if isinstance(f, str) else f), "form")
+
+    def last_exec(self):
+        """What the last call on this communicator ran (ftar_comm_last_exec), as a dict."""
+        e = Exec()
+        _check(_lib.ftar_comm_last_exec(self.handle, ctypes.byref(e)), "last_exec")
+        return e.as_dict()
 
     def allreduce(self, sendbuf, recvbuf, count, dtype="f32", op="sum", topo_=None, lonely=0, stream=None):
         t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
@@ -601,6 +705,10 @@ class LocalGroup:
     def set_chunk_bytes(self, b):
         for c in self.comms:
             c.chunk_bytes = b
+
+    def set_form(self, f):
+        for c in self.comms:
+            c.form = f
 
     def set_allgather(self, mode):
         for c in self.comms:

@@ -135,6 +135,64 @@ double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes);
 ftar_status_t ftar_cost_set_params(double alpha_us, double link_gbps, double hbm_gbps);
 ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* hbm_gbps);
 
+/* ---- execution model: (topology, data-movement form, pipeline piece) -------
+ * The role of the reference's CostModel (cost_model/CostModel.h:82-120: a
+ * width list chosen for a chunk size), re-derived for one MI355X node.  With
+ * the one-round forms every topology moves tree(P)'s bytes, so what varies on
+ * a node is the form and the piece size; the model prices both:
+ *   per piece of a round: r(x) = max(alpha + x / link, issue)  (x = bytes per
+ *   link), a fold of k sources (k + 1) * c / hbm on the reduce stream, the
+ *   fill / drain of that two-stream pipeline simulated piece by piece; peer
+ *   forms: barriers, xGMI loads / stores and their local copy pass.
+ * Forms (ftar_comm_set_form; the env FTAR_FORM=auto|direct|stages|collective|
+ * peer-read|peer-write at init): */
+typedef enum {
+  FTAR_FORM_AUTO = -1,       /* the model chooses per call (the default) */
+  FTAR_FORM_DIRECT = 0,      /* one-round reduce-scatter + all-gather, RCCL p2p */
+  FTAR_FORM_STAGES = 1,      /* the reference's rounds both ways, RCCL p2p */
+  FTAR_FORM_COLLECTIVE = 2,  /* one-round reduce-scatter + ncclAllGather */
+  FTAR_FORM_PEER_READ = 3,   /* IPC peer-direct read (FTAR_PEER_READ) */
+  FTAR_FORM_PEER_WRITE = 4   /* IPC peer-direct write (FTAR_PEER_WRITE) */
+} ftar_form_t;
+/* The model's constants, SI-like units as named.  A field <= 0 in
+ * ftar_cost_set restores its default; FTAR_COST_<FIELD> in the environment
+ * (ALPHA_US, LINK_GBPS, HBM_GBPS, ISSUE_US, BARRIER_US, PEER_READ_GBPS,
+ * PEER_WRITE_GBPS, COPY_GBPS, COLL_GBPS) overrides both.  peer_*_gbps and
+ * coll_gbps default to 0 = unmeasured: those forms are then never chosen.
+ * Process-wide; every rank must hold the same values (compared at a
+ * communicator's first call). */
+typedef struct {
+  double alpha_us;        /* one p2p group (one piece of one round): launch + handshake */
+  double link_gbps;       /* RCCL p2p, one peer, one direction */
+  double hbm_gbps;        /* the fold's rate, algorithmic bytes ((k+1) x piece) per second */
+  double issue_us;        /* host time to enqueue one piece of one round (groups, events, fold) */
+  double barrier_us;      /* one stream-ordered barrier of the peer forms */
+  double peer_read_gbps;  /* one peer, kernel loads over xGMI (0 = unmeasured) */
+  double peer_write_gbps; /* one peer, kernel stores over xGMI (0 = unmeasured) */
+  double copy_gbps;       /* local copy, algorithmic bytes (read + written) per second */
+  double coll_gbps;       /* ncclAllGather: bytes each rank receives per second (0 = unmeasured) */
+} ftar_cost_params_t;
+ftar_status_t ftar_cost_set(const ftar_cost_params_t* params);
+ftar_status_t ftar_cost_get(ftar_cost_params_t* params);
+/* Predicted seconds of one AllReduce of `bytes` per rank: topology, form
+ * (not AUTO), piece size (0 = whole blocks); registered != 0 prices the peer
+ * forms on registered buffers (no local pass).  < 0: not runnable that way. */
+double ftar_cost_predict(const ftar_topo_t* topo, int form, size_t chunk_bytes, int nranks, size_t bytes,
+                         int registered);
+typedef struct {
+  ftar_topo_t topo;
+  int form;            /* ftar_form_t */
+  size_t chunk_bytes;  /* pipeline piece (the one-round and staged forms); 0 for the peer forms */
+  double seconds;      /* predicted */
+} ftar_exec_t;
+#define FTAR_CHOOSE_TOPO 1  /* the topology is free (else inout->topo is used) */
+#define FTAR_CHOOSE_FORM 2  /* the form is free (else inout->form) */
+#define FTAR_CHOOSE_CHUNK 4 /* the piece size is free (else inout->chunk_bytes) */
+#define FTAR_CHOOSE_PEER 8  /* the peer forms may be chosen (their rates permitting) */
+/* The model's argmin over what `flags` leaves free; ties keep the fewest
+ * stages, then the simpler form, then the larger piece. */
+ftar_status_t ftar_exec_choose(int nranks, size_t bytes, int flags, ftar_exec_t* inout);
+
 /* The reference's own cost model, restated bit for bit
  * (cost_model/CostModel.h:1-120; tests/golden/costmodel.jsonl holds its
  * output).  ftar_topo_choose uses it instead of the xGMI model when
@@ -177,9 +235,21 @@ ftar_status_t ftar_comm_destroy(ftar_comm_t comm);
 ftar_status_t ftar_comm_rank(ftar_comm_t comm, int* rank);
 ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size);
 ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device);
-/* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = default. */
+/* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = the
+ * execution model's piece for each call (the default; FTAR_CHUNK_BYTES at
+ * init fixes it).  get: 0 while the model chooses. */
 ftar_status_t ftar_comm_set_chunk_bytes(ftar_comm_t comm, size_t bytes);
 ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
+/* The data-movement form (ftar_form_t).  FTAR_FORM_AUTO (the default): the
+ * execution model chooses per call among the forms the communicator can run
+ * (peer forms only once their rates are set, ftar_cost_set); any other value
+ * fixes it, as do ftar_comm_set_allgather / _reduce_scatter / _peer_direct
+ * (get then reports the form those describe, or -2 for a mix no form names).
+ * A host-bootstrapped communicator keeps its peer form.
+ * ftar_comm_last_exec: what the last call on this communicator ran. */
+ftar_status_t ftar_comm_set_form(ftar_comm_t comm, int form);
+ftar_status_t ftar_comm_get_form(ftar_comm_t comm, int* form);
+ftar_status_t ftar_comm_last_exec(ftar_comm_t comm, ftar_exec_t* out);
 /* How the all-gather phase is moved.  After the reduce-scatter stages every
  * rank holds exactly one fully reduced block (block r on trees, lonely ranks
  * included; block (r+1) mod P on the ring), so the phase only delivers final

@@ -246,48 +246,43 @@ def ddp(comm, res, world, rank):
 
 def full_size(comm, res, world, rank):
     """BASELINE's full buckets over RCCL at P = world (8 for C4/C5): C4 = 2^28 fp32 on the ring (direct and
-    the reference's staged rounds), C5 = 2^29 bf16 on the width-P tree; out of place, device-resident.  Each
-    rank's whole output must equal every other rank's (a checksum of its bits, all-gathered), and 65,536
-    sampled elements plus every block boundary must equal the reference's fold of the P inputs there
-    (tests/sample_fold.py, pinned to the oracle by tests/test_sample_fold.py)."""
-    import numpy as np
+    the reference's staged rounds, default pieces and pieces of 24 MiB + 4 KiB that divide no block), C5 = 2^29
+    bf16 on the width-P tree; out of place, device-resident, random inputs that differ per rank.  Every rank
+    regenerates all P inputs from their seeds and compares its WHOLE output bit for bit with the reference's
+    fold over the whole bucket (tests/whole_fold.py, pinned to the oracle by tests/test_whole_fold.py)."""
     import torch
-    import torch.distributed as dist
 
-    import sample_fold
+    import whole_fold
     res["full"] = []
-    for n, dt, topo, form in (((1 << 28), "f32", "1", "direct"), ((1 << 28), "f32", "1", "stages"),
-                              ((1 << 29), "bf16", str(world), "direct")):
+    odd = 24 * (1 << 20) + 4096
+    for n, dt, topo, form, chunk in (((1 << 28), "f32", "1", "direct", 0), ((1 << 28), "f32", "1", "stages", 0),
+                                     ((1 << 28), "f32", "1", "direct", odd), ((1 << 28), "f32", "1", "stages", odd),
+                                     ((1 << 29), "bf16", str(world), "direct", 0)):
         tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
         comm.allgather = form
         comm.reduce_scatter = "stages" if form == "stages" else "direct"
-        g = torch.Generator(device="cuda")
-        g.manual_seed(2024 + rank)
-        x = (torch.rand(n, generator=g, device="cuda") * 2 - 1).to(tdt)
+        comm.chunk_bytes = chunk
+
+        def gen(r):
+            g = torch.Generator(device="cuda")
+            g.manual_seed(2024 + r)
+            return (torch.rand(n, generator=g, device="cuda") * 2 - 1).to(tdt)
+
+        x = gen(rank)
         y = torch.empty_like(x)
         comm.allreduce(x, y, n, dt, "sum", topo_=topo, stream=torch.cuda.current_stream())
         torch.cuda.synchronize()
-        split = -(-n // world)
-        rng = np.random.default_rng(7)
-        idx = np.unique(np.concatenate([rng.integers(0, n, 65536), np.arange(world) * split,
-                                        np.minimum(np.arange(1, world + 1) * split, n) - 1]))
-        it = torch.from_numpy(idx).cuda()
-        mine = x[it].float().cpu()
-        allv = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allv, mine)
-        exp = sample_fold.fold(np.stack([a.numpy() for a in allv]), idx, n, "ring" if topo == "1" else "tree",
-                               bf16=dt == "bf16")
-        got = y[it].float().cpu().numpy()
-        bits = y.view(torch.int16 if dt == "bf16" else torch.int32).to(torch.int64)
-        h = torch.tensor([int((bits * (torch.arange(n, device="cuda") % 65521 + 1)).sum().item())])
-        hs = [torch.empty_like(h) for _ in range(world)]
-        dist.all_gather(hs, h)
-        ok = np.array_equal(got.view(np.uint32), exp.view(np.uint32)) and len({int(v) for v in hs}) == 1
-        res["full"].append(f"{dt} n={n} topo={topo} {form}: {'ok' if ok else 'MISMATCH'}")
-        if not ok:
+        xs = [x if r == rank else gen(r) for r in range(world)]
+        exp = whole_fold.fold(xs, n, "ring" if topo == "1" else "tree")
+        bad = whole_fold.first_mismatch(y, exp)
+        what = f"{dt} n={n} topo={topo} {form} chunk={chunk or 'default'}"
+        res["full"].append(f"{what}: " + ("ok (whole bucket)" if bad is None else
+                                          f"MISMATCH in {bad[0]} elements, first at {bad[1]}"))
+        if bad is not None:
             res["fail"].append(res["full"][-1])
-        del x, y, bits
+        del x, y, xs, exp
         torch.cuda.empty_cache()
+    comm.chunk_bytes = 0
 
 
 def capture(comm, res, world, rank):

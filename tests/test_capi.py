@@ -23,6 +23,17 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_kernel_variants_live_in_the_bench_library_only():
+    """The A/B kernel variants and kernel test hooks are in libftar_bench.so (tools/kbench*.py, the bf16
+    conversion test), not in the product library, which keeps only what the engine dispatches and the
+    ftar_debug_last_kernel hook bench.py ties its PMC traffic to."""
+    import ftar
+    moved = ("ftar_debug_reduce_variant", "ftar_debug_reduce_nested_lds", "ftar_debug_bf16_cvt_check")
+    assert not [n for n in moved if hasattr(ftar.lib(), n)]
+    assert all(hasattr(ftar.bench_lib(), n) for n in moved)
+    assert hasattr(ftar.lib(), "ftar_debug_last_kernel")
+
+
 def test_version_and_status_strings():
     import ftar
     assert "gfx950" in ftar.version()

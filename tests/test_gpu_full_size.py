@@ -1,42 +1,54 @@
-"""The AllReduce at BASELINE's full bucket sizes, through size-independent properties.
+"""The AllReduce at BASELINE's full bucket sizes, every element checked.
 
-C3 = 2 ranks x 2^26 fp32 ring, C4 = 8 ranks x 2^28 fp32 ring (both data-movement forms), C5 = 8 ranks x
-2^29 bf16 width-8 tree: every rank of an in-process group (ftar_comm_init_local) on cuda:0, the product's
-plan executor, pipelining and reduce kernels, out of place.  The oracle would need 8-16 GiB of host arrays
-here, so instead:
-  * a sample of elements (every block boundary, the ends, 4096 seeded random indices) is bit-exact against
-    the reference's fold of those elements (tests/sample_fold.py, itself pinned to the oracle by
-    tests/test_sample_fold.py);
-  * every rank ends with the same bits over the whole bucket;
-  * the call on the negated inputs gives exactly the negated result everywhere (round-to-nearest-even is
-    sign-symmetric), which also proves the call read all of this call's data.
+C3 = 2 ranks x 2^26 fp32 ring, C4 = 8 ranks x 2^28 fp32 (the ring in both data-movement forms, and the
+width-8 tree), C5 = 8 ranks x 2^29 bf16 width-8 tree: every rank of an in-process group (ftar_comm_init_local)
+on cuda:0, the product's plan executor, pipelining and reduce kernels, out of place.  Random inputs differ per
+rank, so the association order shows in the bits.  Every rank's WHOLE output is compared bit for bit with the
+reference's fold of the P inputs, evaluated over the whole bucket on the GPU by tests/whole_fold.py (pinned to
+the oracle by tests/test_whole_fold.py).  Some cases use pipeline pieces that do not divide a block
+(FTAR_CHUNK_BYTES / the host piece size), so piece boundaries fall mid-block and every block ends on a short
+piece; in host mode the (stage, piece) steps also run skewed (engine.cpp step_order).
 """
-import numpy as np
 import pytest
 
-import sample_fold
+import whole_fold
 
 pytestmark = pytest.mark.gpu
 
-
-def _sample_index(n, P, seed=99):
-    split = -(-n // P)
-    pts = {0, n - 1}
-    for b in range(1, P):
-        for d in (-1, 0, 1):
-            pts.add(b * split + d)
-    rng = np.random.default_rng(seed)
-    pts.update(int(v) for v in rng.integers(0, n, 4096))
-    return np.array(sorted(p for p in pts if 0 <= p < n), dtype=np.int64)
+MiB = 1 << 20
+# pieces that divide no block: 24 MiB + 4 KiB (C4: 128 MiB blocks -> 5 whole pieces + an 8 MiB tail; the
+# element count is a multiple of 64, as the engine rounds it) and 20 MiB + 256 B for the host pipeline
+ODD_CHUNK = 24 * MiB + 4096
+ODD_HOST_CHUNK = 20 * MiB + 256
 
 
-@pytest.mark.parametrize("P,n,dt,topo,form", [
-    (2, 1 << 26, "f32", "1", "direct"),     # C3
-    (8, 1 << 28, "f32", "1", "direct"),     # C4, one-round forms (the default)
-    (8, 1 << 28, "f32", "1", "stages"),     # C4, the reference's 2(P-1) ring steps
-    (8, 1 << 29, "bf16", "8", "direct"),    # C5, the cost model's width-8 tree
+def _inputs(P, n, tdt, seed, dev):
+    import torch
+    xs = []
+    for r in range(P):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed + r)
+        xs.append((torch.rand(n, generator=gen, device=dev) * 2 - 1).to(tdt))
+    return xs
+
+
+def _check_whole(ys, exp, what):
+    for r, y in enumerate(ys):
+        bad = whole_fold.first_mismatch(y, exp)
+        assert bad is None, f"{what}: rank {r}: {bad[0]} elements differ from the reference's fold, first at {bad[1]}"
+
+
+@pytest.mark.parametrize("P,n,dt,topo,form,chunk", [
+    (2, 1 << 26, "f32", "1", "direct", 0),            # C3
+    (8, 1 << 28, "f32", "1", "direct", 0),            # C4, one-round forms (the default)
+    (8, 1 << 28, "f32", "1", "stages", 0),            # C4, the reference's 2(P-1) ring steps
+    (8, 1 << 28, "f32", "8", "direct", 0),            # C4's bucket on the width-8 tree
+    (8, 1 << 28, "f32", "1", "direct", ODD_CHUNK),    # C4, piece boundaries mid-block, short last pieces
+    (8, 1 << 28, "f32", "1", "stages", ODD_CHUNK),
+    (8, 1 << 29, "bf16", "8", "direct", 0),           # C5, the cost model's width-8 tree
+    (8, 1 << 29, "bf16", "8", "direct", ODD_CHUNK),
 ])
-def test_allreduce_full_size_properties(P, n, dt, topo, form):
+def test_allreduce_full_size_whole_bucket(P, n, dt, topo, form, chunk):
     import torch
 
     import ftar
@@ -47,32 +59,14 @@ def test_allreduce_full_size_properties(P, n, dt, topo, form):
     try:
         g.set_allgather(form)
         g.set_reduce_scatter(form)
-        for r in range(P):
-            gen = torch.Generator(device=dev)
-            gen.manual_seed(4242 + r)
-            xs.append((torch.rand(n, generator=gen, device=dev) * 2 - 1).to(tdt))
-            ys.append(torch.empty(n, dtype=tdt, device=dev))
-        idx = _sample_index(n, P)
-        it = torch.from_numpy(idx).to(dev)
-        samp = np.stack([x[it].float().cpu().numpy() for x in xs])
-
+        if chunk:
+            g.set_chunk_bytes(chunk)
+        xs = _inputs(P, n, tdt, 4242, dev)
+        ys = [torch.empty(n, dtype=tdt, device=dev) for _ in range(P)]
         g.allreduce(xs, ys, n, dt, "sum", topo_=topo)
         torch.cuda.synchronize()
-        exp = sample_fold.fold(samp, idx, n, "ring" if topo == "1" else "tree", bf16=dt == "bf16")
-        got = ys[0][it].float().cpu().numpy()
-        bad = np.nonzero(got.view(np.uint32) != exp.view(np.uint32))[0]
-        assert bad.size == 0, f"{bad.size} sampled elements differ, first at {idx[bad[0]]}: {got[bad[0]]} vs {exp[bad[0]]}"
-        for r in range(1, P):
-            assert torch.equal(ys[r], ys[0]), f"rank {r} differs from rank 0"
-
-        y0 = ys[0].clone()
-        for x in xs:
-            x.neg_()
-        g.allreduce(xs, ys, n, dt, "sum", topo_=topo)
-        torch.cuda.synchronize()
-        assert torch.equal(ys[0], y0.neg_()), "negated inputs did not give the negated result"
-        for r in range(1, P):
-            assert torch.equal(ys[r], ys[0]), f"rank {r} differs from rank 0 (negated call)"
+        exp = whole_fold.fold(xs, n, "ring" if topo == "1" else "tree")
+        _check_whole(ys, exp, f"P={P} n={n} {dt} topo={topo} {form} chunk={chunk}")
     finally:
         g.destroy()
         xs.clear()
@@ -83,8 +77,9 @@ def test_allreduce_full_size_properties(P, n, dt, topo, form):
 @pytest.mark.parametrize("topo", ["1", "2"])
 def test_allreduce_past_int32_elements(topo):
     """2^31 + 77 u8 elements per rank (the reference's `int count` stops below 2^31, mpi_mod.hpp:1724): block
-    offsets and piece indices past 2^31 in the engine.  u8 sums wrap and are associative, so the sample check is
-    exact in any order; then linearity over the whole bucket: inputs + 1 on every rank give result + P (mod 256)."""
+    offsets and piece indices past 2^31 in the engine.  u8 sums wrap and are associative, so torch's x0 + x1
+    (uint8, wrapping) is the reference's result in any order: every element of both ranks is compared; then
+    linearity over the whole bucket: inputs + 1 on every rank give result + P (mod 256)."""
     import torch
 
     import ftar
@@ -98,13 +93,12 @@ def test_allreduce_past_int32_elements(topo):
             gen.manual_seed(777 + r)
             xs.append(torch.randint(0, 256, (n,), generator=gen, dtype=torch.uint8, device=dev))
             ys.append(torch.empty(n, dtype=torch.uint8, device=dev))
-        idx = _sample_index(n, P)
-        it = torch.from_numpy(idx).to(dev)
         g.allreduce(xs, ys, n, "u8", "sum", topo_=topo)
         torch.cuda.synchronize()
-        exp = sum(x[it].to(torch.int64) for x in xs) % 256
-        assert torch.equal(ys[0][it].to(torch.int64), exp)
-        assert torch.equal(ys[1], ys[0])
+        exp = xs[0] + xs[1]
+        assert torch.equal(ys[0], exp)
+        assert torch.equal(ys[1], exp)
+        del exp
         y0 = ys[0].clone()
         for x in xs:
             x.add_(1)
@@ -119,49 +113,37 @@ def test_allreduce_past_int32_elements(topo):
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("P,n,dt,topo", [
-    (8, 1 << 28, "f32", "1"),     # C4 through the MPI_Allreduce_FT path (host buffers, in place)
-    (8, 1 << 29, "bf16", "8"),    # C5, same
+@pytest.mark.parametrize("P,n,dt,topo,piece", [
+    (8, 1 << 28, "f32", "1", 0),                 # C4 through the MPI_Allreduce_FT path (host buffers, in place)
+    (8, 1 << 29, "bf16", "8", 0),                # C5, same
+    (8, 1 << 28, "f32", "1", ODD_HOST_CHUNK),    # C4 with host pieces that divide no block (skewed steps)
 ])
-def test_host_allreduce_full_size_properties(P, n, dt, topo):
-    """ftar_allreduce_host (H2D / exchange / D2H pipelined per piece) on pinned host buckets of BASELINE's full
-    size, in place like benchmark.cpp:161: the sampled per-element fold, rank agreement, negation symmetry."""
+def test_host_allreduce_full_size_whole_bucket(P, n, dt, topo, piece):
+    """ftar_allreduce_host (H2D / exchange / D2H pipelined per piece, stage s+1 one piece behind stage s) on
+    pinned host buckets of BASELINE's full size, in place like benchmark.cpp:161: every rank's whole bucket
+    against the reference's fold of the P inputs."""
     import torch
 
     import ftar
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
     dev = torch.device("cuda", 0)
     g = ftar.Comm.init_local(P)
-    hs, orig = [], []
+    hs = []
     try:
-        for r in range(P):
-            gen = torch.Generator(device=dev)
-            gen.manual_seed(5151 + r)
-            hs.append((torch.rand(n, generator=gen, device=dev) * 2 - 1).to(tdt).cpu().pin_memory())
-        orig.extend(h.clone() for h in hs)
-        idx = _sample_index(n, P)
-        it = torch.from_numpy(idx)
-        samp = np.stack([h[it].float().numpy() for h in hs])
+        if piece:
+            g.set_host_chunk_bytes(piece)
+        xs = _inputs(P, n, tdt, 5151, dev)
+        hs = [x.cpu().pin_memory() for x in xs]
+        exp = whole_fold.fold(xs, n, "ring" if topo == "1" else "tree")
+        del xs
         g.allreduce(None, hs, n, dt, "sum", topo_=topo, host=True)
         torch.cuda.synchronize()
-        exp = sample_fold.fold(samp, idx, n, "ring" if topo == "1" else "tree", bf16=dt == "bf16")
-        got = hs[0][it].float().numpy()
-        bad = np.nonzero(got.view(np.uint32) != exp.view(np.uint32))[0]
-        assert bad.size == 0, f"{bad.size} sampled elements differ, first at {idx[bad[0]]}"
-        for r in range(1, P):
-            assert torch.equal(hs[r], hs[0]), f"rank {r} differs from rank 0"
-        y0 = hs[0].clone()
-        for h, x in zip(hs, orig):
-            torch.neg(x, out=h)
-        g.allreduce(None, hs, n, dt, "sum", topo_=topo, host=True)
-        torch.cuda.synchronize()
-        assert torch.equal(hs[0], y0.neg_()), "negated inputs did not give the negated result"
-        for r in range(1, P):
-            assert torch.equal(hs[r], hs[0]), f"rank {r} differs from rank 0 (negated call)"
+        for r, h in enumerate(hs):
+            bad = whole_fold.first_mismatch(h.to(dev), exp)
+            assert bad is None, f"rank {r}: {bad[0]} elements differ from the reference's fold, first at {bad[1]}"
     finally:
         g.destroy()
         hs.clear()
-        orig.clear()
         torch.cuda.empty_cache()
 
 

@@ -94,10 +94,11 @@ def test_ddp_comm_hook_over_rccl(world, dtype):
 
 
 def test_rccl_p2p_baseline_c4_c5_full_size():
-    """BASELINE configs[3] (8 ranks x 2^28 fp32, the ring, direct and staged) and configs[4] (8 ranks x 2^29
-    bf16, the width-8 tree) over RCCL between 8 processes: every rank's whole output identical across ranks,
-    and 65,536 sampled elements plus the block boundaries equal the reference's fold (sample_fold)."""
+    """BASELINE configs[3] (8 ranks x 2^28 fp32, the ring, direct and staged, default pieces and pieces that
+    divide no block) and configs[4] (8 ranks x 2^29 bf16, the width-8 tree) over RCCL between 8 processes,
+    random inputs per rank: every rank's WHOLE output bit for bit against the reference's fold of all P inputs
+    (tests/whole_fold.py, each rank regenerating every rank's input from its seed)."""
     p, res = run_loopback(8, {"FTAR_LOOPBACK_MODE": "full"})
     assert p.returncode == 0 and len(res) == 8, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
-        assert not r["fail"] and len(r["full"]) == 3, r
+        assert not r["fail"] and len(r["full"]) == 5, r

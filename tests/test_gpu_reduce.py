@@ -311,7 +311,7 @@ def test_bf16_hardware_conversion_is_the_rne_for_every_float():
     2^32 float bit patterns, NaN payloads, infinities and denormals included: the kernels may use either."""
     import ctypes
     import ftar
-    lib = ftar.lib()
+    lib = ftar.bench_lib()
     lib.ftar_debug_bf16_cvt_check.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_uint)]
     bad, first = ctypes.c_ulonglong(0), ctypes.c_uint(0)
     assert lib.ftar_debug_bf16_cvt_check(ctypes.byref(bad), ctypes.byref(first)) == 0

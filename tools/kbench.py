@@ -3,7 +3,7 @@
 
     python tools/kbench.py [--elements N] [--rounds R] [--variants 0,1,..] [--ks 2,4,8] [--dtypes f32,bf16]
 Each variant = (vectors/lane, nt loads, nt stores, workgroup size, grid cap),
-see ftar_debug_reduce_variant in csrc/reduce_variants.hip.  Prints median/min
+see ftar_debug_reduce_variant in csrc/bench_kernels.hip (libftar_bench.so).  Prints median/min
 kernel time and GB/s ((k+1)*n*esz bytes) per (dtype, k, variant), plus a
 device-to-device copy as a reference point.  Every variant's output is
 compared with variant 0's.
@@ -29,7 +29,7 @@ ap.add_argument("--ks", default="2,4,8")
 ap.add_argument("--dtypes", default="f32,bf16")
 ap.add_argument("--shapes", default="", help='nested folds instead of variants, e.g. "8;2,4;2,2,2" ("8" = flat)')
 a = ap.parse_args()
-lib = ftar.lib()
+lib = ftar.bench_lib()
 lib.ftar_debug_reduce_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 dev = torch.device("cuda:0")

@@ -33,7 +33,7 @@ ap.add_argument("--inplace", action="store_true", help="dst = source 0 (the in-p
 ap.add_argument("--shapes", default="", help='nested folds instead of flat variants, e.g. "2,4;4,2;2,2,2": variant 1 '
                                              '= LDS-staged (production), 0 = register kernel (round 1)')
 a = ap.parse_args()
-lib = ftar.lib()
+lib = ftar.bench_lib()
 lib.ftar_debug_reduce_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
                                           ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 lib.ftar_debug_reduce_nested_lds.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int,
