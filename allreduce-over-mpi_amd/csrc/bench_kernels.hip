@@ -198,3 +198,37 @@ extern "C" ftar_status_t ftar_debug_bf16_cvt_check(unsigned long long* mismatche
   ftar::hip_ignore(hipFree(d_first));
   return st;
 }
+
+// ---------------------------------------------------------------------------
+// Rehearsal hook of bench.py: a stream that really never drains while the RCCL preflight is
+// waited for.  One wave spins on a host flag (a system-scope atomic load, vector memory) until the host
+// releases it or `seconds` pass -- every wave reaches that exit, so the stream always drains in the end.
+// ---------------------------------------------------------------------------
+namespace {
+__global__ void block_stream_kernel(int* flag, unsigned long long limit_ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+         wall_clock64() - t0 < limit_ticks)
+    __builtin_amdgcn_s_sleep(8);
+}
+}  // namespace
+
+// Enqueues the spinning wave on `stream`; returns the host flag to release (ftar_debug_unblock), or NULL.
+extern "C" void* ftar_debug_block_stream(void* stream, double seconds) {
+  int* flag = nullptr;
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&flag), sizeof(int), hipHostMallocCoherent | hipHostMallocMapped) !=
+          hipSuccess)
+    return nullptr;
+  __atomic_store_n(flag, 0, __ATOMIC_SEQ_CST);
+  const unsigned long long ticks = (unsigned long long)(seconds * 1e3 * khz);
+  hipLaunchKernelGGL(block_stream_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), flag, ticks);
+  if (hipGetLastError() != hipSuccess) return nullptr;
+  return flag;
+}
+
+// Releases a stream blocked by ftar_debug_block_stream (the 4-byte flag stays allocated).
+extern "C" void ftar_debug_unblock(void* flag) {
+  if (flag) __atomic_store_n(static_cast<int*>(flag), 1, __ATOMIC_SEQ_CST);
+}

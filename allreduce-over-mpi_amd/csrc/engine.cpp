@@ -18,6 +18,8 @@
 // The caller's stream is joined at entry and at exit with events, so the call
 // is stream-ordered like any other HIP operation.
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <cstdio>
@@ -30,6 +32,15 @@
 #include "ftar_internal.h"
 
 using ftar::hip_ignore;
+
+// The outcome of a communicator's first contact, shared with the helper thread that runs it.
+struct FirstContact {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  ftar_status_t st = FTAR_SUCCESS;
+  std::string err;
+};
 
 struct ftar_comm {
   int rank = 0, nranks = 1, device = 0;
@@ -77,6 +88,11 @@ struct ftar_comm {
   int allgather = FTAR_AG_DIRECT;
   int reduce_scatter = FTAR_RS_DIRECT;
   bool settings_agreed = false;  // agree_settings ran (engine.cpp comm_setup / the first call)
+  // the first contact (first_contact) did not finish within its deadline: every call fails with
+  // FTAR_ERR_TIMEOUT, and teardown aborts the transport instead of draining it
+  bool broken = false;
+  std::thread contact_thread;  // the first contact's helper (joined, or left behind on a broken communicator)
+  std::shared_ptr<struct FirstContact> contact;
   // the scratch buffer registered with RCCL (ncclCommRegister), so p2p receives may land in it without
   // RCCL's staging copies (FTAR_RCCL_REGISTER=1 / ftar_debug_set_rccl_register; bench.py sweeps it)
   bool rccl_reg = false;
@@ -219,9 +235,11 @@ ftar_status_t grow_events(ftar_comm* c, size_t n) {
 }
 }  // namespace
 
-ftar_status_t agree_settings(ftar_comm* c);
+ftar_status_t agree_settings(ftar_comm* c, bool failed = false);
 
-ftar_status_t comm_setup(ftar_comm* c) {
+namespace {
+// the local part of a communicator's bring-up: streams, events, settings from the environment
+ftar_status_t comm_setup_local(ftar_comm* c) {
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   if (const char* rc = getenv("FTAR_REDUCE_CUS")) FTAR_RETURN_IF(set_reduce_cus(c, atoi(rc)));
@@ -260,14 +278,24 @@ ftar_status_t comm_setup(ftar_comm* c) {
   const char* cb = getenv("FTAR_CHUNK_BYTES");
   const size_t cbv = cb ? strtoull(cb, nullptr, 0) : 0;
   c->chunk_bytes = cbv ? std::max<size_t>(256, cbv & ~size_t(255)) : 0;
-  // a host-bootstrapped communicator compares its settings now (its host collective cannot hang on a
-  // rank whose bring-up failed: that rank reports through it too); an RCCL one at its first call, so a
-  // rank whose RCCL bring-up failed leaves no peer waiting in a collective inside ftar_comm_init_rank
-  if (!c->tp->async_p2p()) {
-    FTAR_RETURN_IF(agree_settings(c));
-    c->settings_agreed = true;
-  }
   return FTAR_SUCCESS;
+}
+}  // namespace
+
+// A host-bootstrapped communicator compares its settings at bring-up, and a rank whose local bring-up
+// failed still takes part in that host collective, flagging its failure, so no peer is left waiting in it
+// (ADVICE r3); an RCCL one compares them at its first call (first_contact), so a rank whose RCCL bring-up
+// failed leaves no peer waiting in a collective inside ftar_comm_init_rank.
+ftar_status_t comm_setup(ftar_comm* c) {
+  ftar_status_t st = comm_setup_local(c);
+  if (!c->tp->async_p2p()) {
+    const std::string local_err = st == FTAR_SUCCESS ? "" : last_error();
+    const ftar_status_t ag = agree_settings(c, st != FTAR_SUCCESS);
+    if (st != FTAR_SUCCESS) set_error(local_err, __FILE__, __LINE__);
+    else st = ag;
+    if (st == FTAR_SUCCESS) c->settings_agreed = true;
+  }
+  return st;
 }
 
 // The environment-derived settings that shape the messages every rank posts (piece sizes, data-movement
@@ -277,7 +305,7 @@ ftar_status_t comm_setup(ftar_comm* c) {
 // instead of hanging a call.
 // Setters (ftar_comm_set_*, ftar_cost_set_params) must likewise be called alike, as RCCL's own
 // configuration must.
-ftar_status_t agree_settings(ftar_comm* c) {
+ftar_status_t agree_settings(ftar_comm* c, bool failed) {
   auto h = [](const char* v) {  // FNV-1a of an environment string ("" = unset)
     uint64_t x = 1469598103934665603ull;
     for (const char* p = v ? v : ""; *p; ++p) x = (x ^ (unsigned char)*p) * 1099511628211ull;
@@ -291,16 +319,66 @@ ftar_status_t agree_settings(ftar_comm* c) {
                                      h(getenv("FT_TOPO")), h(getenv("FT_LONELY")), h(getenv("FTAR_COST_MODEL"))};
   static_assert(sizeof k % 8 == 0, "cost params are doubles");
   memcpy(&cfg[10], &k, sizeof k);
+  if (failed) cfg[0] = ~uint64_t(0);  // this rank's bring-up failed: no peer can match it
   bool same = true;
   FTAR_RETURN_IF(c->tp->agree(cfg, sizeof cfg, &same));
+  if (failed) return FTAR_ERR_INTERNAL;
   if (!same) {
-    set_error("ranks disagree on FTAR_CHUNK_BYTES / FTAR_HOST_CHUNK_BYTES / FTAR_PEER_DIRECT / "
-              "FTAR_HOST_PEER_PIPELINE / FTAR_REDUCE_SCATTER / FTAR_ALLGATHER / FTAR_FORM / FT_TOPO / FT_LONELY / "
+    set_error("another rank's bring-up failed, or the ranks disagree on FTAR_CHUNK_BYTES / FTAR_HOST_CHUNK_BYTES / "
+              "FTAR_PEER_DIRECT / FTAR_HOST_PEER_PIPELINE / FTAR_REDUCE_SCATTER / FTAR_ALLGATHER / FTAR_FORM / FT_TOPO / FT_LONELY / "
               "the cost model or its constants: launch every rank with the same environment",
               __FILE__, __LINE__);
     return FTAR_ERR_INVALID_ARG;
   }
   return FTAR_SUCCESS;
+}
+
+// A communicator's first contact: the settings agreement, then (RCCL) one byte each way with every peer so
+// that RCCL's lazy p2p connection handshakes happen here and no later call's ncclGroupEnd blocks on one.
+// Where the transport may block the host in it (RCCL), it runs on a helper thread that the caller waits for
+// with a deadline, FTAR_FIRST_CONTACT_TIMEOUT_S (default 600 s; 0 = no helper, no deadline): a peer that
+// never shows up, or a transport stuck at its first transfer, then fails the call with FTAR_ERR_TIMEOUT
+// instead of hanging it (bench.py's RCCL preflight relies on it), and the communicator is
+// marked broken -- every later call fails the same way and teardown aborts the transport.
+ftar_status_t first_contact(ftar_comm* c) {
+  if (c->broken) {
+    set_error("this communicator's first contact timed out earlier: it is unusable (destroy it)", __FILE__, __LINE__);
+    return FTAR_ERR_TIMEOUT;
+  }
+  const char* e = getenv("FTAR_FIRST_CONTACT_TIMEOUT_S");
+  const double limit = e && *e ? atof(e) : 600.0;
+  auto run = [](ftar_comm* cc) {
+    ftar_status_t st = agree_settings(cc);
+    if (st == FTAR_SUCCESS) st = cc->tp->connect_peers(cc->rank);
+    return st;
+  };
+  if (!c->tp->first_contact_blocks() || limit <= 0) return run(c);
+  auto fc = std::make_shared<FirstContact>();
+  c->contact = fc;
+  c->contact_thread = std::thread([c, fc, run] {
+    hip_ignore(hipSetDevice(c->device));
+    const ftar_status_t st = run(c);
+    std::lock_guard<std::mutex> g(fc->mu);
+    fc->st = st;
+    fc->err = st == FTAR_SUCCESS ? "" : last_error();
+    fc->done = true;
+    fc->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(fc->mu);
+  if (!fc->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return fc->done; })) {
+    c->broken = true;
+    set_error("first contact of the RCCL communicator (settings all-gather, p2p connections) not complete after " +
+                  std::to_string(limit) + " s: a peer is missing or the transport is stuck; the communicator is "
+                  "unusable (FTAR_FIRST_CONTACT_TIMEOUT_S)",
+              __FILE__, __LINE__);
+    return FTAR_ERR_TIMEOUT;
+  }
+  const ftar_status_t st = fc->st;
+  const std::string err = fc->err;
+  lk.unlock();
+  c->contact_thread.join();
+  if (st != FTAR_SUCCESS) set_error("first contact: " + err, __FILE__, __LINE__);
+  return st;
 }
 
 // The topology of a call with topo == NULL, from the environment AT THIS CALL
@@ -338,8 +416,27 @@ static ftar_status_t env_topology(ftar_comm* c, bool* is_auto, Topology* out) {
   return FTAR_SUCCESS;
 }
 
-void comm_teardown(ftar_comm* c) {
+// false: the communicator must not be freed (its first contact's helper thread may still be inside the
+// transport after the abort; it is left behind with the memory it uses)
+bool comm_teardown(ftar_comm* c) {
   hip_ignore(hipSetDevice(c->device));
+  if (c->contact_thread.joinable()) {
+    if (c->broken && c->tp) c->tp->abort();  // ncclCommAbort: the stuck first contact returns with an error
+    bool done = false;
+    {
+      std::unique_lock<std::mutex> lk(c->contact->mu);
+      done = c->contact->cv.wait_for(lk, std::chrono::seconds(c->broken ? 10 : 600), [&] { return c->contact->done; });
+    }
+    if (!done) {
+      c->contact_thread.detach();
+      return false;
+    }
+    c->contact_thread.join();
+  }
+  if (c->broken) {  // the transport is aborted: nothing on its streams can be waited for
+    c->tp.reset();
+    return true;
+  }
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) hip_ignore(hipStreamSynchronize(st));
   if (c->tp) {
@@ -368,6 +465,7 @@ void comm_teardown(ftar_comm* c) {
   if (c->staging) hip_ignore(hipFree(c->staging));
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) hip_ignore(hipStreamDestroy(st));
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -775,6 +873,12 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   auto work = [&](auto&& fn) {
     if (st == FTAR_SUCCESS) st = fn();
   };
+  // a failed call leaves only after its copies stopped touching the caller's host buffers: H2D reads of
+  // io.src and D2H writes of io.dst may still be in flight on their streams
+  auto leave = [&]() -> ftar_status_t {
+    for (hipStream_t s : {c->h2d_s, c->d2h_s, c->comm_s}) hip_ignore(hipStreamSynchronize(s));
+    return st;
+  };
   auto sync = [&]() -> bool {  // a barrier; false: some rank failed, leave the call
     bool all_ok = true;
     const ftar_status_t b = tp->barrier_status(c->comm_s, st == FTAR_SUCCESS, &all_ok);
@@ -814,7 +918,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
     return FTAR_SUCCESS;
   });
-  if (!sync()) return st;  // piece 0 is in everywhere
+  if (!sync()) return leave();  // piece 0 is in everywhere
   work([&] { return mark(c, "piece 0 in", c->comm_s); });
   std::vector<Segment> segs;
   for (size_t k = 0; k < m; ++k) {
@@ -827,7 +931,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
       if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
       return FTAR_SUCCESS;
     });
-    if (!sync()) return st;  // piece k folded everywhere (and piece k+1 in)
+    if (!sync()) return leave();  // piece k folded everywhere (and piece k+1 in)
     work([&]() -> ftar_status_t {
       segs.clear();
       for (const Transfer& x : ag.recvs)
@@ -845,8 +949,8 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     });
   }
   work([&] { return mark(c, "pieces folded and gathered", c->comm_s); });
-  if (!sync()) return st;  // no peer reads my X after the call
-  FTAR_RETURN_IF(st);
+  if (!sync()) return leave();  // no peer reads my X after the call
+  if (st != FTAR_SUCCESS) return leave();
   FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
@@ -1087,8 +1191,9 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     bool is_auto = false;
     FTAR_RETURN_IF(topo ? to_topology(topo, c->nranks, &t) : env_topology(c, &is_auto, &t));
   }
+  if (c->broken) return first_contact(c);  // reports why
   if (!c->settings_agreed && !c->capturing) {  // an RCCL communicator's first call (see comm_setup); a
-    FTAR_RETURN_IF(agree_settings(c));          // 1-rank one too, which exercises the same all-gather
+    FTAR_RETURN_IF(first_contact(c));          // 1-rank one too, which exercises the same all-gather
     c->settings_agreed = true;
   }
   if (c->nranks == 1) {  // mpi_mod.hpp:1739-1746
@@ -1418,8 +1523,7 @@ ftar_status_t ftar_comm_init_local(ftar_comm_t* comms, int nranks, const int* de
 
 ftar_status_t ftar_comm_destroy(ftar_comm_t comm) {
   if (!comm) return FTAR_ERR_INVALID_ARG;
-  ftar::comm_teardown(comm);
-  delete comm;
+  if (ftar::comm_teardown(comm)) delete comm;  // else a stuck first contact still uses it: left behind
   return FTAR_SUCCESS;
 }
 
@@ -1433,6 +1537,8 @@ ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size) {
   *size = comm->nranks;
   return FTAR_SUCCESS;
 }
+const char* ftar_comm_transport(ftar_comm_t comm) { return comm && comm->tp ? comm->tp->name() : ""; }
+
 ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device) {
   if (!comm || !device) return FTAR_ERR_INVALID_ARG;
   *device = comm->device;

@@ -223,6 +223,16 @@ class Transport {
     *same = true;
     return FTAR_SUCCESS;
   }
+  // The first contact of a communicator (engine.cpp first_contact) may block the host inside the transport
+  // library (RCCL: the settings all-gather and the p2p connection handshakes): the engine then runs it on a
+  // helper thread it waits for with a deadline.  connect_peers makes every p2p connection now (collective);
+  // abort stops the transport's in-flight work for good (ncclCommAbort), so a stuck helper returns.
+  virtual bool first_contact_blocks() const { return false; }
+  virtual ftar_status_t connect_peers(int rank) {
+    (void)rank;
+    return FTAR_SUCCESS;
+  }
+  virtual void abort() {}
   // RCCL user-buffer registration (ncclCommRegister, a local call): lets RCCL move p2p data straight
   // between registered buffers where it can.  Returns a handle, or nullptr where the transport has no
   // such registration or RCCL refused it (the transfers then take RCCL's staging path, same bytes).

@@ -258,10 +258,48 @@ class RcclTransport final : public Transport {
  public:
   explicit RcclTransport(ncclComm_t c) : comm_(c) {
     if (ncclCommCount(comm_, &nranks_) != ncclSuccess || nranks_ < 1) nranks_ = 1;
+    // the agreement's buffer and stream exist before any agreement is attempted, so a rank never leaves
+    // its peers waiting in that collective because an allocation failed at its start
+    if (hipMalloc(&agree_buf_, kAgreeBytes * (size_t)(nranks_ + 1) + 2 * (size_t)nranks_) != hipSuccess ||
+        hipStreamCreateWithFlags(&agree_s_, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      agree_ready_ = false;
+    }
   }
   ~RcclTransport() override {
     if (comm_) ncclCommDestroy(comm_);
+    if (agree_s_) hip_ignore(hipStreamDestroy(agree_s_));
+    if (agree_buf_) hip_ignore(hipFree(agree_buf_));
     if (scratch_) hip_ignore(hipFree(scratch_));
+  }
+  bool first_contact_blocks() const override { return true; }
+  // one byte each way with every peer in one group, waited for: RCCL connects a p2p pair lazily, inside the
+  // ncclGroupEnd of its first ncclSend/ncclRecv, and that connection handshake blocks the host until the peer
+  // makes the same call (tools/rccl_order: two communicators whose first exchanges were issued in opposite
+  // orders hung there); done once at a communicator's first contact, no later call blocks on it
+  ftar_status_t connect_peers(int rank) override {
+    if (nranks_ < 2) return FTAR_SUCCESS;
+    if (!agree_ready_) {
+      set_error("RCCL transport: no agreement buffer (allocation at bring-up failed)", __FILE__, __LINE__);
+      return FTAR_ERR_NO_MEMORY;
+    }
+    char* base = static_cast<char*>(agree_buf_) + kAgreeBytes * (size_t)(nranks_ + 1);
+    bool ok = ncclGroupStart() == ncclSuccess;
+    for (int q = 0; q < nranks_ && ok; ++q)
+      if (q != rank)
+        ok = ncclSend(base + q, 1, ncclUint8, q, comm_, agree_s_) == ncclSuccess &&
+             ncclRecv(base + nranks_ + q, 1, ncclUint8, q, comm_, agree_s_) == ncclSuccess;
+    ok = ncclGroupEnd() == ncclSuccess && ok;
+    ok = ok && hipStreamSynchronize(agree_s_) == hipSuccess;
+    if (!ok) {
+      set_error("RCCL transport: connecting the peers (one byte each way) failed", __FILE__, __LINE__);
+      return FTAR_ERR_RCCL;
+    }
+    return FTAR_SUCCESS;
+  }
+  void abort() override {
+    if (comm_) ncclCommAbort(comm_);
+    comm_ = nullptr;
   }
   // a 4-byte all-reduce: complete on any rank's stream only once every rank's
   // stream has reached it
@@ -384,17 +422,17 @@ class RcclTransport final : public Transport {
   // every rank's bytes through one ncclAllGather on a private stream (host-blocking; communicator
   // bring-up only)
   ftar_status_t agree(const void* mine, size_t bytes, bool* same) override {
-    char* dev = nullptr;
-    FTAR_CHECK_ALLOC(hipMalloc(&dev, (size_t)(nranks_ + 1) * bytes));
+    if (bytes > kAgreeBytes || !agree_ready_) {
+      set_error("settings agreement: no agreement buffer, or more than 256 bytes to agree on", __FILE__, __LINE__);
+      return FTAR_ERR_INTERNAL;
+    }
+    char* dev = static_cast<char*>(agree_buf_);
     std::vector<char> all((size_t)nranks_ * bytes);
-    hipStream_t s = nullptr;
-    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-              hipMemcpyAsync(dev, mine, bytes, hipMemcpyHostToDevice, s) == hipSuccess &&
-              ncclAllGather(dev, dev + bytes, bytes, ncclUint8, comm_, s) == ncclSuccess &&
-              hipMemcpyAsync(all.data(), dev + bytes, all.size(), hipMemcpyDeviceToHost, s) == hipSuccess &&
-              hipStreamSynchronize(s) == hipSuccess;
-    if (s) hip_ignore(hipStreamDestroy(s));
-    hip_ignore(hipFree(dev));
+    const bool ok = hipMemcpyAsync(dev, mine, bytes, hipMemcpyHostToDevice, agree_s_) == hipSuccess &&
+                    ncclAllGather(dev, dev + kAgreeBytes, bytes, ncclUint8, comm_, agree_s_) == ncclSuccess &&
+                    hipMemcpyAsync(all.data(), dev + kAgreeBytes, all.size(), hipMemcpyDeviceToHost, agree_s_) ==
+                        hipSuccess &&
+                    hipStreamSynchronize(agree_s_) == hipSuccess;
     if (!ok) {
       set_error("settings agreement: the all-gather failed", __FILE__, __LINE__);
       return FTAR_ERR_RCCL;
@@ -405,6 +443,11 @@ class RcclTransport final : public Transport {
   }
 
  private:
+  static constexpr size_t kAgreeBytes = 256;
+  void* agree_buf_ = nullptr;  // one agreement per rank (all-gathered) + the connection bytes
+  hipStream_t agree_s_ = nullptr;
+  bool agree_ready_ = true;
+
   // sum of every rank's `mine` (host-blocking, on a private stream)
   ftar_status_t agree_failures(int mine, int* total) {
     int* word = reinterpret_cast<int*>(static_cast<char*>(scratch_) + 128);

@@ -3,9 +3,10 @@
 The data-parallel caller of the hot path: DDP packs gradients into buckets and hands each bucket to a hook
 once its gradients are ready; the hook below reduces the bucket in place with ftar_allreduce on the stream the
 backward pass runs on (the FlexTree schedule of FT_TOPO / FT_LONELY or `topo`, else the cost model; RCCL p2p
-over xGMI, the reduce kernel on ftar's own stream) and divides by the world size, which is what DDP's default
-allreduce hook returns.  No host synchronisation: the division and every later use of the bucket are ordered
-after the AllReduce by that stream.
+over xGMI, the reduce kernel on ftar's own stream); the bucket is divided by the world size first, as DDP's own
+allreduce hook does (so the mean rounds as DDP's does and keeps its overflow headroom).  No host
+synchronisation: the AllReduce and every later use of the bucket are ordered after the division by that
+stream.
 
     comm = ftar.dist.init_comm()                       # one rank per GPU, RCCL over the DDP process group's ids
     model = DistributedDataParallel(model, device_ids=[local_rank])
@@ -28,13 +29,14 @@ class HookState:
 
 
 def allreduce_hook(state, bucket):
-    """DDP comm hook: in-place FlexTree AllReduce of the bucket, then / world size; returns a completed future
-    whose tensor the reducer copies back into the gradients on the same stream."""
+    """DDP comm hook: the bucket / world size (first, as torch's default hook divides before it reduces), then
+    its in-place FlexTree AllReduce; returns a completed future whose tensor the reducer copies back into the
+    gradients on the same stream."""
     t = bucket.buffer()
     stream = torch.cuda.current_stream(t.device)
+    t.div_(state.comm.nranks)
     state.comm.allreduce(None, t, t.numel(), ftar._dt(str(t.dtype)), "sum", topo_=state.topo, lonely=state.lonely,
                          stream=stream)
-    t.div_(state.comm.nranks)
     state.calls += 1
     fut = torch.futures.Future(devices=[t.device])
     fut.set_result(t)

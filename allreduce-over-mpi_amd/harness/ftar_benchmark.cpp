@@ -22,7 +22,8 @@
 //                     recycles the handles), one exact integer-valued
 //                     MPI_Allreduce_FT on each;
 //   --comm-threads T  T duplicates driven at once from T threads
-//                     (MPI_THREAD_MULTIPLE), 3 exact calls each;
+//                     (MPI_THREAD_MULTIPLE), 3 exact calls each; refused (exit 2)
+//                     on the RCCL transport, which cannot order them;
 //   --register-check  MPI_Allreduce_FT_register / _unregister semantics on a
 //                     scratch buffer (needs a GPU: hipHostRegister).
 // --check is two-sided here: the reference only flags results that are too
@@ -317,7 +318,24 @@ int main(int argc, char** argv) {
     }
     lifecycle_bad += bad_c;
   }
+  // RCCL communicators driven from several threads at once are refused: RCCL itself deadlocks when two
+  // communicators' operations reach the GPU in different orders on different ranks -- at their first
+  // exchange inside ncclGroupEnd (its lazy connection handshake), and with the connections made, on the
+  // device (tools/rccl_order, profiles/r04/rccl_order/) -- NCCL's rule for concurrent communicators
+  const char* world_tp = "";
   if (comm_threads > 0 && comm_type == "flextree") {
+    ftar_comm_t fc = nullptr;
+    if (MPI_Allreduce_FT_comm(MPI_COMM_WORLD, &fc) == MPI_SUCCESS && fc) world_tp = ftar_comm_transport(fc);
+  }
+  if (comm_threads > 0 && comm_type == "flextree" && !strcmp(world_tp, "rccl")) {
+    if (rank == 0)
+      printf("COMM_THREADS refused: the RCCL transport cannot drive communicators from %d threads at once -- "
+             "RCCL deadlocks when operations on different communicators reach the GPU in different orders on "
+             "different ranks (NCCL's rule for concurrent communicators; profiles/r04/rccl_order/); issue "
+             "them in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n", comm_threads);
+    fflush(stdout);
+    lifecycle_bad += 1;
+  } else if (comm_threads > 0 && comm_type == "flextree") {
     if (provided < MPI_THREAD_MULTIPLE) {
       if (rank == 0) printf("COMM_THREADS skipped: MPI provides thread level %d\n", provided);
     } else {

@@ -143,6 +143,9 @@ def cpu_baseline(k, n, seconds):
                                  capture_output=True, text=True, timeout=seconds * 6 + 120, check=True).stdout
             d = json.loads(out.strip().splitlines()[-1])
             return {"value": round(d["GBps_best"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+                    "median": round(d["GBps_median"], 3), "mean": round(d["GBps_mean"], 3), "samples": d["iters"],
+                    "statistic": "value = the best call (the reference harness's min time, benchmark.cpp:229-240); "
+                                 "median and mean of the same calls beside it; the shared host spreads them widely",
                     "cores_available": hc,
                     "sample": f"FlexTree::reduce_sum<float> k={k} n={n} fp32, best of {d['iters']} calls in ~{seconds:.0f}s "
                               f"(mean {d['GBps_mean']:.2f} GB/s); {d['threads']} OpenMP threads (mpi_mod.hpp:820) on "
@@ -156,13 +159,16 @@ def cpu_baseline(k, n, seconds):
     m = min(n, 1 << 24)
     xs = [fi.fill("f32", 0x5EED, j, m) for j in range(k)]
     out = np.empty(m, np.float32)
-    best, iters, t_end = 1e30, 0, time.time() + seconds
-    while time.time() < t_end or iters == 0:
+    times, t_end = [], time.time() + seconds
+    while time.time() < t_end or not times:
         t0 = time.perf_counter()
         oracle_lib.reduce(6, 0, xs, out=out)
-        best = min(best, time.perf_counter() - t0)
-        iters += 1
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    best, med, iters = times[0], times[len(times) // 2], len(times)
     return {"value": round((k + 1) * m * 4 / best / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "median": round((k + 1) * m * 4 / med / 1e9, 3), "samples": iters,
+            "statistic": "value = the best call; median beside it",
             "cores_available": hc,
             "sample": f"oracle reduce k={k} n={m} fp32 single thread, best of {iters}"}
 
@@ -451,6 +457,153 @@ def rccl_p2p_best(sweep, world, gpus, bucket, links_of):
                     "min(5, steps) calls after 1 warmup)"}
 
 
+def sweep_form(form):
+    """A sweep entry's form as the execution model prices it: (form name, registered) -- tuning suffixes
+    (":cus224", ":ncclreg", ":plain", ":vec", ":dma", ":wgN") move the same bytes and are priced as their base
+    form; "-reg" marks the peer forms on registered buffers (no local pass)."""
+    base = form.split(":")[0]
+    return (base[:-4], True) if base.endswith("-reg") else (base, False)
+
+
+def predict_ms(ftar, topology, form, chunk, world, bucket):
+    """The execution model's predicted ms for one sweep entry under the constants set now; None where it
+    cannot price it (an unmeasured rate)."""
+    name, reg = sweep_form(form)
+    if name not in ftar.FORM:
+        return None
+    v = ftar.cost_predict("1" if topology == "ring" else topology, name, chunk, world, bucket, reg)
+    return None if v is None else round(v * 1e3, 4)
+
+
+def pieces_per_round(chunk, world, bucket, esz):
+    """Pipeline pieces per round of one block (the engine's rule: chunk rounded down to 64 elements;
+    0 = whole blocks)."""
+    split = -(-(bucket // esz) // world)
+    if not chunk:
+        return 1
+    c = max(64, (chunk // esz) & ~63)
+    return max(1, -(-split // c))
+
+
+def issue_from_enqueue(sweep, world, bucket, esz):
+    """The host's enqueue time of one piece of one round (us): the median over the sweep's one-round RCCL
+    entries of the time ftar_allreduce took to return (`enqueue_ms`) divided by the groups it issued
+    (2 rounds x pieces).  None without such entries."""
+    per = []
+    for r in sweep:
+        if r.get("form") == "direct" and r.get("enqueue_ms") and r.get("check") == "ok":
+            groups = 2 * pieces_per_round(r["chunk_bytes"], world, bucket, esz)
+            per.append(r["enqueue_ms"] * 1e3 / groups)
+    if not per:
+        return None
+    per.sort()
+    return per[len(per) // 2]
+
+
+def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
+    """The execution model's p2p constants re-fitted to this run's own sweep: alpha (one p2p
+    group), link (one peer, one direction) and issue (host enqueue of one piece) minimise the squared log
+    error of the model's prediction over the validated RCCL p2p entries (forms direct / stages, no tuning
+    suffix; several topologies and piece sizes), by a log-grid search refined twice around its best point.
+    `fixed` names constants measured directly (e.g. {"issue_us": ...}) that the search keeps.  Leaves the
+    model on the best constants found and returns {"params", "entries", "rms_log_err"} (None: < 3 entries)."""
+    import math
+    pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in ("direct", "stages")]
+    if len(pts) < 3:
+        return None
+    base = ftar.cost_get()
+    fixed = {k: v for k, v in (fixed or {}).items() if v}
+
+    def err(alpha, link, issue):
+        ftar.cost_set(**dict(base, **dict(dict(alpha_us=alpha, link_gbps=link, issue_us=issue), **fixed)))
+        s = 0.0
+        for r in pts:
+            p = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
+            if p is None or p <= 0:
+                return float("inf")
+            s += math.log(p / r["ms"]) ** 2
+        return s
+
+    def geom(lo, hi, n):
+        return [lo * (hi / lo) ** (i / (n - 1)) for i in range(n)]
+
+    grids = {"alpha_us": geom(0.5, 5000.0, 11), "link_gbps": geom(1.0, 1000.0, 13), "issue_us": geom(0.5, 5000.0, 11)}
+    if "issue_us" in fixed:
+        grids["issue_us"] = [fixed["issue_us"]]
+    best = (float("inf"), None)
+    for a_ in grids["alpha_us"]:
+        for l_ in grids["link_gbps"]:
+            for i_ in grids["issue_us"]:
+                e = err(a_, l_, i_)
+                if e < best[0]:
+                    best = (e, [a_, l_, i_])
+    if best[1] is None:
+        ftar.cost_set(**base)
+        return None
+    # pattern search in log space from the grid's best point: a step that improves is taken, none improving
+    # halves the steps, down to 1 %
+    x, fx = list(best[1]), best[0]
+    steps = [math.log(2.5), math.log(1.8), 0.0 if "issue_us" in fixed else math.log(2.5)]
+    lo, hi = (0.1, 0.5, 0.1), (1e5, 5e3, 1e5)   # us, GB/s, us
+    while max(steps) > math.log(1.01):
+        moved = False
+        for d in range(3):
+            for sgn in (1, -1):
+                if not steps[d]:
+                    continue
+                y = list(x)
+                y[d] = min(hi[d], max(lo[d], x[d] * math.exp(sgn * steps[d])))
+                fy = err(*y)
+                if fy < fx:
+                    x, fx, moved = y, fy, True
+                    break
+        if not moved:
+            steps = [s_ / 2 for s_ in steps]
+    best = (fx, x)
+    a0, l0, i0 = best[1]
+    params = ftar.cost_set(**dict(base, **dict(dict(alpha_us=a0, link_gbps=l0, issue_us=i0), **fixed)))
+    return {"params": {k: round(v, 3) for k, v in params.items()}, "entries": len(pts),
+            "rms_log_err": round(math.sqrt(best[0] / len(pts)), 4)}
+
+
+def refit_form_rate(ftar, sweep, world, bucket, field, forms):
+    """One more constant of the execution model fitted to this run's sweep: the rate `field` (peer_read_gbps,
+    peer_write_gbps or coll_gbps) that minimises the squared log error over the validated entries whose form
+    is in `forms` (a 1-D golden-section search in log space, 1 .. 5000 GB/s).  Leaves the model on it;
+    returns {"value", "entries", "rms_log_err"} or None (no entries)."""
+    import math
+    pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in forms]
+    if not pts:
+        return None
+    base = ftar.cost_get()
+
+    def err(lx):
+        ftar.cost_set(**dict(base, **{field: math.exp(lx)}))
+        e = 0.0
+        for r in pts:
+            p = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
+            if p is None or p <= 0:
+                return float("inf")
+            e += math.log(p / r["ms"]) ** 2
+        return e
+    a, b = math.log(1.0), math.log(5000.0)
+    g = (math.sqrt(5) - 1) / 2
+    c, d = b - g * (b - a), a + g * (b - a)
+    fc, fd = err(c), err(d)
+    while b - a > 1e-3:
+        if fc < fd:
+            b, d, fd = d, c, fc
+            c = b - g * (b - a)
+            fc = err(c)
+        else:
+            a, c, fc = c, d, fd
+            d = a + g * (b - a)
+            fd = err(d)
+    lx = (a + b) / 2
+    e = err(lx)
+    return {"value": round(math.exp(lx), 3), "entries": len(pts), "rms_log_err": round(math.sqrt(e / len(pts)), 4)}
+
+
 def _factorizations(n):
     out = []
 
@@ -589,7 +742,9 @@ def bench_distributed(a):
             a.host_comm = True
     if comm is None:
         comm = ftar.dist.init_host_comm(device=local)
-    base_form = "peer-read" if a.host_comm else "direct"   # the default configuration's data movement
+    # the default configuration's data movement: the execution model's choice per call ("auto"); a
+    # host-bootstrapped communicator moves data by the peer forms only
+    base_form = "peer-read" if a.host_comm else "auto"
     n = a.n or (1 << 28)
     esz = ftar.dtype_size(a.dtype)
     tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
@@ -611,18 +766,33 @@ def bench_distributed(a):
 
     def preflight(timeout_s):
         """First contact of RCCL p2p between the ranks: one small call of the default configuration, waited
-        for with a deadline (an event polled from the host), so a transfer that never completes becomes the
-        IPC fallback below instead of a run the watchdog cuts with nothing measured.  Returns "" or why not."""
+        for with a deadline, so a transfer that never completes becomes the IPC fallback below instead of a
+        run the watchdog cuts with nothing measured.  The call itself is bounded too: its first contact (the
+        settings all-gather and RCCL's p2p connections, which block the host) runs under
+        FTAR_FIRST_CONTACT_TIMEOUT_S = timeout_s and fails with FTAR_ERR_TIMEOUT instead of hanging
+        (ADVICE r3).  FTAR_BENCH_PREFLIGHT_HANG=1 rehearses the path with a stream that really does not drain
+        (a spinning wave, libftar_bench.so, released at the end of the run).  Returns "" or why not."""
         npf = min(n, 1 << 20)
+        os.environ["FTAR_FIRST_CONTACT_TIMEOUT_S"] = str(timeout_s)
         try:
             comm.chunk_bytes = default_chunk
             comm.peer_direct, comm.allgather, comm.reduce_scatter = 0, "direct", "direct"
-            comm.allreduce(x[:npf], y[:npf], npf, a.dtype, "sum", topo_=default_topo, stream=stream)
+            try:
+                comm.allreduce(x[:npf], y[:npf], npf, a.dtype, "sum", topo_=default_topo, stream=stream)
+            except ftar.FtarError as e:
+                if e.status == 7:   # FTAR_ERR_TIMEOUT: the first contact never completed
+                    return f"RCCL preflight ({npf} elements) not complete after {timeout_s:.0f}s: {str(e)[:160]}"
+                raise
+            if os.environ.get("FTAR_BENCH_PREFLIGHT_HANG"):   # rehearsal: this stream now really never drains
+                import ctypes
+                lib = ftar.bench_lib()
+                lib.ftar_debug_block_stream.restype = ctypes.c_void_p
+                lib.ftar_debug_block_stream.argtypes = [ctypes.c_void_p, ctypes.c_double]
+                state["blocked_flag"] = lib.ftar_debug_block_stream(stream.cuda_stream, 3 * timeout_s + 60)
             ev = torch.cuda.Event()
             ev.record(stream)
+            state["preflight_ev"] = ev
             t_end = time.time() + timeout_s
-            if os.environ.get("FTAR_BENCH_PREFLIGHT_HANG"):   # rehearses the hang path (nothing hangs)
-                return f"RCCL preflight ({npf} elements) not complete after {timeout_s:.0f}s (simulated)"
             while not ev.query():
                 if time.time() > t_end:
                     return f"RCCL preflight ({npf} elements) not complete after {timeout_s:.0f}s"
@@ -631,23 +801,42 @@ def bench_distributed(a):
         except Exception as e:  # noqa: BLE001
             return f"RCCL preflight failed: {str(e)[:180]}"
 
+    def unblock():
+        """the rehearsal's spinning wave (FTAR_BENCH_PREFLIGHT_HANG), released so the device drains"""
+        if state.get("blocked_flag"):
+            import ctypes
+            lib = ftar.bench_lib()
+            lib.ftar_debug_unblock.argtypes = [ctypes.c_void_p]
+            lib.ftar_debug_unblock(state.pop("blocked_flag"))
+
+    enq = {"ms": None}   # the last timed() run's host enqueue time per call (median, max over ranks)
+
     def timed(fn, steps, warmup):
-        """barrier + sync on both sides of `steps` calls; max over ranks (ms per call)."""
+        """barrier + sync on both sides of `steps` calls; max over ranks (ms per call).  Also the host time
+        each call took to return (ftar_allreduce returns once everything is enqueued): its median, max over
+        ranks, in enq["ms"] -- the enqueue cost the execution model's `issue` constant prices."""
         for _ in range(warmup):
             fn()
         sync()
         dist.barrier()
         sync()
+        per = []
         t0 = time.perf_counter()
         for _ in range(steps):
+            t1 = time.perf_counter()
             fn()
+            per.append(time.perf_counter() - t1)
         sync()
         dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        per.sort()
+        t = torch.tensor([time.perf_counter() - t0, per[len(per) // 2] if per else 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return t.item() / max(1, steps) * 1e3
+        enq["ms"] = round(t[1].item() * 1e3, 4)
+        return t[0].item() / max(1, steps) * 1e3
 
     def run_with(topo, chunk, form="direct"):
+        # form "auto": the execution model's form per call (and its piece where chunk is 0); the topology
+        # is `topo`, or the model's too when topo is None
         # peer-form tuning suffix: ":plain" = plain (not nontemporal) copies, ":vec" = register-kernel fold,
         # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
@@ -664,10 +853,13 @@ def bench_distributed(a):
         kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
         no local pass)."""
         comm.chunk_bytes = chunk
-        peer = form.startswith("peer-")
-        comm.peer_direct = form.split("-")[1] if peer else 0
-        comm.allgather = "direct" if peer else form
-        comm.reduce_scatter = "stages" if form == "stages" else "direct"
+        if form == "auto":
+            comm.form = "auto"
+        else:
+            peer = form.startswith("peer-")
+            comm.peer_direct = form.split("-")[1] if peer else 0
+            comm.allgather = "direct" if peer else form
+            comm.reduce_scatter = "stages" if form == "stages" else "direct"
         xin, yout = (reg_bufs() if form.endswith("-reg") or tune == "ncclreg" else (x, y))
 
         def fn():
@@ -687,31 +879,114 @@ def bench_distributed(a):
         return reg["x"], reg["y"]
 
     def fit_cost_model(probe):
-        """The xGMI cost model's constants from this node: link = the probe's per-link,
-        per-direction rate; alpha = half the time of a 4 KiB direct-form AllReduce (two p2p rounds, no
-        bandwidth term to speak of).  Set process-wide (ftar_cost_set_params) on every rank alike, so the
-        C5 line item and every later choice use them; reported next to the defaults and to the reference
-        model's own choice (CostModel.h, chunk 100)."""
-        default = ftar.cost_params()
+        """The execution model's constants from this node's probe, before the sweep prices
+        anything: link = the probe's per-link, per-direction copy rate; peer read / write = the probe's
+        read / write from all peers per link (so the peer forms become candidates); alpha = half a 4 KiB
+        direct-form AllReduce (two p2p rounds, no bandwidth term to speak of); barrier = a third of a 4 KiB
+        peer-read call (three barriers).  Set process-wide on every rank alike (rank 0's values broadcast),
+        so every later choice uses them; the sweep then re-fits the p2p constants to its own timings."""
+        default = ftar.cost_get()
         link = link_rate_from_probe(probe, world)
+
+        def per_link(key):
+            v = (probe or {}).get(key)
+            v = v[0] if isinstance(v, (list, tuple)) else v
+            return v / max(1, world - 1) if isinstance(v, (int, float)) and v > 0 else 0.0
         small = torch.zeros(1024, device=dev)
         small_y = torch.empty_like(small)
         comm.peer_tuning()
+        comm.chunk_bytes = 0
         comm.peer_direct = "read" if base_form.startswith("peer-") else 0   # host-bootstrapped: peer forms only
         comm.allgather, comm.reduce_scatter = "direct", "direct"
-        ms_small = timed(lambda: comm.allreduce(small, small_y, 1024, "f32", "sum", topo_=ftar.topo(str(world)),
-                                                stream=stream), 20, 3)
-        v = torch.tensor([link or 0.0, ms_small], dtype=torch.float64)
+        t_small = ftar.topo(str(world))
+        ms_small = timed(lambda: comm.allreduce(small, small_y, 1024, "f32", "sum", topo_=t_small, stream=stream),
+                         20, 3)
+        comm.peer_direct = "read"
+        ms_peer = timed(lambda: comm.allreduce(small, small_y, 1024, "f32", "sum", topo_=t_small, stream=stream),
+                        20, 3)
+        v = torch.tensor([link or 0.0, ms_small, ms_peer, per_link("read_all_peers"), per_link("write_all_peers")],
+                         dtype=torch.float64)
         dist.broadcast(v, 0)  # one set of constants on every rank: identical choices everywhere
-        link, ms_small = (v[0].item() or None), v[1].item()
-        fitted = ftar.cost_params(alpha_us=ms_small * 1e3 / 2, link_gbps=link or 0.0)
+        link, ms_small, ms_peer, pr, pw = (x.item() for x in v)
+        fitted = ftar.cost_set(**dict(default, alpha_us=ms_small * 1e3 / 2, link_gbps=link or 0.0,
+                                      barrier_us=ms_peer * 1e3 / 3, peer_read_gbps=pr, peer_write_gbps=pw))
         t_ref, _ = ftar.topo_choose_reference(world)
         return {"default": {k: round(x, 3) for k, x in default.items()},
                 "fitted": {k: round(x, 3) for k, x in fitted.items()},
-                "source": "link: ftar_xgmi_probe best per-link one-direction rate (rank 0); alpha: half a 4 KiB "
-                          "direct AllReduce" + ("" if link else "; probe gave no link rate: default link kept"),
-                "choice_fitted": str(ftar.topo_choose(world, bucket)),
+                "source": "link, peer read/write: ftar_xgmi_probe per-link one-direction rates (rank 0); alpha: "
+                          "half a 4 KiB direct AllReduce; barrier: a third of a 4 KiB peer-read call"
+                          + ("" if link else "; probe gave no link rate: default link kept"),
+                "choice_fitted": ftar.exec_choose(world, bucket).as_dict(),
                 "choice_reference_model": str(t_ref)}
+
+    def validate_model(sweep):
+        import math
+        keys = list(ftar.cost_get())
+        before = ftar.cost_get()
+        for r in sweep:
+            if "ms" in r:
+                r["model_ms"] = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
+
+        def log_err(field):
+            e = [abs(math.log(r[field] / r["ms"])) for r in sweep
+                 if r.get("check") == "ok" and r.get(field) and r.get("ms")]
+            e.sort()
+            return {"median_abs_log_err": round(e[len(e) // 2], 4) if e else None, "entries": len(e)}
+        issue = issue_from_enqueue(sweep, world, bucket, esz)
+        p2p = refit_cost_model(ftar, sweep, world, bucket, fixed={"issue_us": issue} if issue else None)
+        rates = {f: refit_form_rate(ftar, sweep, world, bucket, f, forms)
+                 for f, forms in (("peer_read_gbps", ("peer-read", "peer-read-reg")),
+                                  ("peer_write_gbps", ("peer-write", "peer-write-reg")),
+                                  ("coll_gbps", ("collective",)))}
+        v = torch.tensor([ftar.cost_get()[k] for k in keys], dtype=torch.float64)
+        dist.broadcast(v, 0)   # one set of constants on every rank: identical choices everywhere
+        refit = ftar.cost_set(**dict(zip(keys, v.tolist())))
+        for r in sweep:
+            if "ms" in r:
+                r["model_ms_refit"] = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
+        ok = [r for r in sweep if r.get("check") == "ok" and "ms" in r]
+        best = min(ok, key=lambda r: r["ms"]) if ok else None
+        fixed = default_topo if (a.topo or os.environ.get("FT_TOPO")) else None
+        if a.host_comm:   # no p2p transfers: the model chooses between the peer forms only
+            cands = []
+            for f in ("peer-read", "peer-write"):
+                try:
+                    cands.append(ftar.exec_choose(world, bucket, topo_=fixed or default_topo, form=f, chunk_bytes=0))
+                except ftar.FtarError:   # that form's rate is unmeasured (the probe did not run)
+                    pass
+            if not cands:
+                return {"constants_probe": before, "note": "no peer-form rate measured: nothing to choose"}
+            ch = min(cands, key=lambda c: c.seconds).as_dict()
+        else:
+            ch = ftar.exec_choose(world, bucket, topo_=fixed, chunk_bytes=a.chunk_bytes or None,
+                                  peer=True).as_dict()
+        ch_chunk = ch["chunk_bytes"] or -(-n // world) * esz
+        same = [r for r in ok if r["topology"] == ch["topology"] and r["form"] == ch["form"] and
+                pieces_per_round(r["chunk_bytes"], world, bucket, esz) ==
+                pieces_per_round(ch_chunk, world, bucket, esz)]
+        if same:
+            measured = min(r["ms"] for r in same)
+        else:   # not in the sweep: time it (validated like every entry)
+            fn = run_with(ftar.topo("1" if ch["topology"] == "ring" else ch["topology"]),
+                          0 if ch["form"].startswith("peer") else ch_chunk, ch["form"])
+            measured = timed(fn, steps=min(5, a.steps), warmup=1)
+            okc, whyc = check_y(fn)
+            sweep.append({"topology": ch["topology"], "chunk_bytes": ch_chunk, "form": ch["form"],
+                          "ms": round(measured, 4), "busbw_GBps": round(bws(measured)[1], 2), "enqueue_ms": enq["ms"],
+                          "check": "ok" if okc else f"MISMATCH ({whyc})", "source": "the refit model's choice",
+                          "model_ms_refit": round(ch["predicted_ms"], 4)})
+            if not okc:
+                measured = None
+        return {"constants_probe": {k: round(x, 3) for k, x in before.items()},
+                "constants_refit": {k: round(x, 3) for k, x in refit.items()},
+                "refit_p2p": p2p, "refit_rates": rates, "issue_us_from_enqueue": issue,
+                "prediction_error_probe": log_err("model_ms"), "prediction_error_refit": log_err("model_ms_refit"),
+                "choice_refit": ch, "choice_refit_measured_ms": None if measured is None else round(measured, 4),
+                "sweep_best": None if best is None else {k: best[k] for k in ("topology", "form", "chunk_bytes", "ms")},
+                "regret_refit": None if (measured is None or best is None) else round(measured / best["ms"] - 1, 4),
+                "note": "model_ms (per sweep entry): the prediction under the probe-fitted constants; model_ms_refit: "
+                        "under the constants re-fitted to this sweep; regret = the refit choice's measured ms over "
+                        "the sweep's best, minus 1"}
 
     # correctness of y: identical on every rank, and within (P-1) * eps * sum|x| of the fp64 sum on a sample
     idx = sample_index(n, dev)
@@ -757,19 +1032,27 @@ def bench_distributed(a):
         return bits == 0, why
 
     def measure_c5():
+        """BASELINE configs[4]: the bf16 1 GiB bucket with the cost model's width -- topology, form and piece
+        all the execution model's (FT_TOPO / --topo fix the topology), then every other width the model
+        weighed, each with the form and piece the model gives it, timed against its prediction."""
         nb = a.n_c5 or (1 << 29)
         xb = (torch.rand(nb, generator=gen, device=dev, dtype=torch.float32) * 2 - 1).to(torch.bfloat16)
         yb = torch.empty_like(xb)
-        t5 = ftar.topo(a.topo, a.lonely, nranks=world) if a.topo else ftar.topo_from_env(world, nb * 2)
-        comm.chunk_bytes = default_chunk
+        fixed = ftar.topo(a.topo, a.lonely, nranks=world) if a.topo else None   # None: FT_TOPO, else the model
+        comm.chunk_bytes = a.chunk_bytes
         comm.rccl_register = False
-        comm.peer_direct = "read" if a.host_comm else 0
-        comm.allgather = "direct"
-        comm.reduce_scatter = "direct"
+        comm.peer_tuning()
+        comm.reduce_cus = 0
+        if a.host_comm:
+            comm.peer_direct = "read"
+        else:
+            comm.form = "auto"
 
         def fn5():
-            comm.allreduce(xb, yb, nb, "bf16", "sum", topo_=t5, stream=stream)
+            comm.allreduce(xb, yb, nb, "bf16", "sum", topo_=fixed, stream=stream)
         ms5 = timed(fn5, min(a.steps, 10), 2)
+        chosen = comm.last_exec()
+        t5 = ftar.topo("1" if chosen["topology"] == "ring" else chosen["topology"])
         # validation: every rank identical; within one bf16 rounding per fold level (at most P) of the fp64 sum
         ix = sample_index(nb, dev)
         xs5 = xb[ix].double().cpu()
@@ -784,7 +1067,7 @@ def bench_distributed(a):
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         alg5 = nb * 2 / (ms5 * 1e-3) / 1e9
         # the other widths the cost model weighed (every ordered factorization of P, and the ring), a few
-        # timed calls each with the same data movement: does its choice hold on this node?
+        # timed calls each with the form and piece the model gives them: does its choice hold on this node?
         widths = {}
         for tp in ["1"] + [",".join(map(str, f)) for f in _factorizations(world)]:
             tw = ftar.topo(tp)
@@ -792,19 +1075,22 @@ def bench_distributed(a):
                 continue
             try:
                 mw = timed(lambda: comm.allreduce(xb, yb, nb, "bf16", "sum", topo_=tw, stream=stream), 3, 1)
-                widths[str(tw)] = {"ms": round(mw, 4), "cost_model_s": round(ftar.topo_cost(tw, world, nb * 2), 6)}
+                ex = comm.last_exec()
+                widths[str(tw)] = {"ms": round(mw, 4), "form": ex["form"], "chunk_bytes": ex["chunk_bytes"],
+                                   "model_ms": None if ex["predicted_ms"] is None else round(ex["predicted_ms"], 4)}
             except Exception as e:  # noqa: BLE001
                 widths[str(tw)] = {"error": str(e)[:120]}
         del xb, yb
         return {"workload": f"{world}xMI355X FlexTree AllReduce, bf16 2^{nb.bit_length() - 1} elements per rank "
-                            "(BASELINE configs[4])", "topology": str(t5), "form": base_form,
-                "chunk_bytes": default_chunk, "ms": round(ms5, 4), "value_GBps": round(world * alg5, 2),
+                            "(BASELINE configs[4])", "topology": str(t5), "form": chosen["form"],
+                "chunk_bytes": chosen["chunk_bytes"], "ms": round(ms5, 4), "value_GBps": round(world * alg5, 2),
                 "algbw_GBps_per_rank": round(alg5, 2),
                 "busbw_GBps_per_rank": round(alg5 * 2 * (world - 1) / world if world > 1 else alg5, 2),
                 "check": "ok" if bool(flag.item()) else "MISMATCH",
-                "cost_model_s": round(ftar.topo_cost(t5, world, nb * 2), 6),
-                "cost_model_params": ftar.cost_params(),
-                "cost_model_choice_now": str(ftar.topo_choose(world, nb * 2)),
+                "model_ms": None if chosen["predicted_ms"] is None else round(chosen["predicted_ms"], 4),
+                "selection": "FT_TOPO / --topo" if (fixed is not None or os.environ.get("FT_TOPO"))
+                             else "the execution model (topology, form, piece)",
+                "cost_model_params": ftar.cost_get(),
                 "reference_model_choice": str(ftar.topo_choose_reference(world)[0]),
                 "other_widths": widths}
 
@@ -879,11 +1165,25 @@ def bench_distributed(a):
 
     # 1. the default configuration: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model
     phase("default")
+    # the default configuration is the execution model's: FT_TOPO / --topo fix the topology,
+    # --chunk-bytes the piece; the rest -- topology, form, piece -- comes from the model under its default
+    # constants (no rate of this node is known yet, so the peer forms are not candidates)
     if a.topo:
         default_topo = ftar.topo(a.topo, a.lonely, nranks=world)
-    else:
+    elif os.environ.get("FT_TOPO") or os.environ.get("FT_LONELY", "0") not in ("", "0"):
         default_topo = ftar.topo_from_env(world, bucket)
-    default_chunk = a.chunk_bytes or comm.chunk_bytes
+    else:
+        default_topo = ftar.exec_choose(world, bucket, chunk_bytes=a.chunk_bytes or None).topo
+    default_chunk = a.chunk_bytes   # 0: the model's piece, per call
+
+    def model_chunk(t, form):
+        """the model's piece for (topology, form) under the constants set now, as explicit bytes (a whole
+        block when the model takes whole blocks)"""
+        try:
+            c = ftar.exec_choose(world, bucket, topo_=t, form=form).chunk_bytes
+        except ftar.FtarError:   # a form whose rate is unmeasured (the collective): its reduce-scatter's piece
+            c = ftar.exec_choose(world, bucket, topo_=t, form="direct").chunk_bytes
+        return c or -(-n // world) * esz
     err = ""
     hung = False
     if not a.host_comm:
@@ -892,8 +1192,12 @@ def bench_distributed(a):
         hung = "not complete" in err
         flag = torch.tensor([1 if hung else 0], dtype=torch.int32)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-        if flag.item():   # some rank's RCCL work may never finish: never wait on the whole device again
+        if flag.item():   # some rank's RCCL work may never finish: never wait on the whole device again,
             sync_state["device"] = False
+            # and leave its stream: everything from here on (ftar calls, torch ops, sync()) runs on a fresh
+            # one, so nothing queues behind the call that never completed
+            stream = torch.cuda.Stream(device=dev)
+            torch.cuda.set_stream(stream)
         phase("default")
     try:
         if err:
@@ -920,15 +1224,22 @@ def bench_distributed(a):
         a.host_comm = True
         comm = ftar.dist.init_host_comm(device=local)
         base_form = "peer-read"
-        default_chunk = a.chunk_bytes or comm.chunk_bytes
+        default_chunk = a.chunk_bytes
         fn_default = run_with(default_topo, default_chunk, base_form)
         ms_default = timed(fn_default, a.steps, a.warmup)
         ok_default, why_default = check_y(fn_default)
+    if state.get("preflight_ev") is not None and not sync_state["device"]:
+        # the rehearsal's proof that the fallback ran beside the stuck stream, not behind it
+        state["stuck_stream_still_blocked"] = not state["preflight_ev"].query()
+    ran = comm.last_exec()   # what the model chose for the default configuration (form "auto")
     default_info = {"topology": str(default_topo), "chunk_bytes": default_chunk, "form": base_form,
-                    "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
-                    "check": "ok" if ok_default else f"MISMATCH ({why_default})"}
+                    "ran": ran, "ms": round(ms_default, 4), "busbw_GBps": round(bws(ms_default)[1], 2),
+                    "enqueue_ms": enq["ms"], "check": "ok" if ok_default else f"MISMATCH ({why_default})"}
     state["line"] = make_result(ms_default, default_topo, default_chunk, base_form, ok_default, a.steps, a.warmup,
                                 {"config_selection": "default (sweep not reached)", "default_config": default_info})
+    if "stuck_stream_still_blocked" in state:
+        state["line"]["fallback_stream"] = {"fresh": True,
+                                            "stuck_stream_still_blocked": state["stuck_stream_still_blocked"]}
 
     # 2. the sweep: every factorization of P and the ring x chunk sizes x form, in tiers (below)
     phase("sweep")
@@ -945,18 +1256,19 @@ def bench_distributed(a):
         if a.host_comm:  # the host-bootstrapped communicator has no p2p transfers: the peer forms only
             forms = []
         for form in forms:
-            chunks = {4 << 20, 16 << 20, 64 << 20, default_chunk}
+            mc = model_chunk(t, form)   # the model's piece for this topology and form (default constants)
+            chunks = {4 << 20, 16 << 20, 64 << 20, mc}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
-                plan.append((t, default_chunk, "direct:cus224"))
-                plan.append((t, default_chunk, "direct:ncclreg"))
+                plan.append((t, mc, "direct:cus224"))
+                plan.append((t, mc, "direct:ncclreg"))
             if form == "stages" and t.ring:
-                chunks = {default_chunk}  # the reference's ring rounds: one point is enough
+                chunks = {mc}  # the reference's ring rounds: one point is enough
             plan += [(t, chunk, form) for chunk in sorted(chunks)]
         if not a.no_peer and t.lonely == 0:  # no pieces: whole-block kernels
-            plan += [(t, default_chunk, f) for f in ("peer-read", "peer-write", "peer-read-reg", "peer-write-reg")]
+            plan += [(t, 0, f) for f in ("peer-read", "peer-write", "peer-read-reg", "peer-write-reg")]
             if key == str(default_topo):  # copy policy and fold kernel over xGMI (same bits)
-                plan += [(t, default_chunk, f) for f in ("peer-read-reg:plain", "peer-write-reg:plain",
+                plan += [(t, 0, f) for f in ("peer-read-reg:plain", "peer-write-reg:plain",
                                                          "peer-read-reg:vec", "peer-write-reg:vec",
                                                          "peer-read-reg:dma", "peer-write-reg:dma", "peer-read:dma")]
     # stable sort into tiers, so the likeliest winners are timed before the budget can run out: the default
@@ -1003,7 +1315,7 @@ def bench_distributed(a):
                 # where a capped copy beat the uncapped one by > 10 % on every rank, the peer forms get a
                 # sweep entry with that cap next (the same decision on every rank: the rates are MIN-reduced)
                 extra = probe_cap_entries(state["line"]["xgmi_probe_GBps"], by_cap)
-                plan[i_plan:i_plan] = [(t, default_chunk, f) for f in extra]
+                plan[i_plan:i_plan] = [(t, 0, f) for f in extra]
             except Exception as e:  # noqa: BLE001
                 state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
             try:
@@ -1025,8 +1337,18 @@ def bench_distributed(a):
             sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "error": str(e)[:200]})
             continue
         sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "ms": round(ms_, 4),
-                      "busbw_GBps": round(bws(ms_)[1], 2), "check": "ok" if ok_ else f"MISMATCH ({why_})"})
+                      "busbw_GBps": round(bws(ms_)[1], 2), "enqueue_ms": enq["ms"],
+                      "check": "ok" if ok_ else f"MISMATCH ({why_})"})
     state["line"]["sweep"] = sweep
+
+    # the execution model against this run's own sweep: every entry's prediction under
+    # the constants the probe gave, the p2p constants re-fitted to the measured times (issue measured
+    # directly from the enqueue times), and the re-fitted model's choice timed next to the sweep's best
+    phase("cost model")
+    try:
+        state["line"]["cost_model"] = validate_model(sweep)
+    except Exception as e:  # noqa: BLE001  the model's report must not cost the run its line
+        state["line"]["cost_model"] = {"error": str(e)[:200]}
 
     # 3. the sweep's best validated configuration, re-timed like the default, if it is faster
     phase("headline")
@@ -1038,7 +1360,8 @@ def bench_distributed(a):
         ms = timed(fn_best, a.steps, a.warmup)
         ok, _ = check_y(fn_best)
         if ok and ms < ms_default:
-            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps", "cost_model_fit") if k in state["line"]}
+            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps", "cost_model_fit", "cost_model", "fallback_stream")
+                     if k in state["line"]}
             state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,
                                         {"config_selection": "best validated configuration of the sweep",
                                          "default_config": default_info, "sweep": sweep, **carry})
@@ -1054,7 +1377,9 @@ def bench_distributed(a):
     # north_star's transport is RCCL point-to-point: its best validated configuration is graded on its own,
     # whatever form won the headline
     if not a.host_comm:
-        hl["rccl_p2p_best"] = rccl_p2p_best(sweep + [{**default_info, "check": "ok" if ok_default else "x"}],
+        hl["rccl_p2p_best"] = rccl_p2p_best(sweep + [{**default_info, "check": "ok" if ok_default else "x",
+                                                      "form": default_info["ran"]["form"],
+                                                      "chunk_bytes": default_info["ran"]["chunk_bytes"]}],
                                             world, torch.cuda.device_count(), bucket,
                                             lambda r: links_driven(world, r["topology"], r["form"]))
         if hl["rccl_p2p_best"] is not None:
@@ -1145,6 +1470,7 @@ def bench_distributed(a):
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
     state["done"] = True
+    unblock()
     if not sync_state["device"]:
         # an RCCL kernel that never completed is still on the device: tearing the runtime down would wait
         # for it, so the line printed above is this process's last act

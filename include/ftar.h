@@ -117,21 +117,25 @@ ftar_status_t ftar_reduce_nested(const void* const* srcs, int k, void* dst, size
 ftar_status_t ftar_topo_parse(const char* ft_topo, const char* ft_lonely, int nranks, ftar_topo_t* out);
 /* FT_TOPO/FT_LONELY from the environment, else ftar_topo_choose(nranks, bytes). */
 ftar_status_t ftar_topo_from_env(int nranks, size_t bytes, ftar_topo_t* out);
-/* Cost-model choice among all ordered factorizations of nranks (plus ring),
- * constants re-fitted for MI355X xGMI (DESIGN.md §Cost model). */
+/* The topology the execution model (below) chooses among all ordered
+ * factorizations of nranks (plus the ring) at the default data movement (the
+ * one-round direct forms, the best piece): the reference's own question
+ * (cost_model/CostModel.h:82-120).  FTAR_COST_MODEL=reference: the
+ * reference's scores instead. */
 ftar_status_t ftar_topo_choose(int nranks, size_t bytes, ftar_topo_t* out);
 /* The candidate set the cost model scores, in the reference's getWidth order
  * (cost_model/GetWidth.h:42-47; its [1,P]/[P,1] entries = the ring), plus the
  * single-stage width-P tree right after the ring (getWidth omits it; FT_TOPO=P
  * is valid).  Writes up to max_out entries, returns the total count (<0 = error). */
 int ftar_topo_candidates(int nranks, ftar_topo_t* out, int max_out);
-/* Model cost (seconds) of one topology for a bucket of `bytes`. */
+/* Predicted seconds of one topology for a bucket of `bytes` at that default
+ * data movement (direct forms, the model's piece). */
 double ftar_topo_cost(const ftar_topo_t* topo, int nranks, size_t bytes);
-/* Constants of that (xGMI) model: alpha = one p2p round's latency (us), link =
- * one peer's one-direction bandwidth (GB/s), hbm = the reduce kernel's rate
- * (GB/s).  Process-wide; a value <= 0 restores the default; the environment
- * (FTAR_COST_ALPHA_US / _LINK_GBPS / _HBM_GBPS) overrides both.  bench.py sets
- * them from ftar_xgmi_probe. */
+/* Three of the execution model's constants (ftar_cost_set sets them all):
+ * alpha = one p2p group's latency (us), link = one peer's one-direction
+ * bandwidth (GB/s), hbm = the reduce kernel's rate (GB/s).  Process-wide; a
+ * value <= 0 restores the default; the environment (FTAR_COST_ALPHA_US /
+ * _LINK_GBPS / _HBM_GBPS) overrides both. */
 ftar_status_t ftar_cost_set_params(double alpha_us, double link_gbps, double hbm_gbps);
 ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* hbm_gbps);
 
@@ -235,6 +239,8 @@ ftar_status_t ftar_comm_destroy(ftar_comm_t comm);
 ftar_status_t ftar_comm_rank(ftar_comm_t comm, int* rank);
 ftar_status_t ftar_comm_size(ftar_comm_t comm, int* size);
 ftar_status_t ftar_comm_device(ftar_comm_t comm, int* device);
+/* The communicator's transport: "rccl", "local" (in-process group) or "host" (ftar_comm_init_host). */
+const char* ftar_comm_transport(ftar_comm_t comm);
 /* Pipelining granularity of the transfers (bytes, rounded to 256 B); 0 = the
  * execution model's piece for each call (the default; FTAR_CHUNK_BYTES at
  * init fixes it).  get: 0 while the model chooses. */

@@ -15,6 +15,7 @@ FTAR_LOOPBACK_MODE=capture instead captures the AllReduce into a HIP graph and r
 FTAR_LOOPBACK_MODE=soak runs seeded random cases with random per-call settings (soak());
 FTAR_LOOPBACK_MODE=ddp trains through DistributedDataParallel with ftar's comm hook (ddp());
 FTAR_LOOPBACK_MODE=full runs BASELINE's C4 and C5 buckets (full_size()).
+FTAR_LOOPBACK_MODE=first_contact: rank 0 calls while the others never do (first_contact()).
 """
 import json
 import os
@@ -87,6 +88,9 @@ def main():
     if os.environ.get("FTAR_LOOPBACK_MODE") == "full":
         full_size(comm, res, world, rank)
         return finish(comm, res)
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "first_contact":
+        first_contact(comm, res, world, rank)
+        return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "soak":
         soak(comm, res, world, rank, run, int(os.environ.get("FTAR_LOOPBACK_SOAK", "40")))
         return finish(comm, res)
@@ -143,7 +147,8 @@ def write_result(res):
 def finish(comm, res):
     import torch
     import torch.distributed as dist
-    torch.cuda.synchronize()
+    if "first_call" not in res:   # a broken communicator's stream may hold an aborted all-gather: not waited on
+        torch.cuda.synchronize()
     comm.destroy()
     print("LOOPBACK " + json.dumps(res), flush=True)
     write_result(res)
@@ -283,6 +288,39 @@ def full_size(comm, res, world, rank):
         del x, y, xs, exp
         torch.cuda.empty_cache()
     comm.chunk_bytes = 0
+
+
+def first_contact(comm, res, world, rank):
+    """A peer that never makes its first call: rank 0's first call on the RCCL communicator would
+    block in the settings all-gather; it runs on a helper thread with a deadline (FTAR_FIRST_CONTACT_TIMEOUT_S,
+    4 s here), so the call fails with FTAR_ERR_TIMEOUT after about that long, every later call fails at once,
+    and the communicator is destroyed (RCCL aborted) without a hang.  The other ranks never call; they
+    destroy their communicators after rank 0 is done."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    import ftar
+    if rank == 0:
+        x = torch.ones(4096, device="cuda")
+        t0 = time.time()
+        try:
+            comm.allreduce(x, x, x.numel(), "f32", "sum", topo_="1", stream=torch.cuda.current_stream())
+            res["fail"].append("the first call returned although no peer took part")
+        except ftar.FtarError as e:
+            res["first_call"] = {"status": e.status, "s": round(time.time() - t0, 2), "error": str(e)[:300]}
+            if e.status != 7 or not 3 <= time.time() - t0 <= 60:
+                res["fail"].append(f"first call: {res['first_call']}")
+        t1 = time.time()
+        try:
+            comm.allreduce(x, x, x.numel(), "f32", "sum", topo_="1", stream=torch.cuda.current_stream())
+            res["fail"].append("the second call on a broken communicator returned")
+        except ftar.FtarError as e:
+            res["second_call"] = {"status": e.status, "s": round(time.time() - t1, 3)}
+            if e.status != 7 or time.time() - t1 > 1:
+                res["fail"].append(f"second call: {res['second_call']}")
+    dist.barrier()
 
 
 def capture(comm, res, world, rank):

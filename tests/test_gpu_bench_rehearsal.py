@@ -53,14 +53,17 @@ def test_bench_n_gt_1_rehearsal(ranks, extra):
                                            ({"FTAR_BENCH_FAIL_DEFAULT": "1"}, "FTAR_BENCH_FAIL_DEFAULT")])
 def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
     """The first-contact failure paths of the 8-GPU run, at world size 1 over a real RCCL communicator: an RCCL
-    call that never completes (simulated: the preflight takes the path without anything hanging) or fails makes
-    every rank fall back to the IPC peer forms; the line names every rank's error and the stage times, and
-    rccl_p2p_best is absent because no RCCL configuration was measured."""
-    d = _bench(1, ["--force-dist", "--no-cpu-baseline"], env_extra)
+    call that never completes or fails makes every rank fall back to the IPC peer forms; the line names every
+    rank's error and the stage times, and rccl_p2p_best is absent because no RCCL configuration was measured.
+    The hang is real: a spinning wave keeps the bench's stream from draining until the run ends,
+    and the fallback runs on a fresh stream -- still blocked when the fallback's default was measured."""
+    d = _bench(1, ["--force-dist", "--no-cpu-baseline"], dict(env_extra, FTAR_BENCH_PREFLIGHT_S="5"))
     assert d["check"] == "ok" and d["config"]["form"].startswith("peer-"), d["config"]
     assert why in d["rccl_init_error"], d["rccl_init_error"]
     assert len(d["rccl_error_by_rank"]) == 1 and why in d["rccl_error_by_rank"][0]["error"]
     assert "default" in d["stage_wall_s"] and d.get("rccl_p2p_best") is None
+    if "FTAR_BENCH_PREFLIGHT_HANG" in env_extra:
+        assert d["fallback_stream"] == {"fresh": True, "stuck_stream_still_blocked": True}, d.get("fallback_stream")
 
 
 @pytest.mark.parametrize("ranks", [2, pytest.param(4, marks=pytest.mark.wide)])
@@ -73,7 +76,13 @@ def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
     d = _bench(ranks, ["--rccl-loopback", "--no-cpu-baseline"], {"FTAR_BENCH_BUDGET_S": "160"})
     assert d["n_gpus"] == ranks and d["check"] == "ok" and "watchdog" not in d, d
     assert "rccl_init_error" not in d and "rccl_error_by_rank" not in d, d.get("rccl_init_error")
-    assert d["default_config"]["form"] == "direct" and d["default_config"]["check"] == "ok", d["default_config"]
+    # the default configuration is the execution model's: form "auto", which ran the one-round RCCL forms
+    assert d["default_config"]["form"] == "auto" and d["default_config"]["check"] == "ok", d["default_config"]
+    assert d["default_config"]["ran"]["form"] == "direct" and d["default_config"]["enqueue_ms"] > 0
+    cm = d["cost_model"]
+    assert "error" not in cm and cm["prediction_error_refit"]["entries"] >= 5, cm
+    assert cm["choice_refit_measured_ms"] and cm["regret_refit"] is not None, cm
+    assert all("model_ms_refit" in r for r in d["sweep"] if r.get("check") == "ok"), d["sweep"]
     best = d["rccl_p2p_best"]
     assert best and best["form"].split(":")[0] in ("direct", "stages") and best["ms"] > 0, best
     rccl_ok = [r for r in d["sweep"] if r.get("check") == "ok" and r["form"].split(":")[0] in ("direct", "stages",

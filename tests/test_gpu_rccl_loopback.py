@@ -93,6 +93,19 @@ def test_ddp_comm_hook_over_rccl(world, dtype):
         assert not r["fail"] and r["ddp_hook_calls"] >= 3, r   # at least one bucket per step
 
 
+def test_first_contact_with_a_missing_peer_times_out():
+    """the first call on an RCCL communicator runs the settings agreement and connects the peers on
+    a helper thread with a deadline, so a peer that never calls fails the call with FTAR_ERR_TIMEOUT
+    (FTAR_FIRST_CONTACT_TIMEOUT_S) instead of hanging it; later calls fail at once; destroy aborts RCCL."""
+    p, res = run_loopback(2, {"FTAR_LOOPBACK_MODE": "first_contact", "FTAR_FIRST_CONTACT_TIMEOUT_S": "4"},
+                          timeout=120)
+    assert p.returncode == 0 and len(res) == 2, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
+    r0 = res[0]
+    assert not r0["fail"], r0
+    assert r0["first_call"]["status"] == 7 and "first contact" in r0["first_call"]["error"], r0
+    assert r0["second_call"]["status"] == 7, r0
+
+
 def test_rccl_p2p_baseline_c4_c5_full_size():
     """BASELINE configs[3] (8 ranks x 2^28 fp32, the ring, direct and staged, default pieces and pieces that
     divide no block) and configs[4] (8 ranks x 2^29 bf16, the width-8 tree) over RCCL between 8 processes,

@@ -374,9 +374,8 @@ def test_harness_rccl_transport_whole_bucket_exact(tmp_path, ranks, topo, n, ext
 def test_harness_rccl_communicator_lifecycle_two_ranks(tmp_path):
     """Communicator lifecycle over real RCCL communicators between MPI processes (loopback sockets): 6
     duplicates and singleton splits of MPI_COMM_WORLD created and freed in turn (an RCCL communicator brought
-    up and destroyed with each), exact sums throughout.  (Not --comm-threads: collectives on two RCCL
-    communicators issued concurrently from two threads may be ordered differently on the two ranks, and RCCL
-    then deadlocks, as NCCL documents for concurrent communicators; that check runs on the ipc transport.)"""
+    up and destroyed with each), exact sums throughout.  (--comm-threads runs on the ipc transport: see
+    test_harness_rccl_refuses_concurrent_communicators.)"""
     env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     args = ["--size", "65536", "--repeat", "2", "--check", "--comm-cycle", "6"]
     p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
@@ -385,3 +384,19 @@ def test_harness_rccl_communicator_lifecycle_two_ranks(tmp_path):
     assert p.stdout.count("(test passed)") == 2, out[-4000:]
     for r in range(2):
         assert re.search(rf"COMM_CYCLE {r}: cycles=6 handles_reused=\d+ ok", p.stdout), out[-4000:]
+
+
+@needs
+@pytest.mark.gpu
+def test_harness_rccl_refuses_concurrent_communicators(tmp_path):
+    """RCCL itself deadlocks when operations on two communicators reach the GPU in different orders on
+    different ranks -- inside ncclGroupEnd at their first exchange, and on the device once connected
+    (tools/rccl_order/rccl_order_probe.cpp, no ftar code; profiles/r04/rccl_order/) -- so the harness refuses
+    to drive RCCL communicators from several threads at once, with a clear message, instead of hanging; the
+    same --comm-threads check passes on the ipc transport (test_harness_communicator_lifecycle_two_ranks)."""
+    env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    args = ["--size", "4096", "--repeat", "1", "--check", "--comm-threads", "2"]
+    p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0, p.stdout[-3000:]
+    assert "COMM_THREADS refused: the RCCL transport" in p.stdout, p.stdout[-3000:]
+    assert p.stdout.count("(test passed)") == 2, p.stdout[-3000:]   # the AllReduce itself ran
