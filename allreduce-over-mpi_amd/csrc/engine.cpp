@@ -1006,10 +1006,16 @@ ftar_status_t decide_exec(ftar_comm* c, Topology* t, bool topo_auto, size_t byte
       ch.form = fixed_form;
       ch.chunk = fixed_chunk;
       ch.seconds = -1;
-      if (flags & FTAR_CHOOSE_TOPO) {  // the ring runs at any size
-        ch.topo = Topology();
-        ch.topo.ring = true;
-        ch.topo.widths = {1};
+      if (flags & FTAR_CHOOSE_TOPO) {  // the topology the default data movement would take (ftar_topo_choose)
+        ExecChoice d;
+        if (choose_exec(c->nranks, bytes, FTAR_CHOOSE_TOPO | FTAR_CHOOSE_CHUNK, *t, FTAR_FORM_DIRECT, 0, &d) ==
+            FTAR_SUCCESS) {
+          ch.topo = d.topo;
+        } else {  // the ring runs at any size
+          ch.topo = Topology();
+          ch.topo.ring = true;
+          ch.topo.widths = {1};
+        }
       }
     }
     if (c->exec_cache.size() > 256) c->exec_cache.clear();
