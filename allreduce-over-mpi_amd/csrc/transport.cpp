@@ -544,8 +544,17 @@ struct LocalHub {
     (t_issue_held ? retired : pool).push_back(e);
   }
   ~LocalHub() {
+    // the last rendezvous rounds and any undelivered messages still hold pooled events whose deleters give
+    // them back here: release them while the pool is alive, then destroy the pool (a barrier's round left
+    // in `done` was given back into the destroyed pool after it, a double free on destroying a group whose
+    // last call was a peer form)
+    done.reset();
+    pending.reset();
+    wire.clear();
     for (hipEvent_t e : pool) hip_ignore(hipEventDestroy(e));
     for (hipEvent_t e : retired) hip_ignore(hipEventDestroy(e));
+    pool.clear();
+    retired.clear();
   }
   // cv wait that lets the other ranks' threads issue meanwhile when this one
   // holds the issue lock (lock order: issue before mu)
