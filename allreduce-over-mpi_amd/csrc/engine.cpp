@@ -46,7 +46,7 @@ struct ftar_comm {
   int rank = 0, nranks = 1, device = 0;
   std::unique_ptr<ftar::Transport> tp;
   hipStream_t comm_s = nullptr, red_s = nullptr;
-  hipStream_t h2d_s = nullptr, d2h_s = nullptr;  // host mode (ftar_allreduce_host)
+  hipStream_t h2d_s = nullptr, d2h_s = nullptr;  // host mode (ftar_allreduce_host), created at its first call
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   void* staging = nullptr;  // host mode: the device copy of the bucket, grow-only
@@ -235,6 +235,13 @@ ftar_status_t grow_events(ftar_comm* c, size_t n) {
 }
 }  // namespace
 
+// the host-buffer path's copy streams, created at the first host-buffer call (see comm_setup_local)
+ftar_status_t ensure_host_streams(ftar_comm* c) {
+  if (!c->h2d_s) FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
+  if (!c->d2h_s) FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t agree_settings(ftar_comm* c, bool failed = false);
 
 namespace {
@@ -244,8 +251,9 @@ ftar_status_t comm_setup_local(ftar_comm* c) {
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   if (const char* rc = getenv("FTAR_REDUCE_CUS")) FTAR_RETURN_IF(set_reduce_cus(c, atoi(rc)));
   else FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->red_s, hipStreamNonBlocking));
-  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
-  FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  // the H2D / D2H streams exist only once a host-buffer call needs them (ensure_host_streams): a process
+  // has 4 hardware queues by default and streams beyond that share them (tools/rccl_order/queue_probe), so a
+  // device-resident user keeps the comm and reduce streams on queues of their own
   FTAR_CHECK_HIP(hipEventCreateWithFlags(&c->done_ev, hipEventDisableTiming));
   if (const char* pd = getenv("FTAR_PEER_DIRECT")) {
     const std::string m(pd);
@@ -876,7 +884,8 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // a failed call leaves only after its copies stopped touching the caller's host buffers: H2D reads of
   // io.src and D2H writes of io.dst may still be in flight on their streams
   auto leave = [&]() -> ftar_status_t {
-    for (hipStream_t s : {c->h2d_s, c->d2h_s, c->comm_s}) hip_ignore(hipStreamSynchronize(s));
+    for (hipStream_t s : {c->h2d_s, c->d2h_s, c->comm_s})
+      if (s) hip_ignore(hipStreamSynchronize(s));
     return st;
   };
   auto sync = [&]() -> bool {  // a barrier; false: some rank failed, leave the call
@@ -1048,7 +1057,8 @@ ftar_status_t resolve_plan(ftar_comm* c, const Topology& t, size_t count, const 
 ftar_status_t ensure_buffer(void** buf, size_t* have, size_t need, std::initializer_list<hipStream_t> users) {
   if (need <= *have) return FTAR_SUCCESS;
   if (*buf) {
-    for (hipStream_t st : users) FTAR_CHECK_HIP(hipStreamSynchronize(st));
+    for (hipStream_t st : users)
+      if (st) FTAR_CHECK_HIP(hipStreamSynchronize(st));  // (a stream not created yet has nothing in flight)
     FTAR_CHECK_HIP(hipFree(*buf));
     *buf = nullptr;
     *have = 0;
@@ -1173,6 +1183,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   // chain in issue order (every wait refers to an event recorded earlier in that order, so the chain keeps
   // every dependency; the comm/reduce overlap is given up inside the graph)
   const bool serial = capturing && serial_capture();
+  if (host) FTAR_RETURN_IF(ensure_host_streams(c));
   hipStream_t saved[4] = {c->comm_s, c->red_s, c->h2d_s, c->d2h_s};
   if (serial) c->comm_s = c->red_s = c->h2d_s = c->d2h_s = stream;
   c->serial = serial;

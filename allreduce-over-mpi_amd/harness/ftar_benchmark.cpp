@@ -22,8 +22,9 @@
 //                     recycles the handles), one exact integer-valued
 //                     MPI_Allreduce_FT on each;
 //   --comm-threads T  T duplicates driven at once from T threads
-//                     (MPI_THREAD_MULTIPLE), 3 exact calls each; refused (exit 2)
-//                     on the RCCL transport, which cannot order them;
+//                     (MPI_THREAD_MULTIPLE), 3 exact calls each; on the RCCL
+//                     transport only with GPU_MAX_HW_QUEUES >= 8 (T + 1), else
+//                     refused (exit 2);
 //   --register-check  MPI_Allreduce_FT_register / _unregister semantics on a
 //                     scratch buffer (needs a GPU: hipHostRegister).
 // --check is two-sided here: the reference only flags results that are too
@@ -318,21 +319,28 @@ int main(int argc, char** argv) {
     }
     lifecycle_bad += bad_c;
   }
-  // RCCL communicators driven from several threads at once are refused: RCCL itself deadlocks when two
-  // communicators' operations reach the GPU in different orders on different ranks -- at their first
-  // exchange inside ncclGroupEnd (its lazy connection handshake), and with the connections made, on the
-  // device (tools/rccl_order, profiles/r04/rccl_order/) -- NCCL's rule for concurrent communicators
+  // RCCL communicators driven from several threads at once: RCCL itself deadlocks when two communicators'
+  // operations reach it in different orders on different ranks -- inside ncclGroupEnd at their first
+  // exchange (its lazy connection handshake; ftar's first contact now makes every connection up front), and
+  // on the device once connected, when their kernels share one of the process's hardware queues (HIP's
+  // default is 4 per process; with 16, two RCCL communicators in opposite orders complete: tools/rccl_order,
+  // profiles/r04/rccl_order/).  So the threads run only when GPU_MAX_HW_QUEUES gives every stream of every
+  // communicator a queue of its own (8 per communicator: ftar's 4, the drop-in's, RCCL's), else refused.
   const char* world_tp = "";
   if (comm_threads > 0 && comm_type == "flextree") {
     ftar_comm_t fc = nullptr;
     if (MPI_Allreduce_FT_comm(MPI_COMM_WORLD, &fc) == MPI_SUCCESS && fc) world_tp = ftar_comm_transport(fc);
   }
-  if (comm_threads > 0 && comm_type == "flextree" && !strcmp(world_tp, "rccl")) {
+  const char* hwq = getenv("GPU_MAX_HW_QUEUES");
+  const int queues = hwq && *hwq ? atoi(hwq) : 4, need_queues = 8 * (comm_threads + 1);
+  if (comm_threads > 0 && comm_type == "flextree" && !strcmp(world_tp, "rccl") && queues < need_queues) {
     if (rank == 0)
-      printf("COMM_THREADS refused: the RCCL transport cannot drive communicators from %d threads at once -- "
-             "RCCL deadlocks when operations on different communicators reach the GPU in different orders on "
-             "different ranks (NCCL's rule for concurrent communicators; profiles/r04/rccl_order/); issue "
-             "them in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n", comm_threads);
+      printf("COMM_THREADS refused: the RCCL transport cannot drive communicators from %d threads at once "
+             "with %d hardware queues per process -- RCCL deadlocks when operations on different communicators "
+             "reach the GPU in different orders on different ranks and their kernels share a queue (NCCL's "
+             "rule for concurrent communicators; profiles/r04/rccl_order/); set GPU_MAX_HW_QUEUES >= %d, issue "
+             "the calls in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n",
+             comm_threads, queues, need_queues);
     fflush(stdout);
     lifecycle_bad += 1;
   } else if (comm_threads > 0 && comm_type == "flextree") {

@@ -488,10 +488,13 @@ def pieces_per_round(chunk, world, bucket, esz):
 def issue_from_enqueue(sweep, world, bucket, esz):
     """The host's enqueue time of one piece of one round (us): the median over the sweep's one-round RCCL
     entries of the time ftar_allreduce took to return (`enqueue_ms`) divided by the groups it issued
-    (2 rounds x pieces).  None without such entries."""
+    (2 rounds x pieces).  Entries whose enqueue took at least half the call are left out: there RCCL's
+    enqueue waited for the device (its work queue was full, so ncclGroupEnd blocks until earlier groups
+    drain), which measures the device, not the host.  None without usable entries."""
     per = []
     for r in sweep:
-        if r.get("form") == "direct" and r.get("enqueue_ms") and r.get("check") == "ok":
+        if (r.get("form") == "direct" and r.get("enqueue_ms") and r.get("check") == "ok" and
+                r["enqueue_ms"] < 0.5 * r.get("ms", 0)):
             groups = 2 * pieces_per_round(r["chunk_bytes"], world, bucket, esz)
             per.append(r["enqueue_ms"] * 1e3 / groups)
     if not per:

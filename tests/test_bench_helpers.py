@@ -251,10 +251,12 @@ def test_pieces_per_round_follow_the_engine():
 
 def test_issue_cost_comes_from_the_enqueue_times():
     import bench
-    sweep = [{"form": "direct", "chunk_bytes": 1 << 20, "enqueue_ms": 25.6, "check": "ok"},   # 256 groups
-             {"form": "direct", "chunk_bytes": 16 << 20, "enqueue_ms": 1.6, "check": "ok"},   # 16 groups
-             {"form": "stages", "chunk_bytes": 1 << 20, "enqueue_ms": 99.0, "check": "ok"},
-             {"form": "direct", "chunk_bytes": 4 << 20, "enqueue_ms": 6.4, "check": "ok"}]    # 64 groups
+    sweep = [{"form": "direct", "chunk_bytes": 1 << 20, "enqueue_ms": 25.6, "ms": 60.0, "check": "ok"},  # 256 groups
+             {"form": "direct", "chunk_bytes": 16 << 20, "enqueue_ms": 1.6, "ms": 9.0, "check": "ok"},   # 16 groups
+             {"form": "stages", "chunk_bytes": 1 << 20, "enqueue_ms": 99.0, "ms": 300.0, "check": "ok"},
+             {"form": "direct", "chunk_bytes": 4 << 20, "enqueue_ms": 6.4, "ms": 20.0, "check": "ok"},    # 64 groups
+             # the enqueue waited for the device (RCCL's work queue full): not a host cost, left out
+             {"form": "direct", "chunk_bytes": 256 << 10, "enqueue_ms": 900.0, "ms": 910.0, "check": "ok"}]
     assert bench.issue_from_enqueue(sweep, 8, 1 << 30, 4) == pytest.approx(100.0)
     assert bench.issue_from_enqueue([], 8, 1 << 30, 4) is None
 

@@ -395,8 +395,26 @@ def test_harness_rccl_refuses_concurrent_communicators(tmp_path):
     to drive RCCL communicators from several threads at once, with a clear message, instead of hanging; the
     same --comm-threads check passes on the ipc transport (test_harness_communicator_lifecycle_two_ranks)."""
     env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    env.pop("GPU_MAX_HW_QUEUES", None)   # HIP's default: 4 hardware queues per process
     args = ["--size", "4096", "--repeat", "1", "--check", "--comm-threads", "2"]
     p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode != 0, p.stdout[-3000:]
     assert "COMM_THREADS refused: the RCCL transport" in p.stdout, p.stdout[-3000:]
     assert p.stdout.count("(test passed)") == 2, p.stdout[-3000:]   # the AllReduce itself ran
+
+
+@needs
+@pytest.mark.gpu
+def test_harness_rccl_concurrent_communicators_with_a_queue_each(tmp_path):
+    """The same two threads over RCCL with GPU_MAX_HW_QUEUES=32: ftar's first contact makes every p2p
+    connection up front and every stream of both communicators gets a hardware queue of its own, so the two
+    communicators' calls complete in whatever order the threads issue them (RCCL alone: the q16 probe,
+    profiles/r04/rccl_order/warm_opposite_q16.log); exact sums, the communicators freed afterwards."""
+    env = dict(os.environ, FT_TOPO="1", FTAR_MPI_TRANSPORT="rccl", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+               GPU_MAX_HW_QUEUES="32")
+    args = ["--size", "65536", "--repeat", "2", "--check", "--comm-threads", "2"]
+    p = subprocess.run(_loopback_mpmd(2, args), cwd=tmp_path, env=env, capture_output=True, text=True, timeout=150)
+    out = p.stdout + p.stderr
+    assert p.returncode == 0, out[-4000:]
+    for r in range(2):
+        assert f"COMM_THREADS {r}: threads=2 ok" in p.stdout, out[-4000:]
