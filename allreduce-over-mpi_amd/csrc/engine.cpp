@@ -1236,8 +1236,17 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   const Plan* planp = nullptr;
   FTAR_RETURN_IF(resolve_plan(c, topology, count, form, &planp));
   const Plan& plan = *planp;
+  // what runs (ftar_comm_last_exec): the model's or the settings' form, unless the plan or the buffers send
+  // the call down another path below (host buffers on a p2p transport, a plan no peer kernel runs, the
+  // collective all-gather a ring or host buffers replace)
+  const bool peer_path = peer_mode && peer_eligible(plan) && (!host || !c->tp->async_p2p());
+  int ran = ex.form;
+  if (peer_path) ran = peer_mode == FTAR_PEER_READ ? FTAR_FORM_PEER_READ : FTAR_FORM_PEER_WRITE;
+  else if (form.reduce_scatter == FTAR_RS_STAGES) ran = plan.allgather == FTAR_AG_STAGES ? FTAR_FORM_STAGES : -2;
+  else ran = plan.allgather == FTAR_AG_DIRECT ? FTAR_FORM_DIRECT
+             : plan.allgather == FTAR_AG_COLLECTIVE ? FTAR_FORM_COLLECTIVE : -2;
   from_topology(topology, &c->last_exec.topo);
-  c->last_exec.form = ex.form;
+  c->last_exec.form = ran;
   c->last_exec.chunk_bytes = ex.chunk;
   c->last_exec.seconds = ex.seconds;
   const size_t nst = plan.stages.size();
