@@ -252,7 +252,12 @@ ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
  * fixes it, as do ftar_comm_set_allgather / _reduce_scatter / _peer_direct
  * (get then reports the form those describe, or -2 for a mix no form names).
  * A host-bootstrapped communicator keeps its peer form.
- * ftar_comm_last_exec: what the last call on this communicator ran. */
+ * ftar_comm_last_exec: what the last call on this communicator ran -- the
+ * topology, the form of the path actually taken (host buffers on an RCCL
+ * communicator run the pipelined p2p path whatever peer form is set; a ring
+ * or host buffers replace the collective all-gather with the direct one; -2
+ * for a mix no form names), the piece, and the model's predicted seconds
+ * (-1: unpriced). */
 ftar_status_t ftar_comm_set_form(ftar_comm_t comm, int form);
 ftar_status_t ftar_comm_get_form(ftar_comm_t comm, int* form);
 ftar_status_t ftar_comm_last_exec(ftar_comm_t comm, ftar_exec_t* out);
