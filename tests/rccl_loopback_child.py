@@ -160,8 +160,8 @@ def finish(comm, res):
 def soak(comm, res, world, rank, run, count):
     """Seeded random cases of this world size (tests/random_cases.py: ring, trees, lonely layouts, every dtype,
     SUM and BAND, ragged sizes down to 0 and 1 element, in place or out of place) over RCCL, each with a random
-    pipeline piece size, data-movement form and device, pinned-host or pageable-host buffers; every rank
-    against the oracle.
+    pipeline piece size, data-movement form (direct, stages, collective, peer read / write, auto) and device,
+    pinned-host or pageable-host buffers; every rank against the oracle.
     Every rank draws the same sequence, so the per-call settings agree across ranks."""
     import random
 
@@ -170,13 +170,14 @@ def soak(comm, res, world, rank, run, count):
     rng = random.Random(4242 + world)
     res["soak"] = 0
     for c in random_cases.cases(seed=900 + world, count=count, P_fixed=world):
-        form = rng.choice(["direct", "stages", "collective"])
+        # every data-movement form: the peer forms map the other processes' exchange buffers over IPC (plans
+        # they cannot run, and host buffers, take the p2p path); "auto" takes the execution model's choice
+        form = rng.choice(["direct", "stages", "collective", "peer-read", "peer-write", "auto"])
         chunk = rng.choice([0, 256, 4096, 1 << 16])
         host = rng.random() < 0.4
         pinned = rng.random() < 0.7
         try:
-            comm.allgather = form
-            comm.reduce_scatter = "stages" if form == "stages" else "direct"
+            comm.form = form
             comm.chunk_bytes = chunk
             comm.host_chunk_bytes = chunk
             out = run(c["ins"][rank], c["topo"], c["lonely"], fi.BY_NAME[c["dtype"]],
