@@ -838,8 +838,11 @@ def bench_distributed(a):
         return t[0].item() / max(1, steps) * 1e3
 
     def run_with(topo, chunk, form="direct"):
-        # form "auto": the execution model's form per call (and its piece where chunk is 0); the topology
-        # is `topo`, or the model's too when topo is None
+        """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
+        rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
+        kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
+        no local pass), "auto" (the execution model's form per call, and its piece where chunk is 0; the
+        topology is `topo`, or the model's too when topo is None)."""
         # peer-form tuning suffix: ":plain" = plain (not nontemporal) copies, ":vec" = register-kernel fold,
         # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
@@ -851,10 +854,6 @@ def bench_distributed(a):
         comm.rccl_register = tune == "ncclreg"
         # ":wgN": the peer forms' cross-GPU copies capped at N workgroups per segment (the probe's best cap)
         comm.peer_wg_cap = int(tune[2:]) if tune.startswith("wg") else 0
-        """form: "direct" (one-round reduce-scatter and all-gather over RCCL p2p), "stages" (the reference's
-        rounds both ways), "collective" (ncclAllGather), "peer-read" / "peer-write" (one-round plan moved by
-        kernel loads / stores through IPC-mapped exchange buffers), "...-reg" (the same on registered buffers,
-        no local pass)."""
         comm.chunk_bytes = chunk
         if form == "auto":
             comm.form = "auto"
