@@ -1,0 +1,330 @@
+// The engine's HOST code under AddressSanitizer + UndefinedBehaviorSanitizer, driven on a real GPU.
+//
+// libftar.so is rebuilt with the host sanitizers only (tools/asan/Makefile: clang++ for the host translation
+// units, hipcc with -fno-gpu-sanitize for the kernels, whose device code is untouched) and this program
+// drives in-process groups (ftar_comm_init_local) through the engine's paths: every data-movement form,
+// the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty and ragged buckets, device and
+// host buffers, in place and out of place, registered buffers for the peer forms, error paths, and groups
+// created and destroyed repeatedly.  Any heap misuse, use after free, double free or undefined behaviour in
+// plan caches, event pools, IPC maps, the local hub or the execution-model cache aborts the run.
+//
+// Results are checked too: inputs are small integers (exact in fp32 and bf16 and in every association
+// order), so the expected value of every element is the plain sum (or AND) whatever the schedule.
+//
+//   engine_stress [calls] [seed]      default 1500 calls, seed 1
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "ftar.h"
+
+namespace {
+
+#define HIP_OK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      exit(2);                                                                          \
+    }                                                                                   \
+  } while (0)
+
+struct Dt {
+  ftar_dtype_t t;
+  size_t size;
+  const char* name;
+};
+const Dt kDtypes[] = {{FTAR_FLOAT32, 4, "f32"}, {FTAR_BFLOAT16, 2, "bf16"}, {FTAR_INT32, 4, "i32"},
+                      {FTAR_UINT8, 1, "u8"}, {FTAR_FLOAT64, 8, "f64"}, {FTAR_INT16, 2, "i16"}};
+
+// element i of rank r: a small integer (|v| <= 8, so P = 8 sums stay exact in bf16's 8-bit mantissa)
+int value(size_t i, int r) { return (int)((i * 7 + (size_t)r * 13 + (i >> 9)) % 17) - 8; }
+
+uint16_t to_bf16(float f) {  // exact for small integers
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  return (uint16_t)(u >> 16);
+}
+float from_bf16(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+void fill(std::vector<uint8_t>& b, const Dt& d, size_t n, int r, bool band) {
+  b.resize(n * d.size);
+  for (size_t i = 0; i < n; ++i) {
+    const int v = band ? (int)((i * 2654435761u + (size_t)r * 40503u) & 0x7fffffff) : value(i, r);
+    switch (d.t) {
+      case FTAR_FLOAT32: { float f = (float)v; memcpy(&b[i * 4], &f, 4); break; }
+      case FTAR_BFLOAT16: { uint16_t h = to_bf16((float)v); memcpy(&b[i * 2], &h, 2); break; }
+      case FTAR_INT32: { int32_t x = v; memcpy(&b[i * 4], &x, 4); break; }
+      case FTAR_UINT8: b[i] = (uint8_t)v; break;
+      case FTAR_FLOAT64: { double f = (double)v; memcpy(&b[i * 8], &f, 8); break; }
+      case FTAR_INT16: { int16_t x = (int16_t)v; memcpy(&b[i * 2], &x, 2); break; }
+      default: abort();
+    }
+  }
+}
+
+// the expected result (every rank): sum or AND of the P inputs, in the element type
+void expect(std::vector<uint8_t>& out, const Dt& d, size_t n, int P, bool band) {
+  std::vector<std::vector<uint8_t>> ins(P);
+  for (int r = 0; r < P; ++r) fill(ins[r], d, n, r, band);
+  out.assign(n * d.size, 0);
+  for (size_t i = 0; i < n; ++i) {
+    switch (d.t) {
+      case FTAR_FLOAT32: {
+        float s = 0;
+        for (int r = 0; r < P; ++r) { float f; memcpy(&f, &ins[r][i * 4], 4); s += f; }
+        memcpy(&out[i * 4], &s, 4);
+        break;
+      }
+      case FTAR_BFLOAT16: {
+        float s = 0;
+        for (int r = 0; r < P; ++r) { uint16_t h; memcpy(&h, &ins[r][i * 2], 2); s += from_bf16(h); }
+        uint16_t h = to_bf16(s);
+        memcpy(&out[i * 2], &h, 2);
+        break;
+      }
+      case FTAR_INT32: {
+        int32_t s = band ? -1 : 0;
+        for (int r = 0; r < P; ++r) {
+          int32_t x;
+          memcpy(&x, &ins[r][i * 4], 4);
+          s = band ? (s & x) : (int32_t)((uint32_t)s + (uint32_t)x);
+        }
+        memcpy(&out[i * 4], &s, 4);
+        break;
+      }
+      case FTAR_UINT8: {
+        uint8_t s = band ? 0xff : 0;
+        for (int r = 0; r < P; ++r) s = band ? (uint8_t)(s & ins[r][i]) : (uint8_t)(s + ins[r][i]);
+        out[i] = s;
+        break;
+      }
+      case FTAR_FLOAT64: {
+        double s = 0;
+        for (int r = 0; r < P; ++r) { double f; memcpy(&f, &ins[r][i * 8], 8); s += f; }
+        memcpy(&out[i * 8], &s, 8);
+        break;
+      }
+      case FTAR_INT16: {
+        int16_t s = band ? -1 : 0;
+        for (int r = 0; r < P; ++r) {
+          int16_t x;
+          memcpy(&x, &ins[r][i * 2], 2);
+          s = band ? (int16_t)(s & x) : (int16_t)((uint16_t)s + (uint16_t)x);
+        }
+        memcpy(&out[i * 2], &s, 2);
+        break;
+      }
+      default: abort();
+    }
+  }
+}
+
+// valid layouts (lonely L with S = P - L ranks in >= 2 stages and L * w0 <= S, as tests/random_cases.py)
+struct Layout {
+  const char* topo;
+  const char* lonely;
+};
+std::vector<Layout> layouts(int P) {
+  switch (P) {
+    case 2: return {{"1", nullptr}, {"2", nullptr}};
+    case 3: return {{"1", nullptr}, {"3", nullptr}};
+    case 4: return {{"1", nullptr}, {"4", nullptr}, {"2,2", nullptr}};
+    case 5: return {{"1", nullptr}, {"5", nullptr}, {"2,2", "1"}};
+    case 6: return {{"1", nullptr}, {"2,3", nullptr}, {"3,2", nullptr}, {"6", nullptr}, {"2,2", "2"}};
+    default: return {{"1", nullptr}, {"8", nullptr}, {"2,4", nullptr}, {"4,2", nullptr}, {"2,2,2", nullptr},
+                     {"3,2", "2"}};
+  }
+}
+
+struct Stats {
+  long calls = 0, checked = 0, refused = 0, groups = 0, regs = 0;
+};
+
+int fail(const std::string& what) {
+  fprintf(stderr, "FAIL %s\n", what.c_str());
+  exit(1);
+}
+
+// one group: `calls` random calls, then destroyed
+void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
+  std::vector<ftar_comm_t> comms(P);
+  std::vector<int> devs(P, 0);
+  if (ftar_comm_init_local(comms.data(), P, devs.data()) != FTAR_SUCCESS) fail(std::string("init_local: ") + ftar_last_error());
+  ++st->groups;
+  const auto lay = layouts(P);
+  const int forms[] = {FTAR_FORM_AUTO, FTAR_FORM_DIRECT, FTAR_FORM_STAGES, FTAR_FORM_COLLECTIVE, FTAR_FORM_PEER_READ,
+                       FTAR_FORM_PEER_WRITE};
+  const size_t chunks[] = {0, 256, 4096 + 256, 1u << 16, 1u << 20};
+  // registered device buffers (the peer forms' no-copy path): one pair per rank, registered collectively
+  const size_t reg_bytes = 1u << 22;
+  std::vector<void*> rx(P), ry(P);
+  std::vector<int> idx(P), idy(P);
+  for (int r = 0; r < P; ++r) {
+    HIP_OK(hipMalloc(&rx[r], reg_bytes));
+    HIP_OK(hipMalloc(&ry[r], reg_bytes));
+  }
+  {
+    std::vector<std::thread> th;
+    std::vector<ftar_status_t> s(P);
+    for (int r = 0; r < P; ++r)
+      th.emplace_back([&, r] {
+        s[r] = ftar_comm_register(comms[r], rx[r], reg_bytes, &idx[r]);
+        if (s[r] == FTAR_SUCCESS) s[r] = ftar_comm_register(comms[r], ry[r], reg_bytes, &idy[r]);
+      });
+    for (auto& t : th) t.join();
+    for (int r = 0; r < P; ++r)
+      if (s[r] != FTAR_SUCCESS) fail(std::string("register: ") + ftar_last_error());
+    st->regs += 2 * P;
+  }
+  for (int call = 0; call < calls; ++call) {
+    const Layout L = lay[rng() % lay.size()];
+    const int form = forms[rng() % 6];
+    const size_t chunk = chunks[rng() % 5];
+    const Dt& d = kDtypes[rng() % 6];
+    const bool band = (d.t == FTAR_INT32 || d.t == FTAR_UINT8 || d.t == FTAR_INT16) && rng() % 3 == 0;
+    const size_t sizes[] = {0, 1, (size_t)P - 1, (size_t)P + 1, 1000 + rng() % 5000, 100000 + rng() % 300000};
+    size_t n = sizes[rng() % 6];
+    const bool host = rng() % 4 == 0;
+    const bool oop = rng() % 2 == 0;
+    const bool registered = !host && oop && rng() % 3 == 0;
+    if (registered) n = std::min(n, reg_bytes / d.size);
+    ftar_topo_t topo;
+    if (ftar_topo_parse(L.topo, L.lonely, P, &topo) != FTAR_SUCCESS) fail(std::string("topo_parse ") + L.topo);
+    for (int r = 0; r < P; ++r) {
+      if (ftar_comm_set_form(comms[r], form) != FTAR_SUCCESS) fail("set_form");
+      if (ftar_comm_set_chunk_bytes(comms[r], chunk) != FTAR_SUCCESS) fail("set_chunk_bytes");
+      if (ftar_comm_set_host_chunk_bytes(comms[r], chunk) != FTAR_SUCCESS) fail("set_host_chunk_bytes");
+    }
+    const size_t bytes = n * d.size;
+    std::vector<std::vector<uint8_t>> in(P);
+    for (int r = 0; r < P; ++r) fill(in[r], d, n, r, band);
+    std::vector<void*> send(P, nullptr), recv(P, nullptr);
+    std::vector<void*> owned;
+    std::vector<std::vector<uint8_t>> hbuf(2 * P);
+    for (int r = 0; r < P; ++r) {
+      if (host) {
+        hbuf[2 * r] = in[r];
+        hbuf[2 * r + 1].assign(bytes, 0x5a);
+        send[r] = oop ? (void*)hbuf[2 * r].data() : nullptr;
+        recv[r] = oop ? (void*)hbuf[2 * r + 1].data() : (void*)hbuf[2 * r].data();
+        if (!bytes) recv[r] = send[r] = nullptr;
+        continue;
+      }
+      void *a = nullptr, *b = nullptr;
+      if (registered) {
+        a = rx[r];
+        b = ry[r];
+      } else {
+        HIP_OK(hipMalloc(&a, bytes ? bytes : 1));
+        owned.push_back(a);
+        if (oop) {
+          HIP_OK(hipMalloc(&b, bytes ? bytes : 1));
+          owned.push_back(b);
+        }
+      }
+      if (bytes) HIP_OK(hipMemcpy(a, in[r].data(), bytes, hipMemcpyHostToDevice));
+      if (oop && bytes) HIP_OK(hipMemset(b, 0x5a, bytes));
+      send[r] = oop ? a : nullptr;
+      recv[r] = oop ? b : a;
+    }
+    const ftar_op_t op = band ? FTAR_BAND : FTAR_SUM;
+    const ftar_status_t s = host ? ftar_allreduce_host_group(send.data(), recv.data(), n, d.t, op, &topo,
+                                                             comms.data(), P, nullptr)
+                                 : ftar_allreduce_group(send.data(), recv.data(), n, d.t, op, &topo, comms.data(),
+                                                        P, nullptr);
+    HIP_OK(hipDeviceSynchronize());
+    ++st->calls;
+    char what[256];
+    snprintf(what, sizeof what, "P=%d topo=%s+%s form=%d chunk=%zu %s %s n=%zu host=%d oop=%d reg=%d", P, L.topo,
+             L.lonely ? L.lonely : "0", form, chunk, d.name, band ? "band" : "sum", n, host, oop, registered);
+    if (s != FTAR_SUCCESS) {
+      // refusals the engine documents: forms a layout cannot take are replaced, so only errors remain
+      fail(std::string(what) + ": " + ftar_status_string(s) + ": " + ftar_last_error());
+    }
+    std::vector<uint8_t> want;
+    expect(want, d, n, P, band);
+    for (int r = 0; r < P; ++r) {
+      std::vector<uint8_t> got(bytes);
+      if (host) got = oop ? hbuf[2 * r + 1] : hbuf[2 * r];
+      else if (bytes) HIP_OK(hipMemcpy(got.data(), recv[r], bytes, hipMemcpyDeviceToHost));
+      if (got != want) {
+        size_t i = 0;
+        while (i < bytes && got[i] == want[i]) ++i;
+        fail(std::string(what) + ": rank " + std::to_string(r) + " differs at byte " + std::to_string(i));
+      }
+    }
+    ++st->checked;
+    for (void* p : owned) HIP_OK(hipFree(p));
+  }
+  // error paths: refused before anything is enqueued, the group stays usable
+  {
+    ftar_topo_t bad;
+    if (ftar_topo_parse("3,3", nullptr, P, &bad) == FTAR_SUCCESS) {
+      std::vector<void*> recv(P, rx[0]);
+      for (int r = 0; r < P; ++r) recv[r] = rx[r];
+      if (ftar_allreduce_group(nullptr, recv.data(), 64, FTAR_FLOAT32, FTAR_SUM, &bad, comms.data(), P, nullptr) ==
+          FTAR_SUCCESS)
+        fail("topology 3,3 accepted");
+      ++st->refused;
+    }
+    std::vector<void*> recv(P);
+    for (int r = 0; r < P; ++r) recv[r] = rx[r];
+    if (ftar_allreduce_group(nullptr, recv.data(), 64, FTAR_FLOAT32, FTAR_BAND, nullptr, comms.data(), P, nullptr) !=
+        FTAR_ERR_UNSUPPORTED)
+      fail("BAND on fp32 not refused");
+    ++st->refused;
+  }
+  for (int r = 0; r < P; ++r) {
+    ftar_comm_deregister(comms[r], idx[r]);
+    ftar_comm_deregister(comms[r], idy[r]);
+  }
+  for (int r = 0; r < P; ++r)
+    if (ftar_comm_destroy(comms[r]) != FTAR_SUCCESS) fail(std::string("destroy: ") + ftar_last_error());
+  for (int r = 0; r < P; ++r) {
+    HIP_OK(hipFree(rx[r]));
+    HIP_OK(hipFree(ry[r]));
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const long total = argc > 1 ? atol(argv[1]) : 1500;
+  const unsigned long seed = argc > 2 ? strtoul(argv[2], nullptr, 0) : 1;
+  HIP_OK(hipSetDevice(0));
+  std::mt19937_64 rng(seed);
+  Stats st;
+  const int worlds[] = {2, 3, 4, 5, 6, 8};
+  long done = 0;
+  int round = 0;
+  while (done < total) {
+    const int P = worlds[round++ % 6];
+    const int calls = 20 + (int)(rng() % 60);  // groups come and go: bring-up and teardown under ASan too
+    run_group(P, calls, rng, &st);
+    done += calls;
+    if (round % 6 == 0) {
+      printf("progress: %ld calls, %ld groups\n", st.calls, st.groups);
+      fflush(stdout);
+    }
+  }
+  printf("{\"calls\": %ld, \"checked\": %ld, \"refused\": %ld, \"groups\": %ld, \"registrations\": %ld, \"seed\": %lu}\n",
+         st.calls, st.checked, st.refused, st.groups, st.regs, seed);
+  fflush(stdout);
+  // every group is destroyed and the device drained; skip the HIP runtime's static teardown, where the
+  // sanitizer's own HIP allocator hooks trip a CHECK once the runtime has unloaded (not ftar code)
+  HIP_OK(hipDeviceSynchronize());
+  _Exit(0);
+}
