@@ -148,7 +148,8 @@ double exec_cost(const Topology& t, int P, size_t bytes, int form, size_t chunk,
       return 3.0 * k.barrier + copy_in + std::max(B / k.peer_read, fold) + B / k.peer_read;
     }
     if (k.peer_write <= 0) return -1.0;
-    const double copy_out = registered ? 0.0 : 2.0 * (P - 1) * B / k.copy;
+    // unregistered outputs: the copy-out of the final blocks, and a third barrier after it (engine.cpp)
+    const double copy_out = registered ? 0.0 : 2.0 * (P - 1) * B / k.copy + k.barrier;
     return 2.0 * k.barrier + 2.0 * B / k.peer_write + fold + copy_out;
   }
   const double c = chunk ? std::min<double>((double)chunk, B) : B;

@@ -739,12 +739,21 @@ ftar_status_t peer_allreduce(const void* sendbuf, void* recvbuf, size_t count, f
     if (!zc) {
       segs.clear();
       for (const Transfer& x : ag.recvs) segs.push_back({X + final_at + x.off * esz, out + x.off * esz, x.len * esz});
+      // test hook (tests/rccl_loopback_child.py write_race): this rank enqueues its copy-out late, as a slow
+      // host would, so a peer already in its next call writes into this exchange buffer meanwhile
+      static const long late_us = getenv("FTAR_DEBUG_PEER_LATE_US") ? atol(getenv("FTAR_DEBUG_PEER_LATE_US")) : 0;
+      if (late_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(late_us));
       if (c->peer_nt) {
         for (const Segment& g : segs) FTAR_RETURN_IF(launch_copy(g.src, g.dst, g.bytes, c->comm_s));
       } else {
         FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, false));
       }
       FTAR_RETURN_IF(mark(c, "copy-out", c->comm_s));
+      // no peer may scatter its next call into my X before my copy-out has read it: a call whose slot area
+      // covers this call's final area would overwrite it (tools/asan/engine_stress rccl found it; test:
+      // test_peer_write_waits_for_every_copy_out)
+      FTAR_RETURN_IF(tp->barrier(c->comm_s));
+      FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
     }
   }
   FTAR_RETURN_IF(tp->before_join());
@@ -1251,7 +1260,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   c->last_exec.seconds = ex.seconds;
   const size_t nst = plan.stages.size();
   if (!c->tp->async_p2p()) {
-    // A host-bootstrapped communicator's paths differ in their host barriers (peer read: 3, write: 2,
+    // A host-bootstrapped communicator's paths differ in their host barriers (peer read: 3, write: 3,
     // host buffers pipelined: m + 2, whole bucket: 3), so every rank must take the same one with the same
     // pieces: the settings that choose it are compared first, and a mismatch fails the call on every rank
     //  instead of pairing barriers of different phases.

@@ -302,7 +302,8 @@ ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter
  *                    pulls every final block (three stream-ordered barriers);
  *   FTAR_PEER_WRITE  each rank pushes its copy of every peer's block into that
  *                    peer's buffer, folds locally, and pushes its final block
- *                    to every peer (two barriers).
+ *                    to every peer (three barriers: the last keeps
+ *                    my exchange buffer until my copy-out has read it).
  * The plan's fold is executed unchanged: same bits.  Other plans keep RCCL p2p. */
 typedef enum { FTAR_PEER_OFF = 0, FTAR_PEER_READ = 1, FTAR_PEER_WRITE = 2 } ftar_peer_mode_t;
 ftar_status_t ftar_comm_set_peer_direct(ftar_comm_t comm, int mode);

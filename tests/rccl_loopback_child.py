@@ -39,6 +39,8 @@ def main():
     faulthandler.enable()   # a crash inside the runtime still names the Python line it came from
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     loopback_env(rank)
+    if os.environ.get("FTAR_LOOPBACK_LATE_RANK") == str(rank):   # write_race: this rank's copy-outs run late
+        os.environ["FTAR_DEBUG_PEER_LATE_US"] = "150000"
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -90,6 +92,9 @@ def main():
         return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "first_contact":
         first_contact(comm, res, world, rank)
+        return finish(comm, res)
+    if os.environ.get("FTAR_LOOPBACK_MODE") == "write_race":
+        write_race(comm, res, world, rank)
         return finish(comm, res)
     if os.environ.get("FTAR_LOOPBACK_MODE") == "soak":
         soak(comm, res, world, rank, run, int(os.environ.get("FTAR_LOOPBACK_SOAK", "40")))
@@ -289,6 +294,32 @@ def full_size(comm, res, world, rank):
         del x, y, xs, exp
         torch.cuda.empty_cache()
     comm.chunk_bytes = 0
+
+
+def write_race(comm, res, world, rank):
+    """The peer-write form's exchange buffer across consecutive calls: a tiny call (its final blocks land at
+    the end of the slot area, final_at = P * slot) then a larger one whose slots cover that final area.  The
+    last rank enqueues its copy-out of every call late (FTAR_DEBUG_PEER_LATE_US, as a slow host would), so its
+    peers are already scattering the next call into its exchange buffer: the call must not return on any rank
+    before every rank's copy-out is done.  Small-integer inputs, so every result is exact."""
+    import numpy as np
+    import torch
+    res["write_race"] = 0
+    comm.form = "peer-write"
+    for it in range(4):
+        for n, dt, tdt in ((9, "f64", torch.float64), (100_003, "f32", torch.float32)):
+            x = (torch.arange(n, device="cuda", dtype=torch.int64) % 7 - 3 + rank + it).to(tdt)
+            y = torch.full_like(x, 55)
+            comm.allreduce(x, y, n, dt, "sum", topo_="1")
+            torch.cuda.synchronize()
+            want = sum((torch.arange(n, dtype=torch.int64) % 7 - 3 + r + it) for r in range(world)).to(tdt)
+            got = y.cpu()
+            if not torch.equal(got, want):
+                bad = int((got != want).sum())
+                res["fail"].append(f"write_race it={it} n={n} {dt}: {bad} elements differ, first "
+                                   f"{int(np.flatnonzero((got != want).numpy())[0])}")
+                continue   # keep making the calls: the peers would wait in them
+            res["write_race"] += 1
 
 
 def first_contact(comm, res, world, rank):

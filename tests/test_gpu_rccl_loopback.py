@@ -93,6 +93,18 @@ def test_ddp_comm_hook_over_rccl(world, dtype):
         assert not r["fail"] and r["ddp_hook_calls"] >= 3, r   # at least one bucket per step
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_peer_write_waits_for_every_copy_out(world):
+    """Consecutive peer-write calls over RCCL with the last rank's copy-out enqueued 150 ms late: a peer that
+    returned early would scatter its next call into that rank's exchange buffer before the copy-out read it
+    (found by tools/asan/engine_stress rccl, profiles/r04/asan_engine_stress_rccl_*.log)."""
+    env = {"FTAR_LOOPBACK_MODE": "write_race", "FTAR_LOOPBACK_LATE_RANK": str(world - 1)}
+    p, res = run_loopback(world, env)
+    assert p.returncode == 0 and len(res) == world, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
+    for r in res:
+        assert not r["fail"] and r["write_race"] == 8, r
+
+
 def test_first_contact_with_a_missing_peer_times_out():
     """the first call on an RCCL communicator runs the settings agreement and connects the peers on
     a helper thread with a deadline, so a peer that never calls fails the call with FTAR_ERR_TIMEOUT

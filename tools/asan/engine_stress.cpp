@@ -11,7 +11,13 @@
 // Results are checked too: inputs are small integers (exact in fp32 and bf16 and in every association
 // order), so the expected value of every element is the plain sum (or AND) whatever the schedule.
 //
-//   engine_stress [calls] [seed]      default 1500 calls, seed 1
+// The rccl mode runs the same random calls on P PROCESSES of one RCCL communicator each (one per rank,
+// loopback sockets between them, as tests/rccl_loopback_child.py), so the RCCL transport, the first-contact
+// helper thread, IPC maps of the other processes' exchange and registered buffers and communicator
+// re-creation run under the sanitizers too.
+//
+//   engine_stress [calls] [seed]               in-process groups, default 1500 calls, seed 1
+//   engine_stress rccl P calls seed [gens]     P processes, `gens` communicators one after the other
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -22,6 +28,10 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
 
 #include "ftar.h"
 
@@ -149,6 +159,37 @@ std::vector<Layout> layouts(int P) {
   }
 }
 
+// one random call; every rank of a multi-process run draws the same sequence, so the settings agree
+struct Case {
+  Layout L;
+  int form;
+  size_t chunk;
+  const Dt* d;
+  bool band;
+  size_t n;
+  bool host, oop, registered;
+};
+Case draw(std::mt19937_64& rng, int P, const std::vector<Layout>& lay, size_t reg_bytes) {
+  static const int forms[] = {FTAR_FORM_AUTO, FTAR_FORM_DIRECT, FTAR_FORM_STAGES, FTAR_FORM_COLLECTIVE,
+                              FTAR_FORM_PEER_READ, FTAR_FORM_PEER_WRITE};
+  static const size_t chunks[] = {0, 256, 4096 + 256, 1u << 16, 1u << 20};
+  Case k;
+  k.L = lay[rng() % lay.size()];
+  k.form = forms[rng() % 6];
+  k.chunk = chunks[rng() % 5];
+  k.d = &kDtypes[rng() % 6];
+  const bool integer = k.d->t == FTAR_INT32 || k.d->t == FTAR_UINT8 || k.d->t == FTAR_INT16;
+  k.band = integer && rng() % 3 == 0;
+  const size_t ragged = 1000 + rng() % 5000, big = 100000 + rng() % 300000;
+  const size_t sizes[] = {0, 1, (size_t)P - 1, (size_t)P + 1, ragged, big};
+  k.n = sizes[rng() % 6];
+  k.host = rng() % 4 == 0;
+  k.oop = rng() % 2 == 0;
+  k.registered = !k.host && k.oop && rng() % 3 == 0;
+  if (k.registered) k.n = std::min(k.n, reg_bytes / k.d->size);
+  return k;
+}
+
 struct Stats {
   long calls = 0, checked = 0, refused = 0, groups = 0, regs = 0;
 };
@@ -165,9 +206,6 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
   if (ftar_comm_init_local(comms.data(), P, devs.data()) != FTAR_SUCCESS) fail(std::string("init_local: ") + ftar_last_error());
   ++st->groups;
   const auto lay = layouts(P);
-  const int forms[] = {FTAR_FORM_AUTO, FTAR_FORM_DIRECT, FTAR_FORM_STAGES, FTAR_FORM_COLLECTIVE, FTAR_FORM_PEER_READ,
-                       FTAR_FORM_PEER_WRITE};
-  const size_t chunks[] = {0, 256, 4096 + 256, 1u << 16, 1u << 20};
   // registered device buffers (the peer forms' no-copy path): one pair per rank, registered collectively
   const size_t reg_bytes = 1u << 22;
   std::vector<void*> rx(P), ry(P);
@@ -190,17 +228,13 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
     st->regs += 2 * P;
   }
   for (int call = 0; call < calls; ++call) {
-    const Layout L = lay[rng() % lay.size()];
-    const int form = forms[rng() % 6];
-    const size_t chunk = chunks[rng() % 5];
-    const Dt& d = kDtypes[rng() % 6];
-    const bool band = (d.t == FTAR_INT32 || d.t == FTAR_UINT8 || d.t == FTAR_INT16) && rng() % 3 == 0;
-    const size_t sizes[] = {0, 1, (size_t)P - 1, (size_t)P + 1, 1000 + rng() % 5000, 100000 + rng() % 300000};
-    size_t n = sizes[rng() % 6];
-    const bool host = rng() % 4 == 0;
-    const bool oop = rng() % 2 == 0;
-    const bool registered = !host && oop && rng() % 3 == 0;
-    if (registered) n = std::min(n, reg_bytes / d.size);
+    const Case k = draw(rng, P, lay, reg_bytes);
+    const Layout L = k.L;
+    const int form = k.form;
+    const size_t chunk = k.chunk;
+    const Dt& d = *k.d;
+    const bool band = k.band, host = k.host, oop = k.oop, registered = k.registered;
+    const size_t n = k.n;
     ftar_topo_t topo;
     if (ftar_topo_parse(L.topo, L.lonely, P, &topo) != FTAR_SUCCESS) fail(std::string("topo_parse ") + L.topo);
     for (int r = 0; r < P; ++r) {
@@ -299,9 +333,188 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
   }
 }
 
+std::string show(const Dt& d, const uint8_t* p) {
+  char b[64];
+  switch (d.t) {
+    case FTAR_FLOAT32: { float f; memcpy(&f, p, 4); snprintf(b, sizeof b, "%g", f); break; }
+    case FTAR_BFLOAT16: { uint16_t h; memcpy(&h, p, 2); snprintf(b, sizeof b, "%g", from_bf16(h)); break; }
+    case FTAR_FLOAT64: { double f; memcpy(&f, p, 8); snprintf(b, sizeof b, "%g", f); break; }
+    case FTAR_INT32: { int32_t x; memcpy(&x, p, 4); snprintf(b, sizeof b, "%d", x); break; }
+    case FTAR_INT16: { int16_t x; memcpy(&x, p, 2); snprintf(b, sizeof b, "%d", x); break; }
+    default: snprintf(b, sizeof b, "%u", (unsigned)*p);
+  }
+  return b;
+}
+
+// ---- rccl mode: one process per rank ---------------------------------------------------------------------
+
+bool read_all(int fd, void* p, size_t n) {
+  auto* b = (uint8_t*)p;
+  while (n) {
+    const ssize_t k = read(fd, b, n);
+    if (k <= 0) return false;
+    b += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+// rank r of P: `gens` communicators in turn, `calls` random calls on each; ids[q] is the pipe rank 0 writes
+// each generation's unique id to for rank q
+int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std::vector<int>& id_pipes) {
+  const std::string host = "ftar-stress-" + std::to_string(r);
+  setenv("NCCL_HOSTID", host.c_str(), 1);
+  setenv("NCCL_SOCKET_IFNAME", "lo", 1);
+  setenv("NCCL_IB_DISABLE", "1", 1);
+  HIP_OK(hipSetDevice(0));
+  std::mt19937_64 rng(seed);  // the same sequence on every rank
+  const auto lay = layouts(P);
+  const size_t reg_bytes = 1u << 22;
+  long checked = 0, refused = 0;
+  for (int g = 0; g < gens; ++g) {
+    ftar_unique_id_t id;
+    if (r == 0) {
+      if (ftar_get_unique_id(&id) != FTAR_SUCCESS) fail(std::string("get_unique_id: ") + ftar_last_error());
+      for (int q = 1; q < P; ++q)
+        if (write(id_pipes[q], &id, sizeof id) != (ssize_t)sizeof id) fail("id pipe write");
+    } else if (!read_all(id_pipes[r], &id, sizeof id)) {
+      fail("id pipe read");
+    }
+    ftar_comm_t c;
+    if (ftar_comm_init_rank(&c, P, id, r, 0) != FTAR_SUCCESS) fail(std::string("init_rank: ") + ftar_last_error());
+    void *rx, *ry;
+    int idx, idy;
+    HIP_OK(hipMalloc(&rx, reg_bytes));
+    HIP_OK(hipMalloc(&ry, reg_bytes));
+    if (ftar_comm_register(c, rx, reg_bytes, &idx) != FTAR_SUCCESS ||
+        ftar_comm_register(c, ry, reg_bytes, &idy) != FTAR_SUCCESS)
+      fail(std::string("register: ") + ftar_last_error());
+    for (long call = 0; call < calls; ++call) {
+      const Case k = draw(rng, P, lay, reg_bytes);
+      const Dt& d = *k.d;
+      const size_t bytes = k.n * d.size;
+      ftar_topo_t topo;
+      if (ftar_topo_parse(k.L.topo, k.L.lonely, P, &topo) != FTAR_SUCCESS) fail("topo_parse");
+      if (ftar_comm_set_form(c, k.form) != FTAR_SUCCESS || ftar_comm_set_chunk_bytes(c, k.chunk) != FTAR_SUCCESS ||
+          ftar_comm_set_host_chunk_bytes(c, k.chunk) != FTAR_SUCCESS)
+        fail("setters");
+      std::vector<uint8_t> in, hout;
+      fill(in, d, k.n, r, k.band);
+      void *send = nullptr, *recv = nullptr, *a = nullptr, *b = nullptr;
+      if (k.host) {
+        hout.assign(bytes, 0x5a);
+        send = k.oop ? (void*)in.data() : nullptr;
+        recv = k.oop ? (void*)hout.data() : (void*)in.data();
+        if (!bytes) send = recv = nullptr;
+      } else {
+        if (k.registered) {
+          a = rx;
+          b = ry;
+        } else {
+          HIP_OK(hipMalloc(&a, bytes ? bytes : 1));
+          if (k.oop) HIP_OK(hipMalloc(&b, bytes ? bytes : 1));
+        }
+        if (bytes) HIP_OK(hipMemcpy(a, in.data(), bytes, hipMemcpyHostToDevice));
+        if (k.oop && bytes) HIP_OK(hipMemset(b, 0x5a, bytes));
+        send = k.oop ? a : nullptr;
+        recv = k.oop ? b : a;
+      }
+      const ftar_op_t op = k.band ? FTAR_BAND : FTAR_SUM;
+      const ftar_status_t s = k.host ? ftar_allreduce_host(send, recv, k.n, d.t, op, &topo, c, nullptr)
+                                     : ftar_allreduce(send, recv, k.n, d.t, op, &topo, c, nullptr);
+      HIP_OK(hipDeviceSynchronize());
+      char what[256];
+      snprintf(what, sizeof what, "rank %d gen %d call %ld: topo=%s+%s form=%d chunk=%zu %s %s n=%zu host=%d oop=%d "
+               "reg=%d", r, g, call, k.L.topo, k.L.lonely ? k.L.lonely : "0", k.form, k.chunk, d.name,
+               k.band ? "band" : "sum", k.n, k.host, k.oop, k.registered);
+      if (s != FTAR_SUCCESS) fail(std::string(what) + ": " + ftar_status_string(s) + ": " + ftar_last_error());
+      std::vector<uint8_t> got(bytes), want;
+      if (k.host) got = k.oop ? hout : in;
+      else if (bytes) HIP_OK(hipMemcpy(got.data(), recv, bytes, hipMemcpyDeviceToHost));
+      expect(want, d, k.n, P, k.band);
+      if (got != want) {
+        std::string diff;
+        int shown = 0;
+        for (size_t i = 0; i < k.n && shown < 12; ++i)
+          if (memcmp(&got[i * d.size], &want[i * d.size], d.size)) {
+            diff += " [" + std::to_string(i) + "] got " + show(d, &got[i * d.size]) + " want " +
+                    show(d, &want[i * d.size]);
+            ++shown;
+          }
+        fail(std::string(what) + ": differs from the exact result:" + diff);
+      }
+      ++checked;
+      if (!k.host && !k.registered) {
+        HIP_OK(hipFree(a));
+        if (b) HIP_OK(hipFree(b));
+      }
+    }
+    // refused alike on every rank before anything is enqueued; the communicator stays usable
+    if (ftar_allreduce(nullptr, rx, 64, FTAR_FLOAT32, FTAR_BAND, nullptr, c, nullptr) != FTAR_ERR_UNSUPPORTED)
+      fail("BAND on fp32 not refused");
+    ++refused;
+    ftar_comm_deregister(c, idx);
+    ftar_comm_deregister(c, idy);
+    if (ftar_comm_destroy(c) != FTAR_SUCCESS) fail(std::string("destroy: ") + ftar_last_error());
+    HIP_OK(hipFree(rx));
+    HIP_OK(hipFree(ry));
+  }
+  printf("{\"rank\": %d, \"checked\": %ld, \"refused\": %ld, \"communicators\": %d}\n", r, checked, refused, gens);
+  fflush(stdout);
+  HIP_OK(hipDeviceSynchronize());
+  _Exit(0);  // as in main: no HIP runtime static teardown under the sanitizer
+}
+
+// forks the P ranks BEFORE anything in this process touches HIP; returns 0 when every rank exits 0
+int rccl_main(int P, long calls, unsigned long seed, int gens) {
+  std::vector<int> rd(P, -1), wr(P, -1);
+  for (int q = 1; q < P; ++q) {
+    int fd[2];
+    if (pipe(fd)) fail("pipe");
+    rd[q] = fd[0];
+    wr[q] = fd[1];
+  }
+  std::vector<pid_t> pids;
+  for (int r = 0; r < P; ++r) {
+    const pid_t pid = fork();
+    if (pid < 0) fail("fork");
+    if (pid == 0) {
+      std::vector<int> mine(P, -1);
+      for (int q = 1; q < P; ++q) mine[q] = r == 0 ? wr[q] : (q == r ? rd[q] : -1);
+      return rccl_rank(r, P, calls, seed, gens, mine);
+    }
+    pids.push_back(pid);
+  }
+  // the first rank to fail ends the run: its peers would wait for it in their next call forever
+  int worst = 0;
+  size_t left = pids.size();
+  while (left) {
+    int status = 0;
+    const pid_t pid = waitpid(-1, &status, 0);
+    if (pid < 0) break;
+    --left;
+    const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + WTERMSIG(status);
+    worst = std::max(worst, code);
+    if (code) {
+      usleep(500000);  // let the other ranks report the same call
+      for (pid_t q : pids)
+        if (q != pid) kill(q, SIGKILL);
+    }
+  }
+  printf("rccl: P=%d calls=%ld seed=%lu communicators=%d: %s\n", P, calls, seed, gens, worst ? "FAILED" : "ok");
+  return worst;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "rccl")) {
+    if (argc < 5) {
+      fprintf(stderr, "usage: engine_stress rccl P calls seed [gens]\n");
+      return 2;
+    }
+    return rccl_main(atoi(argv[2]), atol(argv[3]), strtoul(argv[4], nullptr, 0), argc > 5 ? atoi(argv[5]) : 2);
+  }
   const long total = argc > 1 ? atol(argv[1]) : 1500;
   const unsigned long seed = argc > 2 ? strtoul(argv[2], nullptr, 0) : 1;
   HIP_OK(hipSetDevice(0));
