@@ -242,7 +242,7 @@ def test_peer_write_in_place_and_out_of_place_repeats():
     ("read", "2,2", ["start", "copy-in", "barrier", "fold (remote reads)", "barrier", "gather (remote reads)",
                      "barrier"]),
     ("write", "4", ["start", "scatter (remote writes)", "barrier", "fold (local)", "push (remote writes)",
-                    "barrier", "copy-out"])])
+                    "barrier", "copy-out", "barrier"])])
 def test_phase_timing(mode, topo, names):
     """ftar_comm_set_phase_timing / ftar_comm_phase_json: the phases of the last call, in issue order."""
     import threading

@@ -444,6 +444,10 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
         fail(std::string(what) + ": differs from the exact result:" + diff);
       }
       ++checked;
+      if (r == 0 && checked % 25 == 0) {  // progress (a silent run is taken to be hung)
+        printf("progress: rank 0 gen %d, %ld calls checked\n", g, checked);
+        fflush(stdout);
+      }
       if (!k.host && !k.registered) {
         HIP_OK(hipFree(a));
         if (b) HIP_OK(hipFree(b));
