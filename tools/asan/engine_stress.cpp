@@ -18,6 +18,8 @@
 //
 //   engine_stress [calls] [seed]               in-process groups, default 1500 calls, seed 1
 //   engine_stress rccl P calls seed [gens]     P processes, `gens` communicators one after the other
+//   engine_stress host P calls seed [gens]     the same on ftar_comm_init_host (shared-memory bootstrap,
+//                                              peer forms only)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -29,7 +31,9 @@
 #include <thread>
 #include <vector>
 
+#include <pthread.h>
 #include <signal.h>
+#include <sys/mman.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -359,9 +363,32 @@ bool read_all(int fd, void* p, size_t n) {
   return true;
 }
 
-// rank r of P: `gens` communicators in turn, `calls` random calls on each; ids[q] is the pipe rank 0 writes
-// each generation's unique id to for rank q
-int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std::vector<int>& id_pipes) {
+// the host transport's bootstrap collective (ftar_comm_init_host): an all-gather through memory shared by
+// the forked ranks, two process-shared barriers per call
+struct Shm {
+  pthread_barrier_t bar;
+  size_t cap;
+  char data[1];
+};
+struct HostCtx {
+  Shm* shm;
+  int rank, P;
+};
+int shm_allgather(const void* mine, void* all, size_t bytes, void* user) {
+  auto* h = static_cast<HostCtx*>(user);
+  if (bytes * (size_t)h->P > h->shm->cap) return 1;
+  memcpy(h->shm->data + (size_t)h->rank * bytes, mine, bytes);
+  pthread_barrier_wait(&h->shm->bar);
+  memcpy(all, h->shm->data, bytes * (size_t)h->P);
+  pthread_barrier_wait(&h->shm->bar);
+  return 0;
+}
+
+// rank r of P: `gens` communicators in turn, `calls` random calls on each.  rccl: ids[q] is the pipe rank 0
+// writes each generation's unique id to for rank q.  host (shm != null): ftar_comm_init_host over the shared
+// memory all-gather; that transport moves data by the peer forms only, on one-round plans
+int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std::vector<int>& id_pipes,
+              Shm* shm = nullptr) {
   const std::string host = "ftar-stress-" + std::to_string(r);
   setenv("NCCL_HOSTID", host.c_str(), 1);
   setenv("NCCL_SOCKET_IFNAME", "lo", 1);
@@ -372,16 +399,22 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
   const size_t reg_bytes = 1u << 22;
   long checked = 0, refused = 0;
   for (int g = 0; g < gens; ++g) {
-    ftar_unique_id_t id;
-    if (r == 0) {
-      if (ftar_get_unique_id(&id) != FTAR_SUCCESS) fail(std::string("get_unique_id: ") + ftar_last_error());
-      for (int q = 1; q < P; ++q)
-        if (write(id_pipes[q], &id, sizeof id) != (ssize_t)sizeof id) fail("id pipe write");
-    } else if (!read_all(id_pipes[r], &id, sizeof id)) {
-      fail("id pipe read");
-    }
     ftar_comm_t c;
-    if (ftar_comm_init_rank(&c, P, id, r, 0) != FTAR_SUCCESS) fail(std::string("init_rank: ") + ftar_last_error());
+    HostCtx hctx{shm, r, P};
+    if (shm) {
+      if (ftar_comm_init_host(&c, P, r, 0, shm_allgather, &hctx) != FTAR_SUCCESS)
+        fail(std::string("init_host: ") + ftar_last_error());
+    } else {
+      ftar_unique_id_t id;
+      if (r == 0) {
+        if (ftar_get_unique_id(&id) != FTAR_SUCCESS) fail(std::string("get_unique_id: ") + ftar_last_error());
+        for (int q = 1; q < P; ++q)
+          if (write(id_pipes[q], &id, sizeof id) != (ssize_t)sizeof id) fail("id pipe write");
+      } else if (!read_all(id_pipes[r], &id, sizeof id)) {
+        fail("id pipe read");
+      }
+      if (ftar_comm_init_rank(&c, P, id, r, 0) != FTAR_SUCCESS) fail(std::string("init_rank: ") + ftar_last_error());
+    }
     void *rx, *ry;
     int idx, idy;
     HIP_OK(hipMalloc(&rx, reg_bytes));
@@ -390,7 +423,11 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
         ftar_comm_register(c, ry, reg_bytes, &idy) != FTAR_SUCCESS)
       fail(std::string("register: ") + ftar_last_error());
     for (long call = 0; call < calls; ++call) {
-      const Case k = draw(rng, P, lay, reg_bytes);
+      Case k = draw(rng, P, lay, reg_bytes);
+      if (shm) {  // the host transport: peer forms on one-round plans (no lonely ranks)
+        k.form = (k.form & 1) ? FTAR_FORM_PEER_READ : FTAR_FORM_PEER_WRITE;
+        if (k.L.lonely) k.L = {"1", nullptr};
+      }
       const Dt& d = *k.d;
       const size_t bytes = k.n * d.size;
       ftar_topo_t topo;
@@ -470,7 +507,19 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
 }
 
 // forks the P ranks BEFORE anything in this process touches HIP; returns 0 when every rank exits 0
-int rccl_main(int P, long calls, unsigned long seed, int gens) {
+int rccl_main(int P, long calls, unsigned long seed, int gens, bool host = false) {
+  Shm* shm = nullptr;
+  if (host) {
+    const size_t cap = 4u << 20;
+    void* m = mmap(nullptr, sizeof(Shm) + cap, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) fail("mmap");
+    shm = static_cast<Shm*>(m);
+    shm->cap = cap;
+    pthread_barrierattr_t a;
+    pthread_barrierattr_init(&a);
+    pthread_barrierattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+    pthread_barrier_init(&shm->bar, &a, (unsigned)P);
+  }
   std::vector<int> rd(P, -1), wr(P, -1);
   for (int q = 1; q < P; ++q) {
     int fd[2];
@@ -485,7 +534,7 @@ int rccl_main(int P, long calls, unsigned long seed, int gens) {
     if (pid == 0) {
       std::vector<int> mine(P, -1);
       for (int q = 1; q < P; ++q) mine[q] = r == 0 ? wr[q] : (q == r ? rd[q] : -1);
-      return rccl_rank(r, P, calls, seed, gens, mine);
+      return rccl_rank(r, P, calls, seed, gens, mine, shm);
     }
     pids.push_back(pid);
   }
@@ -505,19 +554,21 @@ int rccl_main(int P, long calls, unsigned long seed, int gens) {
         if (q != pid) kill(q, SIGKILL);
     }
   }
-  printf("rccl: P=%d calls=%ld seed=%lu communicators=%d: %s\n", P, calls, seed, gens, worst ? "FAILED" : "ok");
+  printf("%s: P=%d calls=%ld seed=%lu communicators=%d: %s\n", host ? "host" : "rccl", P, calls, seed, gens,
+         worst ? "FAILED" : "ok");
   return worst;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc > 1 && !strcmp(argv[1], "rccl")) {
+  if (argc > 1 && (!strcmp(argv[1], "rccl") || !strcmp(argv[1], "host"))) {
     if (argc < 5) {
-      fprintf(stderr, "usage: engine_stress rccl P calls seed [gens]\n");
+      fprintf(stderr, "usage: engine_stress rccl|host P calls seed [gens]\n");
       return 2;
     }
-    return rccl_main(atoi(argv[2]), atol(argv[3]), strtoul(argv[4], nullptr, 0), argc > 5 ? atoi(argv[5]) : 2);
+    return rccl_main(atoi(argv[2]), atol(argv[3]), strtoul(argv[4], nullptr, 0), argc > 5 ? atoi(argv[5]) : 2,
+                     !strcmp(argv[1], "host"));
   }
   const long total = argc > 1 ? atol(argv[1]) : 1500;
   const unsigned long seed = argc > 2 ? strtoul(argv[2], nullptr, 0) : 1;
