@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <random>
 #include <string>
 #include <thread>
@@ -146,21 +147,55 @@ void expect(std::vector<uint8_t>& out, const Dt& d, size_t n, int P, bool band) 
   }
 }
 
-// valid layouts (lonely L with S = P - L ranks in >= 2 stages and L * w0 <= S, as tests/random_cases.py)
+// every valid layout of P: the ring, each ordered factorization, and lonely L with S = P - L ranks in >= 2
+// stages and L * w0 <= S (as tests/random_cases.py)
 struct Layout {
   const char* topo;
   const char* lonely;
 };
-std::vector<Layout> layouts(int P) {
-  switch (P) {
-    case 2: return {{"1", nullptr}, {"2", nullptr}};
-    case 3: return {{"1", nullptr}, {"3", nullptr}};
-    case 4: return {{"1", nullptr}, {"4", nullptr}, {"2,2", nullptr}};
-    case 5: return {{"1", nullptr}, {"5", nullptr}, {"2,2", "1"}};
-    case 6: return {{"1", nullptr}, {"2,3", nullptr}, {"3,2", nullptr}, {"6", nullptr}, {"2,2", "2"}};
-    default: return {{"1", nullptr}, {"8", nullptr}, {"2,4", nullptr}, {"4,2", nullptr}, {"2,2,2", nullptr},
-                     {"3,2", "2"}};
+void factorizations(int n, std::vector<int>& cur, std::vector<std::vector<int>>& out) {
+  if (n == 1) {
+    if (!cur.empty()) out.push_back(cur);
+    return;
   }
+  for (int f = 2; f <= n; ++f)
+    if (n % f == 0) {
+      cur.push_back(f);
+      factorizations(n / f, cur, out);
+      cur.pop_back();
+    }
+}
+std::vector<Layout> layouts(int P) {
+  static std::deque<std::string> keep;  // the strings the layouts point at (stable, never freed)
+  auto str = [](const std::vector<int>& f) {
+    std::string t;
+    for (int w : f) t += (t.empty() ? "" : ",") + std::to_string(w);
+    return t;
+  };
+  std::vector<std::pair<std::string, int>> opts = {{"1", 0}};
+  std::vector<int> cur;
+  std::vector<std::vector<int>> fs;
+  factorizations(P, cur, fs);
+  for (auto& f : fs)
+    if (f.size() <= 4) opts.push_back({str(f), 0});
+  for (int L = 1; L < P; ++L) {
+    std::vector<std::vector<int>> gs;
+    factorizations(P - L, cur, gs);
+    for (auto& f : gs)
+      if (f.size() >= 2 && f.size() <= 4 && L * f[0] <= P - L) opts.push_back({str(f), L});
+  }
+  std::vector<Layout> out;
+  for (auto& o : opts) {
+    keep.push_back(o.first);
+    const char* t = keep.back().c_str();
+    const char* l = nullptr;
+    if (o.second) {
+      keep.push_back(std::to_string(o.second));
+      l = keep.back().c_str();
+    }
+    out.push_back({t, l});
+  }
+  return out;
 }
 
 // one random call; every rank of a multi-process run draws the same sequence, so the settings agree
@@ -200,7 +235,8 @@ struct Stats {
 
 int fail(const std::string& what) {
   fprintf(stderr, "FAIL %s\n", what.c_str());
-  exit(1);
+  fflush(stderr);
+  _Exit(1);  // no HIP runtime static teardown under the sanitizer (see main)
 }
 
 // one group: `calls` random calls, then destroyed
