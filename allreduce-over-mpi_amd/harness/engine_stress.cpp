@@ -1,12 +1,15 @@
-// The engine's HOST code under AddressSanitizer + UndefinedBehaviorSanitizer, driven on a real GPU.
+// Random AllReduce calls through the engine's paths, every result checked, as a stress driver of its HOST
+// code: every data-movement form, the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty
+// and ragged buckets, six dtypes with SUM and BAND, device and host buffers, in place and out of place,
+// registered buffers for the peer forms, error paths, and groups and communicators created and destroyed
+// repeatedly.
 //
-// libftar.so is rebuilt with the host sanitizers only (tools/asan/Makefile: clang++ for the host translation
-// units, hipcc with -fno-gpu-sanitize for the kernels, whose device code is untouched) and this program
-// drives in-process groups (ftar_comm_init_local) through the engine's paths: every data-movement form,
-// the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty and ragged buckets, device and
-// host buffers, in place and out of place, registered buffers for the peer forms, error paths, and groups
-// created and destroyed repeatedly.  Any heap misuse, use after free, double free or undefined behaviour in
-// plan caches, event pools, IPC maps, the local hub or the execution-model cache aborts the run.
+// Built two ways: plainly against lib/libftar.so (csrc/Makefile: lib/ftar_engine_stress, run by
+// tests/test_gpu_engine_stress.py), and against a libftar.so rebuilt with the host sanitizers only
+// (tools/asan/Makefile: clang++ -fsanitize=address,undefined for the host translation units, hipcc with
+// -fno-gpu-sanitize for the kernels, whose device code is untouched), where any heap misuse, use after free,
+// double free or undefined behaviour in plan caches, event pools, IPC maps, the local hub or the
+// execution-model cache aborts the run.
 //
 // Results are checked too: inputs are small integers (exact in fp32 and bf16 and in every association
 // order), so the expected value of every element is the plain sum (or AND) whatever the schedule.

@@ -1,0 +1,37 @@
+"""The engine stress driver (allreduce-over-mpi_amd/harness/engine_stress.cpp, built as lib/ftar_engine_stress)
+on the production library: seeded random calls with every result checked against the exact sum of
+small-integer inputs -- in-process groups created and destroyed (P = 2..8), and P processes of one RCCL
+communicator or of the host-bootstrapped transport each (loopback sockets; two communicators in turn).  The
+same source built against a host-sanitized libftar.so is tools/asan/ (profiles/r04/asan_*.log); the RCCL mode
+found the peer-write race that test_peer_write_waits_for_every_copy_out now pins."""
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib", "ftar_engine_stress")
+
+
+def _run(args, timeout):
+    env = dict(os.environ, NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    p = subprocess.run([EXE] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout, env=env)
+    return p
+
+
+def test_in_process_groups():
+    p = _run([1200, 5], 240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    stats = json.loads(p.stdout.strip().splitlines()[-1])
+    assert stats["checked"] == stats["calls"] >= 1200 and stats["groups"] >= 20, stats
+
+
+@pytest.mark.parametrize("mode,P,calls,seed", [("rccl", 4, 120, 41), ("rccl", 8, 80, 12), ("host", 4, 120, 43)])
+def test_processes(mode, P, calls, seed):
+    p = _run([mode, P, calls, seed, 2], 240)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    ranks = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith('{"rank"')]
+    assert len(ranks) == P and all(r["checked"] == 2 * calls for r in ranks), ranks
+    assert f"{mode}: P={P}" in p.stdout and p.stdout.rstrip().endswith("ok"), p.stdout[-500:]
