@@ -1191,7 +1191,7 @@ ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_d
   // serial capture: every internal stream is the caller's for this call, so the captured graph is one
   // chain in issue order (every wait refers to an event recorded earlier in that order, so the chain keeps
   // every dependency; the comm/reduce overlap is given up inside the graph)
-  const bool serial = capturing && serial_capture();
+  const bool serial = capturing && (serial_capture() || c->tp->capture_serially());
   if (host) FTAR_RETURN_IF(ensure_host_streams(c));
   hipStream_t saved[4] = {c->comm_s, c->red_s, c->h2d_s, c->d2h_s};
   if (serial) c->comm_s = c->red_s = c->h2d_s = c->d2h_s = stream;
@@ -1861,9 +1861,8 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
   std::vector<ftar_status_t> st(nranks, FTAR_SUCCESS);
   std::vector<std::string> why(nranks);
   std::vector<std::thread> th;
-  // Capturing streams (the caller forked every rank's stream from one capture):
-  // the ranks' threads take turns issuing (Transport::capture_enter), and nobody
-  // synchronises; the caller joins the streams back and ends the capture.
+  // Capturing streams (the caller's capture stream for every rank): the ranks' threads take turns issuing
+  // (Transport::capture_enter), and nobody synchronises; the caller ends the capture.
   bool capturing = false;
   if (streams && streams[0]) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -1871,6 +1870,18 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
     FTAR_CHECK_HIP(hipStreamIsCapturing(static_cast<hipStream_t>(streams[0]), &cs));
     capturing = cs != hipStreamCaptureStatusNone;
   }
+  // Under capture every rank's call goes on the caller's capture stream itself.  A stream forked per rank
+  // from the capture makes HIP's hipStreamEndCapture recurse without end at every P probed, 7.0 and 7.2 alike,
+  // even when ftar funnels the ranks onto one of those streams (tools/capture/depth_probe.sh,
+  // profiles/r04/capture_depth_probe.log): refused here rather than crashing the caller at its end of capture.
+  if (capturing)
+    for (int r = 1; r < nranks; ++r)
+      if (streams[r] != streams[0]) {
+        ftar::set_error("ftar_allreduce_group under stream capture: pass the capture stream itself for every rank "
+                        "(streams forked per rank make hipStreamEndCapture recurse without end)",
+                        __FILE__, __LINE__);
+        return FTAR_ERR_UNSUPPORTED;
+      }
   for (int r = 0; r < nranks; ++r)
     th.emplace_back([&, r] {
       hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;

@@ -256,6 +256,11 @@ class Transport {
   // peer), so the one capture graph is built by one host thread at a time.
   virtual void capture_enter() {}
   virtual void capture_leave() {}
+  // A captured call issues serially on the caller's stream whatever the runtime (serial_capture, engine.cpp):
+  // the in-process group.  Its ranks' forked comm/reduce streams, cross-waiting through the hub's events, make
+  // HIP 7.2's hipStreamEndCapture recurse without end from P = 3 on (tools/capture/depth_probe.sh; P = 2
+  // ends), while the serial form ends at every P, layout and piece size probed.
+  virtual bool capture_serially() const { return false; }
   // Called by every rank before it joins its internal streams back into the
   // caller's stream.  Under capture the local transport makes the ranks meet
   // here first: HIP's capture breaks (hipStreamEndCapture recurses without

@@ -648,6 +648,7 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   const char* name() const override { return "local"; }
+  bool capture_serially() const override { return true; }
   void capture_enter() override {
     hub_->issue.lock();
     t_issue_held = true;

@@ -1,8 +1,8 @@
 // Random AllReduce calls through the engine's paths, every result checked, as a stress driver of its HOST
 // code: every data-movement form, the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty
 // and ragged buckets, six dtypes with SUM and BAND, device and host buffers, in place and out of place,
-// registered buffers for the peer forms, error paths, and groups and communicators created and destroyed
-// repeatedly.
+// registered buffers for the peer forms, calls captured into HIP graphs and replayed (in-process groups),
+// error paths, and groups and communicators created and destroyed repeatedly.
 //
 // Built two ways: plainly against lib/libftar.so (csrc/Makefile: lib/ftar_engine_stress, run by
 // tests/test_gpu_engine_stress.py), and against a libftar.so rebuilt with the host sanitizers only
@@ -94,9 +94,10 @@ void fill(std::vector<uint8_t>& b, const Dt& d, size_t n, int r, bool band) {
 }
 
 // the expected result (every rank): sum or AND of the P inputs, in the element type
-void expect(std::vector<uint8_t>& out, const Dt& d, size_t n, int P, bool band) {
+// (off: the inputs of ranks off .. off + P - 1, for the graph replays' fresh inputs)
+void expect(std::vector<uint8_t>& out, const Dt& d, size_t n, int P, bool band, int off = 0) {
   std::vector<std::vector<uint8_t>> ins(P);
-  for (int r = 0; r < P; ++r) fill(ins[r], d, n, r, band);
+  for (int r = 0; r < P; ++r) fill(ins[r], d, n, r + off, band);
   out.assign(n * d.size, 0);
   for (size_t i = 0; i < n; ++i) {
     switch (d.t) {
@@ -233,13 +234,59 @@ Case draw(std::mt19937_64& rng, int P, const std::vector<Layout>& lay, size_t re
 }
 
 struct Stats {
-  long calls = 0, checked = 0, refused = 0, groups = 0, regs = 0;
+  long calls = 0, checked = 0, refused = 0, groups = 0, regs = 0, captured = 0;
 };
 
 int fail(const std::string& what) {
   fprintf(stderr, "FAIL %s\n", what.c_str());
   fflush(stderr);
   _Exit(1);  // no HIP runtime static teardown under the sanitizer (see main)
+}
+
+// The call just made, captured into a HIP graph (relaxed mode; every rank's call on the capture stream, the
+// form the HIP runtime ends: a stream forked per rank from the capture stream makes hipStreamEndCapture recurse
+// without end, DESIGN §4 and profiles/r03/capture) and replayed twice on fresh inputs in the same buffers; the
+// uncaptured call before it grew every buffer the plan needs
+void capture_replay(int P, std::vector<ftar_comm_t>& comms, std::vector<void*>& send, std::vector<void*>& recv,
+                    size_t n, const Dt& d, ftar_op_t op, bool band, const ftar_topo_t* topo, bool oop,
+                    const std::string& what, Stats* st) {
+  const size_t bytes = n * d.size;
+  if (getenv("FTAR_STRESS_VERBOSE")) {
+    fprintf(stderr, "capture: %s\n", what.c_str());
+    fflush(stderr);
+  }
+  hipStream_t s0;
+  HIP_OK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  HIP_OK(hipStreamBeginCapture(s0, hipStreamCaptureModeRelaxed));
+  std::vector<void*> rsv(P, (void*)s0);
+  const ftar_status_t s = ftar_allreduce_group(oop ? send.data() : nullptr, recv.data(), n, d.t, op, topo,
+                                               comms.data(), P, rsv.data());
+  const std::string err = s == FTAR_SUCCESS ? "" : ftar_last_error();
+  hipGraph_t g = nullptr;
+  const hipError_t e = hipStreamEndCapture(s0, &g);
+  if (s != FTAR_SUCCESS) fail(what + ": captured call: " + ftar_status_string(s) + ": " + err);
+  if (e != hipSuccess) fail(what + ": hipStreamEndCapture: " + hipGetErrorString(e));
+  hipGraphExec_t x;
+  HIP_OK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+  for (int rep = 1; rep <= 2; ++rep) {
+    std::vector<uint8_t> in, want, got(bytes);
+    for (int r = 0; r < P; ++r) {
+      fill(in, d, n, r + 7 * rep, band);
+      HIP_OK(hipMemcpy(oop ? send[r] : recv[r], in.data(), bytes, hipMemcpyHostToDevice));
+      if (oop) HIP_OK(hipMemset(recv[r], 0x5a, bytes));
+    }
+    HIP_OK(hipGraphLaunch(x, s0));
+    HIP_OK(hipStreamSynchronize(s0));
+    expect(want, d, n, P, band, 7 * rep);
+    for (int r = 0; r < P; ++r) {
+      HIP_OK(hipMemcpy(got.data(), recv[r], bytes, hipMemcpyDeviceToHost));
+      if (got != want) fail(what + ": graph replay " + std::to_string(rep) + ": rank " + std::to_string(r) + " differs");
+    }
+  }
+  ++st->captured;
+  HIP_OK(hipGraphExecDestroy(x));
+  HIP_OK(hipGraphDestroy(g));
+  HIP_OK(hipStreamDestroy(s0));
 }
 
 // one group: `calls` random calls, then destroyed
@@ -344,6 +391,8 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
       }
     }
     ++st->checked;
+    // now and then the same call again, captured into a graph and replayed
+    if (!host && bytes && rng() % 8 == 0) capture_replay(P, comms, send, recv, n, d, op, band, &topo, oop, what, st);
     for (void* p : owned) HIP_OK(hipFree(p));
   }
   // error paths: refused before anything is enqueued, the group stays usable
@@ -627,8 +676,9 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   }
-  printf("{\"calls\": %ld, \"checked\": %ld, \"refused\": %ld, \"groups\": %ld, \"registrations\": %ld, \"seed\": %lu}\n",
-         st.calls, st.checked, st.refused, st.groups, st.regs, seed);
+  printf("{\"calls\": %ld, \"checked\": %ld, \"captured\": %ld, \"refused\": %ld, \"groups\": %ld, "
+         "\"registrations\": %ld, \"seed\": %lu}\n",
+         st.calls, st.checked, st.captured, st.refused, st.groups, st.regs, seed);
   fflush(stdout);
   // every group is destroyed and the device drained; skip the HIP runtime's static teardown, where the
   // sanitizer's own HIP allocator hooks trip a CHECK once the runtime has unloaded (not ftar code)

@@ -337,7 +337,11 @@ ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg);
 ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
                              const ftar_topo_t* topo, ftar_comm_t comm, void* stream);
 /* Drive every rank of an ftar_comm_init_local group from this one call
- * (one internal host thread per rank); blocks until all ranks are done. */
+ * (one internal host thread per rank); blocks until all ranks are done.
+ * Under stream capture pass the capture stream itself for every rank (the
+ * call is then captured serially, one graph chain); streams forked per rank
+ * from the capture are refused with FTAR_ERR_UNSUPPORTED, as HIP's
+ * hipStreamEndCapture recurses without end on them. */
 ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
                                    ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,
                                    int nranks, void* const* streams);

@@ -462,20 +462,36 @@ def _capture_in_child(tmp_path, P, topo, rs, ag, chunk, shared, n=10007, replays
             assert got[f"it{it}_r{r}"].tobytes() == ref[r].tobytes(), (it, r)
 
 
-@pytest.mark.parametrize("topo", ["1", "2"])
-def test_allreduce_group_captures_into_a_hip_graph(topo):
-    """A whole 2-rank in-process group AllReduce (ring or tree(2), one piece per block) captured into ONE HIP
-    graph from plain C++ on the HIP runtime of /opt/rocm (allreduce-over-mpi_amd/lib/ftar_capture_check:
+@pytest.mark.parametrize("P,topo,n,chunk", [(2, "1", 10007, 0), (2, "2", 10007, 0), (3, "3", 2, 0),
+                                            (3, "1", 3000, 0), (4, "2,2", 3000, 4096), (8, "8", 100003, 0),
+                                            (8, "1", 100003, 4096)])
+def test_allreduce_group_captures_into_a_hip_graph(P, topo, n, chunk):
+    """A whole in-process group AllReduce (P = 2..8, rings and trees, whole blocks and 4 KiB pieces) captured into
+    ONE HIP graph from plain C++ on the HIP runtime of /opt/rocm (allreduce-over-mpi_amd/lib/ftar_capture_check:
     hipStreamBeginCapture relaxed on s0, every rank's call on s0, hipGraphInstantiate) and replayed three times
     on fresh inputs: every replay's outputs are bit-identical to an uncaptured call on the same inputs.  The
     ranks' host threads take turns issuing (Transport::capture_enter), every record under capture uses a fresh
     event, the ranks meet before joining their internal streams back, and nothing allocates or synchronises
-    under capture (a warm-up call sizes the buffers)."""
+    under capture (a warm-up call sizes the buffers).  In-process groups capture serially on every runtime
+    (LocalTransport::capture_serially): with forked internal streams hipStreamEndCapture (7.2) recursed
+    without end from P = 3 on (tools/capture/depth_probe.sh, found by the engine stress driver)."""
     import subprocess
     exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "allreduce-over-mpi_amd", "lib",
                        "ftar_capture_check")
-    p = subprocess.run([exe, "2", topo, "10007", "0", "shared"], capture_output=True, text=True, timeout=120)
+    p = subprocess.run([exe, str(P), topo, str(n), str(chunk), "shared"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "group capture ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-3000:])
+
+
+def test_allreduce_group_capture_refuses_streams_forked_per_rank():
+    """A stream forked per rank from the capture makes hipStreamEndCapture recurse without end (HIP 7.0 and 7.2,
+    every P probed: tools/capture/depth_probe.sh): the group call refuses it with FTAR_ERR_UNSUPPORTED and a
+    message instead of the caller crashing at the end of its capture."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "allreduce-over-mpi_amd", "lib",
+                       "ftar_capture_check")
+    p = subprocess.run([exe, "3", "1", "3000", "0"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 3 and "pass the capture stream itself for every rank" in p.stderr, (p.returncode,
+                                                                                              p.stderr[-2000:])
 
 
 @pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 0, True),
