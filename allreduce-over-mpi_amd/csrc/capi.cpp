@@ -183,7 +183,7 @@ const char* ftar_status_string(ftar_status_t s) {
   switch (s) {
     case FTAR_SUCCESS: return "success";
     case FTAR_ERR_INVALID_ARG: return "invalid argument";
-    case FTAR_ERR_UNSUPPORTED: return "unsupported dtype/op";
+    case FTAR_ERR_UNSUPPORTED: return "unsupported (dtype/op, form or operation; see ftar_last_error)";
     case FTAR_ERR_INVALID_TOPO: return "invalid FT_TOPO/FT_LONELY";
     case FTAR_ERR_HIP: return "HIP error";
     case FTAR_ERR_RCCL: return "RCCL error";

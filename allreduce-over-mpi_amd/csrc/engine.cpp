@@ -1005,7 +1005,8 @@ ftar_status_t decide_exec(ftar_comm* c, Topology* t, bool topo_auto, size_t byte
   if (topo_auto) flags |= FTAR_CHOOSE_TOPO;
   if (c->form == FTAR_FORM_AUTO && c->tp->async_p2p()) {
     flags |= FTAR_CHOOSE_FORM;
-    if (!host && !c->capturing && c->nranks > 1) flags |= FTAR_CHOOSE_PEER;
+    // the same choice captured or not: a warm-up call of the shape sizes exactly what its capture uses
+    if (!host && c->nranks > 1) flags |= FTAR_CHOOSE_PEER;
   }
   if (!c->chunk_bytes && !host) flags |= FTAR_CHOOSE_CHUNK;
   // a fixed mix of settings no form names is priced as the form of its reduce-scatter

@@ -49,7 +49,7 @@ ALLGATHER = {"stages": 0, "collective": 1, "direct": 2}   # ftar_allgather_t
 _AG_NAME = {v: k for k, v in ALLGATHER.items()}
 REDUCE_SCATTER = {"stages": 0, "direct": 1}                 # ftar_reduce_scatter_t
 _RS_NAME = {v: k for k, v in REDUCE_SCATTER.items()}
-STATUS = {0: "success", 1: "invalid argument", 2: "unsupported dtype/op", 3: "invalid FT_TOPO/FT_LONELY",
+STATUS = {0: "success", 1: "invalid argument", 2: "unsupported", 3: "invalid FT_TOPO/FT_LONELY",
           4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout",
           8: "out of device memory"}
 MAX_STAGES = 16

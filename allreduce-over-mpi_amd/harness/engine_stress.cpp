@@ -2,7 +2,8 @@
 // code: every data-movement form, the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty
 // and ragged buckets, six dtypes with SUM and BAND, device and host buffers, in place and out of place,
 // registered buffers for the peer forms, calls captured into HIP graphs and replayed (in-process groups),
-// error paths, and groups and communicators created and destroyed repeatedly.
+// the execution model steered per group so that "auto" takes every form, error paths, and groups and
+// communicators created and destroyed repeatedly.
 //
 // Built two ways: plainly against lib/libftar.so (csrc/Makefile: lib/ftar_engine_stress, run by
 // tests/test_gpu_engine_stress.py), and against a libftar.so rebuilt with the host sanitizers only
@@ -233,6 +234,23 @@ Case draw(std::mt19937_64& rng, int P, const std::vector<Layout>& lay, size_t re
   return k;
 }
 
+// The execution model's constants for the next group / communicator: the defaults, or steered so that "auto"
+// takes the peer forms, the collective all-gather or many small pieces (every rank draws the same preset)
+void steer_model(std::mt19937_64& rng) {
+  ftar_cost_params_t k{};  // all <= 0: defaults
+  switch (rng() % 5) {
+    case 1: k.peer_read_gbps = 5000; k.barrier_us = 1; break;
+    case 2: k.peer_write_gbps = 5000; k.barrier_us = 1; break;
+    case 3: k.coll_gbps = 5000; break;
+    case 4: k.alpha_us = 0.05; k.issue_us = 0.05; k.link_gbps = 700; break;
+    default: break;
+  }
+  if (ftar_cost_set(&k) != FTAR_SUCCESS) {
+    fprintf(stderr, "FAIL ftar_cost_set\n");
+    _Exit(1);
+  }
+}
+
 struct Stats {
   long calls = 0, checked = 0, refused = 0, groups = 0, regs = 0, captured = 0;
 };
@@ -291,6 +309,7 @@ void capture_replay(int P, std::vector<ftar_comm_t>& comms, std::vector<void*>& 
 
 // one group: `calls` random calls, then destroyed
 void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
+  steer_model(rng);
   std::vector<ftar_comm_t> comms(P);
   std::vector<int> devs(P, 0);
   if (ftar_comm_init_local(comms.data(), P, devs.data()) != FTAR_SUCCESS) fail(std::string("init_local: ") + ftar_last_error());
@@ -487,6 +506,7 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
   const size_t reg_bytes = 1u << 22;
   long checked = 0, refused = 0;
   for (int g = 0; g < gens; ++g) {
+    steer_model(rng);  // before the communicator's first call, where the ranks compare the constants
     ftar_comm_t c;
     HostCtx hctx{shm, r, P};
     if (shm) {
