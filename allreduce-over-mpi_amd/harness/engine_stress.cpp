@@ -44,6 +44,13 @@
 
 #include "ftar.h"
 
+// the library's A/B knobs (exported, not in ftar.h)
+extern "C" {
+ftar_status_t ftar_debug_set_peer_tuning(ftar_comm_t comm, int nt, int lds);
+ftar_status_t ftar_debug_set_peer_dma(ftar_comm_t comm, int dma);
+ftar_status_t ftar_debug_set_rccl_register(ftar_comm_t comm, int on);
+}
+
 namespace {
 
 #define HIP_OK(x)                                                                       \
@@ -212,6 +219,11 @@ struct Case {
   bool band;
   size_t n;
   bool host, oop, registered;
+  // per-call knobs: the peer forms' copy tuning (nt, lds, dma bits), the reduce stream's CU share, RCCL's own
+  // buffer registration, phase timing, and (in-process) a user stream per rank from a small pool (-1: none)
+  int tune, cus;
+  bool rccl_reg, timing;
+  int stream_sel;
 };
 Case draw(std::mt19937_64& rng, int P, const std::vector<Layout>& lay, size_t reg_bytes) {
   static const int forms[] = {FTAR_FORM_AUTO, FTAR_FORM_DIRECT, FTAR_FORM_STAGES, FTAR_FORM_COLLECTIVE,
@@ -231,6 +243,12 @@ Case draw(std::mt19937_64& rng, int P, const std::vector<Layout>& lay, size_t re
   k.oop = rng() % 2 == 0;
   k.registered = !k.host && k.oop && rng() % 3 == 0;
   if (k.registered) k.n = std::min(k.n, reg_bytes / k.d->size);
+  static const int cus[] = {0, 0, 32, 128};
+  k.tune = (int)(rng() % 8);
+  k.cus = cus[rng() % 4];
+  k.rccl_reg = rng() % 4 == 0;
+  k.timing = rng() % 6 == 0;
+  k.stream_sel = rng() % 3 == 0 ? (int)(rng() % 2) : -1;
   return k;
 }
 
@@ -247,6 +265,24 @@ void steer_model(std::mt19937_64& rng) {
   }
   if (ftar_cost_set(&k) != FTAR_SUCCESS) {
     fprintf(stderr, "FAIL ftar_cost_set\n");
+    _Exit(1);
+  }
+}
+
+// FTAR_STRESS_SKIP=dma,cus,timing,streams,tune,rcclreg: draw the knob (the call sequence stays the same) but
+// leave it at its default -- to bisect a failure
+bool skip(const char* knob) {
+  const char* e = getenv("FTAR_STRESS_SKIP");
+  return e && strstr(e, knob);
+}
+void apply_knobs(ftar_comm_t c, const Case& k, bool rccl) {
+  const int nt = skip("tune") ? 1 : k.tune & 1, lds = skip("tune") ? 1 : (k.tune >> 1) & 1;
+  const int dma = skip("dma") ? 0 : (k.tune >> 2) & 1;
+  if (ftar_debug_set_peer_tuning(c, nt, lds) != FTAR_SUCCESS || ftar_debug_set_peer_dma(c, dma) != FTAR_SUCCESS ||
+      ftar_comm_set_reduce_cus(c, skip("cus") ? 0 : k.cus) != FTAR_SUCCESS ||
+      ftar_comm_set_phase_timing(c, skip("timing") ? 0 : k.timing) != FTAR_SUCCESS ||
+      (rccl && ftar_debug_set_rccl_register(c, skip("rcclreg") ? 0 : k.rccl_reg) != FTAR_SUCCESS)) {
+    fprintf(stderr, "FAIL knobs: %s\n", ftar_last_error());
     _Exit(1);
   }
 }
@@ -293,6 +329,7 @@ void capture_replay(int P, std::vector<ftar_comm_t>& comms, std::vector<void*>& 
       HIP_OK(hipMemcpy(oop ? send[r] : recv[r], in.data(), bytes, hipMemcpyHostToDevice));
       if (oop) HIP_OK(hipMemset(recv[r], 0x5a, bytes));
     }
+    HIP_OK(hipDeviceSynchronize());  // s0 is non-blocking: the legacy-stream writes above must be done first
     HIP_OK(hipGraphLaunch(x, s0));
     HIP_OK(hipStreamSynchronize(s0));
     expect(want, d, n, P, band, 7 * rep);
@@ -314,6 +351,8 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
   std::vector<int> devs(P, 0);
   if (ftar_comm_init_local(comms.data(), P, devs.data()) != FTAR_SUCCESS) fail(std::string("init_local: ") + ftar_last_error());
   ++st->groups;
+  std::vector<void*> pool(2 * P);
+  for (auto& q : pool) HIP_OK(hipStreamCreateWithFlags(reinterpret_cast<hipStream_t*>(&q), hipStreamNonBlocking));
   const auto lay = layouts(P);
   // registered device buffers (the peer forms' no-copy path): one pair per rank, registered collectively
   const size_t reg_bytes = 1u << 22;
@@ -350,7 +389,11 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
       if (ftar_comm_set_form(comms[r], form) != FTAR_SUCCESS) fail("set_form");
       if (ftar_comm_set_chunk_bytes(comms[r], chunk) != FTAR_SUCCESS) fail("set_chunk_bytes");
       if (ftar_comm_set_host_chunk_bytes(comms[r], chunk) != FTAR_SUCCESS) fail("set_host_chunk_bytes");
+      apply_knobs(comms[r], k, false);
     }
+    std::vector<void*> user_streams;  // one of two streams per rank (calls alternate streams unsynchronised)
+    if (k.stream_sel >= 0 && !skip("streams"))
+      for (int r = 0; r < P; ++r) user_streams.push_back(pool[2 * r + k.stream_sel]);
     const size_t bytes = n * d.size;
     std::vector<std::vector<uint8_t>> in(P);
     for (int r = 0; r < P; ++r) fill(in[r], d, n, r, band);
@@ -384,15 +427,18 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
       recv[r] = oop ? b : a;
     }
     const ftar_op_t op = band ? FTAR_BAND : FTAR_SUM;
+    void* const* sv = user_streams.empty() ? nullptr : user_streams.data();
     const ftar_status_t s = host ? ftar_allreduce_host_group(send.data(), recv.data(), n, d.t, op, &topo,
-                                                             comms.data(), P, nullptr)
+                                                             comms.data(), P, sv)
                                  : ftar_allreduce_group(send.data(), recv.data(), n, d.t, op, &topo, comms.data(),
-                                                        P, nullptr);
+                                                        P, sv);
     HIP_OK(hipDeviceSynchronize());
     ++st->calls;
     char what[256];
-    snprintf(what, sizeof what, "P=%d topo=%s+%s form=%d chunk=%zu %s %s n=%zu host=%d oop=%d reg=%d", P, L.topo,
-             L.lonely ? L.lonely : "0", form, chunk, d.name, band ? "band" : "sum", n, host, oop, registered);
+    snprintf(what, sizeof what,
+             "P=%d topo=%s+%s form=%d chunk=%zu %s %s n=%zu host=%d oop=%d reg=%d tune=%d cus=%d timing=%d stream=%d",
+             P, L.topo, L.lonely ? L.lonely : "0", form, chunk, d.name, band ? "band" : "sum", n, host, oop, registered,
+             k.tune, k.cus, (int)k.timing, k.stream_sel);
     if (s != FTAR_SUCCESS) {
       // refusals the engine documents: forms a layout cannot take are replaced, so only errors remain
       fail(std::string(what) + ": " + ftar_status_string(s) + ": " + ftar_last_error());
@@ -442,6 +488,7 @@ void run_group(int P, int calls, std::mt19937_64& rng, Stats* st) {
     HIP_OK(hipFree(rx[r]));
     HIP_OK(hipFree(ry[r]));
   }
+  for (auto q : pool) HIP_OK(hipStreamDestroy(static_cast<hipStream_t>(q)));
 }
 
 std::string show(const Dt& d, const uint8_t* p) {
@@ -543,6 +590,7 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
       if (ftar_comm_set_form(c, k.form) != FTAR_SUCCESS || ftar_comm_set_chunk_bytes(c, k.chunk) != FTAR_SUCCESS ||
           ftar_comm_set_host_chunk_bytes(c, k.chunk) != FTAR_SUCCESS)
         fail("setters");
+      apply_knobs(c, k, !shm);
       std::vector<uint8_t> in, hout;
       fill(in, d, k.n, r, k.band);
       void *send = nullptr, *recv = nullptr, *a = nullptr, *b = nullptr;
