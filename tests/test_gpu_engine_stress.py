@@ -1,7 +1,8 @@
 """The engine stress driver (allreduce-over-mpi_amd/harness/engine_stress.cpp, built as lib/ftar_engine_stress)
 on the production library: seeded random calls with every result checked against the exact sum of
-small-integer inputs -- in-process groups created and destroyed (P = 2..8), and P processes of one RCCL
-communicator or of the host-bootstrapped transport each (loopback sockets; two communicators in turn).  The
+small-integer inputs -- in-process groups created and destroyed (P = 2..8; some calls captured into HIP graphs
+and replayed), and P processes of one RCCL communicator or of the host-bootstrapped transport each (loopback
+sockets; two communicators in turn); per-call knobs and a steered execution model.  The
 same source built against a host-sanitized libftar.so is tools/asan/ (profiles/r04/asan_*.log); the RCCL mode
 found the peer-write race that test_peer_write_waits_for_every_copy_out now pins."""
 import json
@@ -22,13 +23,13 @@ def _run(args, timeout):
 
 
 def test_in_process_groups():
-    p = _run([1200, 5], 240)
+    p = _run([500, 5], 240)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
     stats = json.loads(p.stdout.strip().splitlines()[-1])
-    assert stats["checked"] == stats["calls"] >= 1200 and stats["groups"] >= 20, stats
+    assert stats["checked"] == stats["calls"] >= 500 and stats["groups"] >= 8 and stats["captured"] > 0, stats
 
 
-@pytest.mark.parametrize("mode,P,calls,seed", [("rccl", 4, 120, 41), ("rccl", 8, 80, 12), ("host", 4, 120, 43)])
+@pytest.mark.parametrize("mode,P,calls,seed", [("rccl", 4, 40, 41), ("rccl", 8, 16, 12), ("host", 4, 60, 43)])
 def test_processes(mode, P, calls, seed):
     p = _run([mode, P, calls, seed, 2], 240)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
