@@ -418,3 +418,28 @@ def test_harness_rccl_concurrent_communicators_with_a_queue_each(tmp_path):
     assert p.returncode == 0, out[-4000:]
     for r in range(2):
         assert f"COMM_THREADS {r}: threads=2 ok" in p.stdout, out[-4000:]
+
+
+MPI_STRESS = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib", "ftar_mpi_stress")
+
+
+@needs
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,ranks,calls,seed", [("ipc", 2, 80, 411), ("ipc", 4, 40, 412), ("rccl", 3, 40, 413)])
+def test_mpi_drop_in_random_calls(tmp_path, transport, ranks, calls, seed):
+    """Random calls through MPI_Allreduce_FT and MPI_Allreduce_FT_device (harness/mpi_stress.cpp): the
+    reference's MPI datatypes with MPI_SUM and MPI_BAND, empty and ragged counts, FT_TOPO / FT_LONELY set per
+    call, MPI_IN_PLACE and separate buffers, registered and pageable host buffers, device buffers, duplicated
+    communicators freed again; every rank's result equals the exact sum / AND of small-integer inputs."""
+    env = dict(os.environ, FTAR_MPI_TRANSPORT=transport, NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+    args = [str(calls), str(seed)]
+    if transport == "rccl":
+        cmd = [MPIEXEC]
+        for r in range(ranks):
+            cmd += ([":"] if r else []) + ["-n", "1", "-env", "NCCL_HOSTID", f"ftar-mpistress-{r}", MPI_STRESS] + args
+    else:
+        cmd = [MPIEXEC, "-n", str(ranks), MPI_STRESS] + args
+    p = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    reports = [ln for ln in p.stdout.splitlines() if ln.startswith('{"rank"')]
+    assert len(reports) == ranks and all(f'"checked": {calls}' in r for r in reports), p.stdout[-2000:]
