@@ -1,7 +1,8 @@
 // Random AllReduce calls through the engine's paths, every result checked, as a stress driver of its HOST
 // code: every data-movement form, the ring, trees and lonely layouts, pieces from 256 B to whole blocks, empty
 // and ragged buckets, six dtypes with SUM and BAND, device and host buffers, in place and out of place,
-// registered buffers for the peer forms, calls captured into HIP graphs and replayed (in-process groups),
+// registered buffers for the peer forms, calls captured into HIP graphs and replayed (in-process groups and
+// each rank of an RCCL communicator),
 // the execution model steered per group so that "auto" takes every form, error paths, and groups and
 // communicators created and destroyed repeatedly.
 //
@@ -551,7 +552,7 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
   std::mt19937_64 rng(seed);  // the same sequence on every rank
   const auto lay = layouts(P);
   const size_t reg_bytes = 1u << 22;
-  long checked = 0, refused = 0;
+  long checked = 0, refused = 0, captured = 0;
   for (int g = 0; g < gens; ++g) {
     steer_model(rng);  // before the communicator's first call, where the ranks compare the constants
     ftar_comm_t c;
@@ -637,6 +638,37 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
         fail(std::string(what) + ": differs from the exact result:" + diff);
       }
       ++checked;
+      // now and then the same call captured into a HIP graph on this rank (every rank alike: the product's
+      // process model under capture) and replayed twice on fresh inputs; the graphs meet through RCCL
+      if (!k.host && bytes && !shm && rng() % 8 == 0) {
+        hipStream_t cs;
+        HIP_OK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+        HIP_OK(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed));
+        const ftar_status_t s2 = ftar_allreduce(send, recv, k.n, d.t, op, &topo, c, cs);
+        const std::string err2 = s2 == FTAR_SUCCESS ? "" : ftar_last_error();
+        hipGraph_t gr = nullptr;
+        const hipError_t e2 = hipStreamEndCapture(cs, &gr);
+        if (s2 != FTAR_SUCCESS) fail(std::string(what) + ": captured call: " + ftar_status_string(s2) + ": " + err2);
+        if (e2 != hipSuccess) fail(std::string(what) + ": hipStreamEndCapture: " + hipGetErrorString(e2));
+        hipGraphExec_t gx;
+        HIP_OK(hipGraphInstantiate(&gx, gr, nullptr, nullptr, 0));
+        for (int rep = 1; rep <= 2; ++rep) {
+          std::vector<uint8_t> in2, want2, got2(bytes);
+          fill(in2, d, k.n, r + 7 * rep, k.band);
+          HIP_OK(hipMemcpy(k.oop ? send : recv, in2.data(), bytes, hipMemcpyHostToDevice));
+          if (k.oop) HIP_OK(hipMemset(recv, 0x5a, bytes));
+          HIP_OK(hipDeviceSynchronize());
+          HIP_OK(hipGraphLaunch(gx, cs));
+          HIP_OK(hipStreamSynchronize(cs));
+          HIP_OK(hipMemcpy(got2.data(), recv, bytes, hipMemcpyDeviceToHost));
+          expect(want2, d, k.n, P, k.band, 7 * rep);
+          if (got2 != want2) fail(std::string(what) + ": graph replay " + std::to_string(rep) + " differs");
+        }
+        HIP_OK(hipGraphExecDestroy(gx));
+        HIP_OK(hipGraphDestroy(gr));
+        HIP_OK(hipStreamDestroy(cs));
+        ++captured;
+      }
       if (r == 0 && checked % 25 == 0) {  // progress (a silent run is taken to be hung)
         printf("progress: rank 0 gen %d, %ld calls checked\n", g, checked);
         fflush(stdout);
@@ -656,7 +688,8 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
     HIP_OK(hipFree(rx));
     HIP_OK(hipFree(ry));
   }
-  printf("{\"rank\": %d, \"checked\": %ld, \"refused\": %ld, \"communicators\": %d}\n", r, checked, refused, gens);
+  printf("{\"rank\": %d, \"checked\": %ld, \"captured\": %ld, \"refused\": %ld, \"communicators\": %d}\n", r, checked,
+         captured, refused, gens);
   fflush(stdout);
   HIP_OK(hipDeviceSynchronize());
   _Exit(0);  // as in main: no HIP runtime static teardown under the sanitizer
