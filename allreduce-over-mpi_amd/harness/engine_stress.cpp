@@ -614,6 +614,12 @@ int rccl_rank(int r, int P, long calls, unsigned long seed, int gens, const std:
         recv = k.oop ? b : a;
       }
       const ftar_op_t op = k.band ? FTAR_BAND : FTAR_SUM;
+      if (getenv("FTAR_STRESS_VERBOSE")) {
+        fprintf(stderr, "rank %d gen %d call %ld: topo=%s+%s form=%d chunk=%zu %s n=%zu host=%d oop=%d reg=%d tune=%d "
+                "cus=%d timing=%d rcclreg=%d\n", r, g, call, k.L.topo, k.L.lonely ? k.L.lonely : "0", k.form, k.chunk,
+                d.name, k.n, k.host, k.oop, k.registered, k.tune, k.cus, (int)k.timing, (int)k.rccl_reg);
+        fflush(stderr);
+      }
       const ftar_status_t s = k.host ? ftar_allreduce_host(send, recv, k.n, d.t, op, &topo, c, nullptr)
                                      : ftar_allreduce(send, recv, k.n, d.t, op, &topo, c, nullptr);
       HIP_OK(hipDeviceSynchronize());
