@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct forms out of the sweep")
+    ap.add_argument("--sweep-cus", action="store_true",
+                    help="N>1: also sweep the reduce stream on 224 CUs (direct:cus224). Off by default: the CU-masked "
+                         "stream is blocking towards the legacy NULL stream, and the engine stress saw RCCL calls "
+                         "with it hang once (DESIGN section 5, open)")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     ap.add_argument("--no-c5", action="store_true", help="N>1: skip the bf16 configs[4] line item")
@@ -1262,7 +1266,8 @@ def bench_distributed(a):
             chunks = {4 << 20, 16 << 20, 64 << 20, mc}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
-                plan.append((t, mc, "direct:cus224"))
+                if a.sweep_cus:
+                    plan.append((t, mc, "direct:cus224"))
                 plan.append((t, mc, "direct:ncclreg"))
             if form == "stages" and t.ring:
                 chunks = {mc}  # the reference's ring rounds: one point is enough
