@@ -364,7 +364,10 @@ ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const
 /* Co-scheduling of the fold with the transport: the reduce stream runs on
  * `cus` of the device's CUs (spread evenly; 0 = all, the default), so the
  * comm stream's kernels (RCCL p2p, copies) always find free CUs while a
- * piece's fold runs (FTAR_REDUCE_CUS at init).  Same bits either way. */
+ * piece's fold runs (FTAR_REDUCE_CUS at init).  Same bits either way.  The
+ * CU-masked stream is blocking towards the legacy NULL stream; calls over RCCL
+ * with it were seen to stall once under the stress driver (DESIGN.md §5,
+ * open): keep it off on RCCL communicators for now. */
 ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus);
 ftar_status_t ftar_comm_get_reduce_cus(ftar_comm_t comm, int* cus);
 /* Host-mode piece size per block (bytes, rounded to 256 B); 0 = auto: 16 MiB,
