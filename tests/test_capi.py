@@ -268,3 +268,17 @@ def test_mpi_dropin_type_and_op_mapping(tmp_path):
                     "/opt/conda/lib/libmpi.so", "-Wl,-rpath,/opt/conda/lib"], check=True)
     out = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "1", exe], capture_output=True, text=True, timeout=60)
     assert out.returncode == 0 and "mpi dtypes ok" in out.stdout, (out.returncode, out.stdout, out.stderr)
+
+
+def test_stress_drivers_are_built_against_the_product_library():
+    """build() makes the engine and MPI drop-in stress drivers (harness/engine_stress.cpp, harness/mpi_stress.cpp)
+    next to libftar.so, linked to it (their GPU runs: tests/test_gpu_engine_stress.py, test_mpi_drop_in_random_calls)"""
+    import subprocess
+    lib = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib")
+    for exe in ("ftar_engine_stress", "ftar_mpi_stress"):
+        path = os.path.join(lib, exe)
+        if exe == "ftar_mpi_stress" and not os.path.exists("/opt/conda/include/mpi.h"):
+            continue
+        assert os.access(path, os.X_OK), path
+        deps = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
+        assert "libftar.so" in deps and os.path.join(lib, "libftar.so") in deps, deps
