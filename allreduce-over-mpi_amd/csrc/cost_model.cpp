@@ -37,11 +37,19 @@ std::mutex g_cost_mu;
 ftar_cost_params_t g_set{};  // fields <= 0: default
 std::atomic<uint64_t> g_generation{0};  // bumped by every set: communicators re-decide their cached choices
 
-// MI355X defaults: alpha one p2p group; link an RCCL p2p stream to one peer (of a 76.8 GB/s xGMI
-// direction); hbm the measured k = 2..8 fold (profiles/r01/kbench3); issue the host enqueue of one piece
-// of one round at P = 8 (enqueue cost); barrier a 4-byte ncclAllReduce; copy the LDS-staged
-// copy (profiles/r03/kbench_copy.log)
-constexpr ftar_cost_params_t kDefaults = {20.0, 48.0, 6300.0, 25.0, 20.0, 0.0, 0.0, 6500.0, 0.0};
+// MI355X defaults, used where no run on the node has fitted them (bench.py at N > 1 does):
+//   alpha   one p2p group's launch and handshake (assumed, 20 us)
+//   link    an RCCL p2p stream to one peer: the xGMI link spec, 76.8 GB/s per direction, times an ASSUMED
+//           RCCL p2p efficiency of 0.7 (protocol and FIFO staging; never measured on xGMI here -- the first
+//           N > 1 run's probe and sweep replace it)
+//   hbm     the measured k = 2..8 fold (profiles/r01/kbench3)
+//   issue   the host enqueue of one piece of one round at P = 8 (enqueue cost)
+//   barrier a 4-byte ncclAllReduce (assumed)
+//   copy    the LDS-staged copy (profiles/r03/kbench_copy.log)
+//   peer read / write, coll: unmeasured (0), so those forms are never chosen until a run measures them
+constexpr double kXgmiLinkSpecGBps = 76.8, kRcclP2pEfficiency = 0.7;
+constexpr ftar_cost_params_t kDefaults = {20.0, kXgmiLinkSpecGBps * kRcclP2pEfficiency, 6300.0, 25.0, 20.0,
+                                          0.0,  0.0,                                      6500.0, 0.0};
 
 double env_or(const char* name, double v) {
   const char* e = getenv(name);
@@ -264,6 +272,13 @@ ftar_status_t choose_exec(int P, size_t bytes, int flags, const Topology& fixed_
     const size_t stages = t.ring ? (size_t)P : t.widths.size() + (t.lonely ? 2 : 0);
     return std::make_tuple(stages, form, c == 0 ? size_t(0) : ~c);  // smaller wins; whole blocks (0) first
   };
+  struct Priced {
+    Topology t;
+    int form;
+    size_t chunk;
+    double s;
+  };
+  std::vector<Priced> priced;
   for (const Topology& t : topos)
     for (int form : forms) {
       const bool peer = form == FTAR_FORM_PEER_READ || form == FTAR_FORM_PEER_WRITE;
@@ -272,6 +287,7 @@ ftar_status_t choose_exec(int P, size_t bytes, int flags, const Topology& fixed_
         if (whole && c && (double)c >= B) continue;  // the same as whole blocks
         const double s = exec_cost(t, P, bytes, form, peer ? 0 : c, false, k);
         if (s < 0) continue;
+        priced.push_back({t, form, peer ? (size_t)0 : c, s});
         const bool better = !found || s < best.seconds * (1 - 1e-9) ||
                             (s <= best.seconds * (1 + 1e-9) &&
                              tie_key(t, form, peer ? 0 : c) < tie_key(best.topo, best.form, best.chunk));
@@ -287,6 +303,21 @@ ftar_status_t choose_exec(int P, size_t bytes, int flags, const Topology& fixed_
   if (!found) {
     set_error("the execution model has no runnable choice for this topology / form", __FILE__, __LINE__);
     return FTAR_ERR_UNSUPPORTED;
+  }
+  // the tie, said out loud: how many candidates the model priced alike, and the highest-ranked tie rule that
+  // set the choice apart from one of them (stages before form before piece)
+  const auto bk = tie_key(best.topo, best.form, best.chunk);
+  best.tied = 0;
+  best.tie_broken_by = FTAR_TIE_NONE;
+  for (const Priced& q : priced) {
+    if (std::fabs(q.s - best.seconds) > best.seconds * 1e-9) continue;
+    ++best.tied;
+    const auto qk = tie_key(q.t, q.form, q.chunk);
+    if (qk == bk) continue;
+    const int rule = std::get<0>(qk) != std::get<0>(bk)   ? FTAR_TIE_STAGES
+                     : std::get<1>(qk) != std::get<1>(bk) ? FTAR_TIE_FORM
+                                                          : FTAR_TIE_PIECE;
+    if (best.tie_broken_by == FTAR_TIE_NONE || rule < best.tie_broken_by) best.tie_broken_by = rule;
   }
   *out = best;
   return FTAR_SUCCESS;
@@ -354,6 +385,8 @@ ftar_status_t ftar_exec_choose(int nranks, size_t bytes, int flags, ftar_exec_t*
   inout->form = ch.form;
   inout->chunk_bytes = ch.chunk;
   inout->seconds = ch.seconds;
+  inout->tied = ch.tied;
+  inout->tie_broken_by = ch.tie_broken_by;
   return FTAR_SUCCESS;
 }
 

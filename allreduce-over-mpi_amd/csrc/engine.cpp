@@ -163,11 +163,22 @@ ftar_status_t mark(ftar_comm* c, const std::string& name, hipStream_t s) {
 // evenly over the mask (CU i is kept iff floor((i+1)*cus/N) > floor(i*cus/N)),
 // so every XCD keeps its share whichever way the mask bits map to XCDs.
 // hipExtStreamCreateWithCUMask makes a blocking stream (it synchronises with
-// the legacy NULL stream), the price of the knob.
+// the legacy NULL stream) on a hardware queue of its own, the price of the knob.
+// Refused on RCCL communicators (Transport::masked_reduce_stream_ok): two runs
+// of the RCCL stress driver stalled ranks inside the first call after the knob
+// moved from 0 to a CU share (profiles/r04/stress_soak/).
 ftar_status_t set_reduce_cus(ftar_comm* c, int cus) {
   int total = 0;
   FTAR_CHECK_HIP(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, c->device));
   if (cus <= 0 || cus >= total) cus = 0;
+  if (cus && c->tp && !c->tp->masked_reduce_stream_ok()) {
+    set_error("the reduce stream cannot be CU-masked on a " + std::string(c->tp->name()) +
+                  " communicator (ftar_comm_set_reduce_cus / FTAR_REDUCE_CUS): a masked stream is a blocking "
+                  "stream on a hardware queue of its own, and over RCCL it stalled ranks (DESIGN §4); "
+                  "0 (every CU) is the only value accepted there",
+              __FILE__, __LINE__);
+    return FTAR_ERR_UNSUPPORTED;
+  }
   if (cus == c->reduce_cus && c->red_s) return FTAR_SUCCESS;
   hipStream_t fresh = nullptr;
   if (cus == 0) {
@@ -441,12 +452,11 @@ bool comm_teardown(ftar_comm* c) {
     }
     c->contact_thread.join();
   }
-  if (c->broken) {  // the transport is aborted: nothing on its streams can be waited for
-    c->tp.reset();
-    return true;
-  }
-  for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
-    if (st) hip_ignore(hipStreamSynchronize(st));
+  // A broken communicator's transport is aborted and its first-contact helper has returned: everything is
+  // released as usual, only its streams are not waited for (nothing on them is waited for after an abort)
+  if (!c->broken)
+    for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
+      if (st) hip_ignore(hipStreamSynchronize(st));
   if (c->tp) {
     c->tp->unmap_peers(&c->xpeers, c->rank);
     for (auto& r : c->regs) {
@@ -999,7 +1009,8 @@ ftar_status_t call_topology(ftar_comm* c, const ftar_topo_t* topo, size_t bytes,
 // What the call runs: the topology, form and piece the caller fixed, the rest from the execution model
 // (cost_model.cpp), cached per communicator.  The same inputs on every rank give the same choice: the
 // model's constants are compared across ranks at the first call (agree_settings).  Peer forms are
-// candidates only for device buffers outside stream capture, and only once their rates are set.
+// candidates only for device buffers (captured or not: a capture takes the choice its warm-up call took),
+// only at P > 1, and only once their rates are set.
 ftar_status_t decide_exec(ftar_comm* c, Topology* t, bool topo_auto, size_t bytes, bool host, ExecChoice* out) {
   int flags = 0;
   if (topo_auto) flags |= FTAR_CHOOSE_TOPO;
@@ -1257,8 +1268,10 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
              : plan.allgather == FTAR_AG_COLLECTIVE ? FTAR_FORM_COLLECTIVE : -2;
   from_topology(topology, &c->last_exec.topo);
   c->last_exec.form = ran;
-  c->last_exec.chunk_bytes = ex.chunk;
+  c->last_exec.chunk_bytes = peer_path ? 0 : ex.chunk;  // the host paths below put the piece they run
   c->last_exec.seconds = ex.seconds;
+  c->last_exec.tied = ex.tied;
+  c->last_exec.tie_broken_by = ex.tie_broken_by;
   const size_t nst = plan.stages.size();
   if (!c->tp->async_p2p()) {
     // A host-bootstrapped communicator's paths differ in their host barriers (peer read: 3, write: 3,
@@ -1288,6 +1301,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
     // of one piece per block gains nothing from it and takes the whole-bucket path below, whose one
     // copy each way beats one per block (C1 through the MPI harness: 0.453 vs 0.487 ms)
     FTAR_RETURN_IF(grow_events(c, 5));
+    c->last_exec.chunk_bytes = host_peer_piece(c, plan.split, esz) * esz;
     return peer_allreduce_host(*host, count, dt, op, plan, c, stream);
   }
   if (host && peer_mode && !c->tp->async_p2p() && peer_eligible(plan)) {
@@ -1321,6 +1335,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   size_t chunk_bytes = c->chunk_bytes ? c->chunk_bytes : ex.chunk ? ex.chunk : plan.split * esz;
   if (host) {
     chunk_bytes = c->host_chunk_bytes ? c->host_chunk_bytes : auto_host_chunk(plan.split * esz);
+    c->last_exec.chunk_bytes = std::max<size_t>(64, (chunk_bytes / esz) & ~size_t(63)) * esz;  // the piece run
     if (count * esz > c->staging_bytes) FTAR_RETURN_IF(refuse_growth_under_capture(c, "the staging buffer"));
     FTAR_RETURN_IF(ensure_buffer(&c->staging, &c->staging_bytes, count * esz, {c->h2d_s, c->comm_s, c->red_s, c->d2h_s}));
     sendbuf = nullptr;

@@ -88,6 +88,8 @@ struct ExecChoice {
   int form = FTAR_FORM_DIRECT;
   size_t chunk = 0;  // 0: whole blocks
   double seconds = 0;
+  int tied = 1;           // candidates priced equal to this one, itself included
+  int tie_broken_by = 0;  // ftar_tie_t
 };
 // argmin over what `flags` (FTAR_CHOOSE_*) leaves free; the rest is fixed_*
 ftar_status_t choose_exec(int P, size_t bytes, int flags, const Topology& fixed_topo, int fixed_form,
@@ -261,6 +263,10 @@ class Transport {
   // HIP 7.2's hipStreamEndCapture recurse without end from P = 3 on (tools/capture/depth_probe.sh; P = 2
   // ends), while the serial form ends at every P, layout and piece size probed.
   virtual bool capture_serially() const { return false; }
+  // The reduce stream may be a CU-masked one (ftar_comm_set_reduce_cus).  Not where the transport's kernels
+  // wait on other processes on the device (RCCL): a masked stream takes a hardware queue of its own out of the
+  // process's four and is a blocking stream, and over RCCL that stalled ranks in a call.
+  virtual bool masked_reduce_stream_ok() const { return true; }
   // Called by every rank before it joins its internal streams back into the
   // caller's stream.  Under capture the local transport makes the ranks meet
   // here first: HIP's capture breaks (hipStreamEndCapture recurses without

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdlib>
@@ -267,7 +268,7 @@ class RcclTransport final : public Transport {
     }
   }
   ~RcclTransport() override {
-    if (comm_) ncclCommDestroy(comm_);
+    if (comm_ && !aborted_.load()) ncclCommDestroy(comm_);
     if (agree_s_) hip_ignore(hipStreamDestroy(agree_s_));
     if (agree_buf_) hip_ignore(hipFree(agree_buf_));
     if (scratch_) hip_ignore(hipFree(scratch_));
@@ -297,9 +298,11 @@ class RcclTransport final : public Transport {
     }
     return FTAR_SUCCESS;
   }
+  // comm_ itself is never cleared: the first-contact helper thread may still be reading it inside an RCCL
+  // call, which the abort makes return; the destructor, which runs after that helper has
+  // finished, then skips ncclCommDestroy
   void abort() override {
-    if (comm_) ncclCommAbort(comm_);
-    comm_ = nullptr;
+    if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
   }
   // a 4-byte all-reduce: complete on any rank's stream only once every rank's
   // stream has reached it
@@ -384,6 +387,7 @@ class RcclTransport final : public Transport {
   }
   const char* name() const override { return "rccl"; }
   bool uses_ipc() const override { return true; }
+  bool masked_reduce_stream_ok() const override { return false; }
   ftar_status_t allgather(const void* send, void* recv, size_t bytes, int rank, int nranks, hipStream_t s) override {
     (void)rank;
     (void)nranks;
@@ -417,7 +421,7 @@ class RcclTransport final : public Transport {
     return h;
   }
   void rccl_deregister(void* handle) override {
-    if (handle) (void)ncclCommDeregister(comm_, handle);
+    if (handle && !aborted_.load()) (void)ncclCommDeregister(comm_, handle);
   }
   // every rank's bytes through one ncclAllGather on a private stream (host-blocking; communicator
   // bring-up only)
@@ -470,6 +474,7 @@ class RcclTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   ncclComm_t comm_;
+  std::atomic<bool> aborted_{false};
   int nranks_ = 1;
   void* scratch_ = nullptr;
   PeerImports imports_;

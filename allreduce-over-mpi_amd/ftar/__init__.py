@@ -90,15 +90,21 @@ class CostParams(ctypes.Structure):
 
 class Exec(ctypes.Structure):
     """ftar_exec_t: what the execution model chose (topology, form, piece) and its predicted seconds."""
-    _fields_ = [("topo", Topo), ("form", ctypes.c_int), ("chunk_bytes", ctypes.c_size_t), ("seconds", ctypes.c_double)]
+    _fields_ = [("topo", Topo), ("form", ctypes.c_int), ("chunk_bytes", ctypes.c_size_t), ("seconds", ctypes.c_double),
+                ("tied", ctypes.c_int), ("tie_broken_by", ctypes.c_int)]
 
     def as_dict(self):
-        return {"topology": str(self.topo), "form": FORM_NAME.get(self.form, self.form),
-                "chunk_bytes": self.chunk_bytes, "predicted_ms": self.seconds * 1e3 if self.seconds >= 0 else None}
+        d = {"topology": str(self.topo), "form": FORM_NAME.get(self.form, self.form),
+             "chunk_bytes": self.chunk_bytes, "predicted_ms": self.seconds * 1e3 if self.seconds >= 0 else None,
+             "tied": self.tied}
+        if self.tied > 1:   # the model priced several candidates alike: say which rule picked this one
+            d["tie_broken_by"] = TIE_NAME.get(self.tie_broken_by, self.tie_broken_by)
+        return d
 
 
 FORM = {"auto": -1, "direct": 0, "stages": 1, "collective": 2, "peer-read": 3, "peer-write": 4}   # ftar_form_t
 FORM_NAME = {v: k for k, v in FORM.items()}
+TIE_NAME = {0: "none", 1: "stages", 2: "form", 3: "piece"}   # ftar_tie_t
 CHOOSE_TOPO, CHOOSE_FORM, CHOOSE_CHUNK, CHOOSE_PEER = 1, 2, 4, 8
 
 

@@ -276,11 +276,22 @@ bool skip(const char* knob) {
   const char* e = getenv("FTAR_STRESS_SKIP");
   return e && strstr(e, knob);
 }
+// On an RCCL communicator the CU share is refused (FTAR_ERR_UNSUPPORTED, the reduce stream stays on every CU:
+// DESIGN §4); the draw still happens, so the call sequence of a seed is the same as before the rule.
 void apply_knobs(ftar_comm_t c, const Case& k, bool rccl) {
   const int nt = skip("tune") ? 1 : k.tune & 1, lds = skip("tune") ? 1 : (k.tune >> 1) & 1;
   const int dma = skip("dma") ? 0 : (k.tune >> 2) & 1;
+  const int cus = skip("cus") ? 0 : k.cus;
+  if (rccl && cus) {
+    int now = -1;
+    if (ftar_comm_set_reduce_cus(c, cus) != FTAR_ERR_UNSUPPORTED || ftar_comm_get_reduce_cus(c, &now) != FTAR_SUCCESS ||
+        now != 0) {
+      fprintf(stderr, "FAIL reduce_cus=%d on an RCCL communicator was not refused (reduce stream on %d)\n", cus, now);
+      _Exit(1);
+    }
+  }
   if (ftar_debug_set_peer_tuning(c, nt, lds) != FTAR_SUCCESS || ftar_debug_set_peer_dma(c, dma) != FTAR_SUCCESS ||
-      ftar_comm_set_reduce_cus(c, skip("cus") ? 0 : k.cus) != FTAR_SUCCESS ||
+      ftar_comm_set_reduce_cus(c, rccl ? 0 : cus) != FTAR_SUCCESS ||
       ftar_comm_set_phase_timing(c, skip("timing") ? 0 : k.timing) != FTAR_SUCCESS ||
       (rccl && ftar_debug_set_rccl_register(c, skip("rcclreg") ? 0 : k.rccl_reg) != FTAR_SUCCESS)) {
     fprintf(stderr, "FAIL knobs: %s\n", ftar_last_error());

@@ -23,7 +23,8 @@
 //                     MPI_Allreduce_FT on each;
 //   --comm-threads T  T duplicates driven at once from T threads
 //                     (MPI_THREAD_MULTIPLE), 3 exact calls each; on the RCCL
-//                     transport only with GPU_MAX_HW_QUEUES >= 8 (T + 1), else
+//                     transport only with GPU_MAX_HW_QUEUES >= 8 (T + 1), so
+//                     at most T = 3 (HIP caps the queues at 32), else
 //                     refused (exit 2);
 //   --register-check  MPI_Allreduce_FT_register / _unregister semantics on a
 //                     scratch buffer (needs a GPU: hipHostRegister).
@@ -332,15 +333,24 @@ int main(int argc, char** argv) {
     if (MPI_Allreduce_FT_comm(MPI_COMM_WORLD, &fc) == MPI_SUCCESS && fc) world_tp = ftar_comm_transport(fc);
   }
   const char* hwq = getenv("GPU_MAX_HW_QUEUES");
+  // HIP accepts at most 32 hardware queues per process, so the RCCL transport runs at most T = 3 threads
+  constexpr int kMaxHwQueues = 32;
   const int queues = hwq && *hwq ? atoi(hwq) : 4, need_queues = 8 * (comm_threads + 1);
   if (comm_threads > 0 && comm_type == "flextree" && !strcmp(world_tp, "rccl") && queues < need_queues) {
-    if (rank == 0)
+    if (rank == 0) {
       printf("COMM_THREADS refused: the RCCL transport cannot drive communicators from %d threads at once "
              "with %d hardware queues per process -- RCCL deadlocks when operations on different communicators "
              "reach the GPU in different orders on different ranks and their kernels share a queue (NCCL's "
-             "rule for concurrent communicators; profiles/r04/rccl_order/); set GPU_MAX_HW_QUEUES >= %d, issue "
-             "the calls in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n",
-             comm_threads, queues, need_queues);
+             "rule for concurrent communicators; profiles/r04/rccl_order/); ",
+             comm_threads, queues);
+      if (need_queues <= kMaxHwQueues)
+        printf("set GPU_MAX_HW_QUEUES >= %d, issue the calls in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n",
+               need_queues);
+      else
+        printf("the RCCL transport supports at most %d threads (8 queues each plus the world's, HIP's limit is %d); "
+               "issue the calls in one agreed order, or use FTAR_MPI_TRANSPORT=ipc\n",
+               kMaxHwQueues / 8 - 1, kMaxHwQueues);
+    }
     fflush(stdout);
     lifecycle_bad += 1;
   } else if (comm_threads > 0 && comm_type == "flextree") {

@@ -47,10 +47,6 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="N=1: CPU baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-peer", action="store_true", help="N>1: leave the peer-direct forms out of the sweep")
-    ap.add_argument("--sweep-cus", action="store_true",
-                    help="N>1: also sweep the reduce stream on 224 CUs (direct:cus224). Off by default: the CU-masked "
-                         "stream is blocking towards the legacy NULL stream, and the engine stress saw RCCL calls "
-                         "with it hang once (DESIGN section 5, open)")
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
     ap.add_argument("--no-c5", action="store_true", help="N>1: skip the bf16 configs[4] line item")
@@ -445,7 +441,7 @@ RCCL_P2P_FORMS = ("direct", "stages")   # ncclSend/ncclRecv both ways ("collecti
 
 def rccl_p2p_best(sweep, world, gpus, bucket, links_of):
     """The fastest validated sweep entry whose data moved by RCCL point-to-point (north_star's transport:
-    ncclSend/ncclRecv, forms "direct", "direct:cusN", "stages"), with its roofline -- reported next to the
+    ncclSend/ncclRecv, forms "direct", "direct:ncclreg", "stages"), with its roofline -- reported next to the
     headline, which may be an IPC peer form, so the RCCL path is graded on its own.  links_of(entry) gives the
     links one rank drives in that entry's form.  None when no such entry validated."""
     ok = [r for r in sweep if "ms" in r and r.get("check") == "ok" and r.get("form", "").split(":")[0] in RCCL_P2P_FORMS]
@@ -463,7 +459,7 @@ def rccl_p2p_best(sweep, world, gpus, bucket, links_of):
 
 def sweep_form(form):
     """A sweep entry's form as the execution model prices it: (form name, registered) -- tuning suffixes
-    (":cus224", ":ncclreg", ":plain", ":vec", ":dma", ":wgN") move the same bytes and are priced as their base
+    (":ncclreg", ":plain", ":vec", ":dma", ":wgN") move the same bytes and are priced as their base
     form; "-reg" marks the peer forms on registered buffers (no local pass)."""
     base = form.split(":")[0]
     return (base[:-4], True) if base.endswith("-reg") else (base, False)
@@ -507,108 +503,198 @@ def issue_from_enqueue(sweep, world, bucket, esz):
     return per[len(per) // 2]
 
 
-def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
-    """The execution model's p2p constants re-fitted to this run's own sweep (DESIGN §7): alpha (one p2p
-    group), link (one peer, one direction) and issue (host enqueue of one piece) minimise the squared log
-    error of the model's prediction over the validated RCCL p2p entries (forms direct / stages, no tuning
-    suffix; several topologies and piece sizes), by a log-grid search refined twice around its best point.
-    `fixed` names constants measured directly (e.g. {"issue_us": ...}) that the search keeps.  Leaves the
-    model on the best constants found and returns {"params", "entries", "rms_log_err"} (None: < 3 entries)."""
+# A fitted constant is reported "unidentified" (and the prior kept: the probe's value, or the default) when
+# the sweep cannot pin it: fewer entries than free constants + 2, a value on its search bound, a flat
+# direction -- doubling or halving it changes the summed squared log error by less than FLAT_SSE per entry
+# (about a 1 % prediction change on average) -- or a ridge: held at 4x or 1/4 of its value, the OTHER
+# constants re-fitted explain the sweep as well ("confounded", e.g. alpha and issue when every piece costs
+# the same whichever term pays for it).  An ill-posed fit never sets the engine's constants.
+FLAT_SSE = 1e-4
+
+
+def _log_sse(ftar, pts, world, bucket):
+    """summed squared log error of the model's predictions over `pts` under the constants set now"""
     import math
-    pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in ("direct", "stages")]
-    if len(pts) < 3:
-        return None
-    base = ftar.cost_get()
-    fixed = {k: v for k, v in (fixed or {}).items() if v}
+    e = 0.0
+    for r in pts:
+        p = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
+        if p is None or p <= 0:
+            return float("inf")
+        e += math.log(p / r["ms"]) ** 2
+    return e
 
-    def err(alpha, link, issue):
-        ftar.cost_set(**dict(base, **dict(dict(alpha_us=alpha, link_gbps=link, issue_us=issue), **fixed)))
-        s = 0.0
-        for r in pts:
-            p = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
-            if p is None or p <= 0:
-                return float("inf")
-            s += math.log(p / r["ms"]) ** 2
-        return s
 
-    def geom(lo, hi, n):
-        return [lo * (hi / lo) ** (i / (n - 1)) for i in range(n)]
-
-    grids = {"alpha_us": geom(0.5, 5000.0, 11), "link_gbps": geom(1.0, 1000.0, 13), "issue_us": geom(0.5, 5000.0, 11)}
-    if "issue_us" in fixed:
-        grids["issue_us"] = [fixed["issue_us"]]
-    best = (float("inf"), None)
-    for a_ in grids["alpha_us"]:
-        for l_ in grids["link_gbps"]:
-            for i_ in grids["issue_us"]:
-                e = err(a_, l_, i_)
-                if e < best[0]:
-                    best = (e, [a_, l_, i_])
-    if best[1] is None:
-        ftar.cost_set(**base)
-        return None
-    # pattern search in log space from the grid's best point: a step that improves is taken, none improving
-    # halves the steps, down to 1 %
-    x, fx = list(best[1]), best[0]
-    steps = [math.log(2.5), math.log(1.8), 0.0 if "issue_us" in fixed else math.log(2.5)]
-    lo, hi = (0.1, 0.5, 0.1), (1e5, 5e3, 1e5)   # us, GB/s, us
-    while max(steps) > math.log(1.01):
+def _fit_log(f, x0, lo, hi, grid):
+    """minimise f over a box in log space: the grid's best point (grid[d]: candidate values of coordinate
+    d), then a pattern search from it (a step that improves is taken; none improving halves the steps, down
+    to 1 %).  Returns (x, f(x))."""
+    import itertools
+    import math
+    best = (float("inf"), list(x0))
+    for y in itertools.product(*grid):
+        fy = f(list(y))
+        if fy < best[0]:
+            best = (fy, list(y))
+    x, fx = best[1], best[0]
+    steps = [math.log(2.5) if len(g) > 1 else 0.0 for g in grid]
+    while max(steps, default=0.0) > math.log(1.01):
         moved = False
-        for d in range(3):
+        for d in range(len(x)):
             for sgn in (1, -1):
                 if not steps[d]:
                     continue
                 y = list(x)
                 y[d] = min(hi[d], max(lo[d], x[d] * math.exp(sgn * steps[d])))
-                fy = err(*y)
+                fy = f(y)
                 if fy < fx:
                     x, fx, moved = y, fy, True
                     break
         if not moved:
             steps = [s_ / 2 for s_ in steps]
-    best = (fx, x)
-    a0, l0, i0 = best[1]
-    params = ftar.cost_set(**dict(base, **dict(dict(alpha_us=a0, link_gbps=l0, issue_us=i0), **fixed)))
+    return x, fx
+
+
+def _identify(f, x, fx, lo, hi, n, grid=None):
+    """why each coordinate of the minimum x of f is not identified (None: it is): 'bound' (within 1 % of
+    lo / hi), 'flat' (doubling and halving it both leave f within FLAT_SSE per entry) or, given the other
+    coordinates' search grids, 'confounded' (held at 4x or 1/4 of its value, the others re-fitted reach f
+    within FLAT_SSE per entry)"""
+    why = []
+    for d in range(len(x)):
+        if x[d] <= lo[d] * 1.01 or x[d] >= hi[d] / 1.01:
+            why.append("bound")
+            continue
+        moved = []
+        for fac in (2.0, 0.5):
+            y = list(x)
+            y[d] = min(hi[d], max(lo[d], x[d] * fac))
+            moved.append(f(y))
+        if min(moved) - fx < FLAT_SSE * n:
+            why.append("flat")
+            continue
+        conf = False
+        for fac in ((4.0, 0.25) if grid and len(x) > 1 else ()):
+            held = min(hi[d], max(lo[d], x[d] * fac))
+            others = [i for i in range(len(x)) if i != d]
+
+            def g(z):
+                y = list(x)
+                y[d] = held
+                for i, v in zip(others, z):
+                    y[i] = v
+                return f(y)
+            _, fz = _fit_log(g, [x[i] for i in others], [lo[i] for i in others], [hi[i] for i in others],
+                             [grid[i] for i in others])
+            conf = conf or fz - fx < FLAT_SSE * n
+        why.append("confounded" if conf else None)
+    return why
+
+
+def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
+    """The execution model's p2p constants re-fitted to this run's own sweep (DESIGN §7): alpha (one p2p
+    group), link (one peer, one direction) and issue (host enqueue of one piece) minimise the squared log
+    error of the model's prediction over the validated RCCL p2p entries (forms direct / stages, no tuning
+    suffix; several topologies and piece sizes): a log grid, then a pattern search.  `fixed` names constants
+    measured directly (e.g. {"issue_us": ...}) that the search keeps.  A constant the sweep cannot pin
+    (fewer entries than free constants + 2, a search bound, a flat direction) keeps its prior -- the value
+    set when the refit started (the probe's, or the default) -- and is listed in "unidentified" with the
+    reason; the others are fitted again with it held.  Leaves the model on the result and returns
+    {"params", "entries", "rms_log_err", "unidentified", "prior"} (None: no validated entry)."""
+    import math
+    pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in ("direct", "stages")]
+    if not pts:
+        return None
+    base = ftar.cost_get()
+    fixed = {k: v for k, v in (fixed or {}).items() if v}
+    names = ["alpha_us", "link_gbps", "issue_us"]
+    lo_all = {"alpha_us": 0.1, "link_gbps": 0.5, "issue_us": 0.1}          # us, GB/s, us
+    hi_all = {"alpha_us": 1e5, "link_gbps": 5e3, "issue_us": 1e5}
+    grid_all = {"alpha_us": (0.5, 5000.0, 11), "link_gbps": (1.0, 1000.0, 13), "issue_us": (0.5, 5000.0, 11)}
+    unidentified = {}
+
+    def geom(lo, hi, n):
+        return [lo * (hi / lo) ** (i / (n - 1)) for i in range(n)]
+
+    def solve(free):
+        held = dict(fixed, **{k: base[k] for k in unidentified})
+
+        def f(y):
+            ftar.cost_set(**dict(base, **held, **dict(zip(free, y))))
+            return _log_sse(ftar, pts, world, bucket)
+        x, fx = _fit_log(f, [base[k] for k in free], [lo_all[k] for k in free], [hi_all[k] for k in free],
+                         [geom(*grid_all[k]) for k in free])
+        return f, x, fx, [geom(lo_, hi_, 7) for lo_, hi_, _ in (grid_all[k] for k in free)]
+
+    free = [k for k in names if k not in fixed]
+    if len(pts) < len(free) + 2:
+        unidentified.update({k: f"entries ({len(pts)} < {len(free)} free + 2)" for k in free})
+        free = []
+    for _ in range(len(names)):          # drop what the sweep cannot pin, fit the rest again
+        if not free:
+            break
+        f, x, fx, coarse = solve(free)
+        why = _identify(f, x, fx, [lo_all[k] for k in free], [hi_all[k] for k in free], len(pts), coarse)
+        bad = {k: w for k, w in zip(free, why) if w}
+        if not bad:
+            break
+        unidentified.update(bad)
+        free = [k for k in free if k not in bad]
+    final = dict(base, **fixed, **{k: base[k] for k in unidentified})
+    if free:
+        final.update(dict(zip(free, x)))
+    params = ftar.cost_set(**final)
+    sse = _log_sse(ftar, pts, world, bucket)
     return {"params": {k: round(v, 3) for k, v in params.items()}, "entries": len(pts),
-            "rms_log_err": round(math.sqrt(best[0] / len(pts)), 4)}
+            "rms_log_err": round(math.sqrt(sse / len(pts)), 4) if sse < float("inf") else None,
+            "unidentified": unidentified, "prior": {k: round(base[k], 3) for k in unidentified}}
 
 
 def refit_form_rate(ftar, sweep, world, bucket, field, forms):
     """One more constant of the execution model fitted to this run's sweep: the rate `field` (peer_read_gbps,
     peer_write_gbps or coll_gbps) that minimises the squared log error over the validated entries whose form
-    is in `forms` (a 1-D golden-section search in log space, 1 .. 5000 GB/s).  Leaves the model on it;
-    returns {"value", "entries", "rms_log_err"} or None (no entries)."""
+    is in `forms` (a 1-D golden-section search in log space, 1 .. 5000 GB/s).  Unidentified (fewer than 3
+    entries, a search bound, a flat direction): the prior -- the value set when the refit started, the
+    probe's or the default -- is kept and the reason given.  Leaves the model on the result; returns
+    {"value", "entries", "rms_log_err", "unidentified"} or None (no entries)."""
     import math
     pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in forms]
     if not pts:
         return None
     base = ftar.cost_get()
+    lo, hi = 1.0, 5000.0
 
-    def err(lx):
-        ftar.cost_set(**dict(base, **{field: math.exp(lx)}))
-        e = 0.0
-        for r in pts:
-            p = predict_ms(ftar, r["topology"], r["form"], r["chunk_bytes"], world, bucket)
-            if p is None or p <= 0:
-                return float("inf")
-            e += math.log(p / r["ms"]) ** 2
-        return e
-    a, b = math.log(1.0), math.log(5000.0)
+    def err_at(v):
+        ftar.cost_set(**dict(base, **{field: v}))
+        return _log_sse(ftar, pts, world, bucket)
+
+    def rms(e):
+        return round(math.sqrt(e / len(pts)), 4) if e < float("inf") else None
+    if len(pts) < 3:
+        ftar.cost_set(**base)
+        return {"value": round(base[field], 3), "entries": len(pts), "unidentified": f"entries ({len(pts)} < 3)",
+                "rms_log_err": rms(_log_sse(ftar, pts, world, bucket))}
+    a, b = math.log(lo), math.log(hi)
     g = (math.sqrt(5) - 1) / 2
     c, d = b - g * (b - a), a + g * (b - a)
-    fc, fd = err(c), err(d)
+    fc, fd = err_at(math.exp(c)), err_at(math.exp(d))
     while b - a > 1e-3:
         if fc < fd:
             b, d, fd = d, c, fc
             c = b - g * (b - a)
-            fc = err(c)
+            fc = err_at(math.exp(c))
         else:
             a, c, fc = c, d, fd
             d = a + g * (b - a)
-            fd = err(d)
-    lx = (a + b) / 2
-    e = err(lx)
-    return {"value": round(math.exp(lx), 3), "entries": len(pts), "rms_log_err": round(math.sqrt(e / len(pts)), 4)}
+            fd = err_at(math.exp(d))
+    v = math.exp((a + b) / 2)
+    e = err_at(v)
+    why = _identify(lambda y: err_at(y[0]), [v], e, [lo], [hi], len(pts))[0]
+    if why:
+        ftar.cost_set(**base)
+        return {"value": round(base[field], 3), "entries": len(pts), "unidentified": why,
+                "fitted_at": round(v, 3), "rms_log_err": rms(_log_sse(ftar, pts, world, bucket))}
+    err_at(v)
+    return {"value": round(v, 3), "entries": len(pts), "rms_log_err": rms(e), "unidentified": None}
 
 
 def _factorizations(n):
@@ -851,8 +937,7 @@ def bench_distributed(a):
         # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
         comm.peer_tuning(nt=tune != "plain", lds=tune != "vec", dma=tune == "dma")
-        # ":cusN": the reduce stream on N CUs, the rest left to RCCL's p2p kernels (DESIGN §4 co-scheduling)
-        comm.reduce_cus = int(tune[3:]) if tune.startswith("cus") else 0
+        # (no ":cusN": a CU-masked reduce stream is refused on RCCL communicators)
         # ":ncclreg": RCCL p2p between buffers registered with RCCL (ncclCommRegister): the comm's scratch
         # and registered copies of x and y, so RCCL may skip its staging copies where it supports that
         comm.rccl_register = tune == "ncclreg"
@@ -1266,8 +1351,6 @@ def bench_distributed(a):
             chunks = {4 << 20, 16 << 20, 64 << 20, mc}
             if key == str(default_topo) and form == "direct":  # 256 KiB ... 64 MiB
                 chunks |= {256 << 10, 1 << 20}
-                if a.sweep_cus:
-                    plan.append((t, mc, "direct:cus224"))
                 plan.append((t, mc, "direct:ncclreg"))
             if form == "stages" and t.ring:
                 chunks = {mc}  # the reference's ring rounds: one point is enough

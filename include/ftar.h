@@ -188,13 +188,26 @@ typedef struct {
   int form;            /* ftar_form_t */
   size_t chunk_bytes;  /* pipeline piece (the one-round and staged forms); 0 for the peer forms */
   double seconds;      /* predicted */
+  int tied;            /* candidates priced equal to the choice (within 1e-9), the choice included:
+                          1 = a strict argmin; > 1 = the model could not tell them apart */
+  int tie_broken_by;   /* ftar_tie_t: the highest-ranked rule that set the choice apart from a tied one */
 } ftar_exec_t;
+/* Tie rules of ftar_exec_choose, in the order they apply. */
+typedef enum {
+  FTAR_TIE_NONE = 0,    /* no tie */
+  FTAR_TIE_STAGES = 1,  /* the fewest stages (the ring last: the flat fold rounds bf16 once) */
+  FTAR_TIE_FORM = 2,    /* the simpler form (ftar_form_t order) */
+  FTAR_TIE_PIECE = 3    /* the larger piece (fewer p2p groups; whole blocks first) */
+} ftar_tie_t;
 #define FTAR_CHOOSE_TOPO 1  /* the topology is free (else inout->topo is used) */
 #define FTAR_CHOOSE_FORM 2  /* the form is free (else inout->form) */
 #define FTAR_CHOOSE_CHUNK 4 /* the piece size is free (else inout->chunk_bytes) */
 #define FTAR_CHOOSE_PEER 8  /* the peer forms may be chosen (their rates permitting) */
 /* The model's argmin over what `flags` leaves free; ties keep the fewest
- * stages, then the simpler form, then the larger piece. */
+ * stages, then the simpler form, then the larger piece, and the result says
+ * how many candidates tied and which rule decided (tied, tie_broken_by): in
+ * the direct form every one-round topology moves tree(P)'s bytes over the
+ * same links, so those price alike and the stage count picks tree(P). */
 ftar_status_t ftar_exec_choose(int nranks, size_t bytes, int flags, ftar_exec_t* inout);
 
 /* The reference's own cost model, restated bit for bit
@@ -256,8 +269,9 @@ ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes);
  * topology, the form of the path actually taken (host buffers on an RCCL
  * communicator run the pipelined p2p path whatever peer form is set; a ring
  * or host buffers replace the collective all-gather with the direct one; -2
- * for a mix no form names), the piece, and the model's predicted seconds
- * (-1: unpriced). */
+ * for a mix no form names), the piece it ran in bytes (host buffers: the
+ * host piece; 0: whole blocks, or a peer form on device buffers), and the
+ * model's predicted seconds (-1: unpriced). */
 ftar_status_t ftar_comm_set_form(ftar_comm_t comm, int form);
 ftar_status_t ftar_comm_get_form(ftar_comm_t comm, int* form);
 ftar_status_t ftar_comm_last_exec(ftar_comm_t comm, ftar_exec_t* out);
@@ -364,10 +378,12 @@ ftar_status_t ftar_allreduce_host_group(const void* const* sendbufs, void* const
 /* Co-scheduling of the fold with the transport: the reduce stream runs on
  * `cus` of the device's CUs (spread evenly; 0 = all, the default), so the
  * comm stream's kernels (RCCL p2p, copies) always find free CUs while a
- * piece's fold runs (FTAR_REDUCE_CUS at init).  Same bits either way.  The
- * CU-masked stream is blocking towards the legacy NULL stream; calls over RCCL
- * with it were seen to stall once under the stress driver (DESIGN.md §5,
- * open): keep it off on RCCL communicators for now. */
+ * piece's fold runs (FTAR_REDUCE_CUS at init).  Same bits either way.
+ * In-process (local) and host-bootstrapped communicators only: on an RCCL
+ * communicator any cus other than 0 returns FTAR_ERR_UNSUPPORTED, and
+ * FTAR_REDUCE_CUS fails ftar_comm_init_rank the same way.  The CU-masked
+ * stream is a blocking stream on a hardware queue of its own, and over RCCL
+ * two stress runs stalled ranks with it. */
 ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus);
 ftar_status_t ftar_comm_get_reduce_cus(ftar_comm_t comm, int* cus);
 /* Host-mode piece size per block (bytes, rounded to 256 B); 0 = auto: 16 MiB,

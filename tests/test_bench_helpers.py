@@ -84,7 +84,7 @@ def test_links_driven():
     assert bench.links_driven(8, "ring", "stages") == 1
     assert bench.links_driven(8, "2,4", "stages") == 3
     assert bench.links_driven(5, "2,2+1", "stages") == 1
-    assert bench.links_driven(2, "2", "direct:cus224") == 1
+    assert bench.links_driven(2, "2", "direct:ncclreg") == 1
 
 
 def test_rccl_p2p_best_is_reported_when_a_peer_form_wins():
@@ -96,7 +96,7 @@ def test_rccl_p2p_best_is_reported_when_a_peer_form_wins():
     sweep = [
         {"topology": "8", "chunk_bytes": 16 << 20, "form": "direct", "ms": 6.0, "check": "ok"},
         {"topology": "8", "chunk_bytes": 1 << 20, "form": "direct", "ms": 5.5, "check": "MISMATCH (sample)"},
-        {"topology": "8", "chunk_bytes": 4 << 20, "form": "direct:cus224", "ms": 5.8, "check": "ok"},
+        {"topology": "8", "chunk_bytes": 4 << 20, "form": "direct:ncclreg", "ms": 5.8, "check": "ok"},
         {"topology": "8", "chunk_bytes": 16 << 20, "form": "collective", "ms": 5.0, "check": "ok"},
         {"topology": "ring", "chunk_bytes": 16 << 20, "form": "stages", "ms": 40.0, "check": "ok"},
         {"topology": "8", "chunk_bytes": 16 << 20, "form": "peer-write-reg", "ms": 4.0, "check": "ok"},
@@ -104,7 +104,7 @@ def test_rccl_p2p_best_is_reported_when_a_peer_form_wins():
         {"skipped": "sweep budget"},
     ]
     best = bench.rccl_p2p_best(sweep, 8, 8, bucket, lambda r: bench.links_driven(8, r["topology"], r["form"]))
-    assert best["form"] == "direct:cus224" and best["chunk_bytes"] == 4 << 20 and best["ms"] == 5.8
+    assert best["form"] == "direct:ncclreg" and best["chunk_bytes"] == 4 << 20 and best["ms"] == 5.8
     assert best["roofline"]["bound"] == "xgmi" and best["roofline"]["peak"] == pytest.approx(7 * 76.8)
     alg = bucket / 5.8e-3 / 1e9
     assert best["busbw_GBps_per_rank"] == pytest.approx(alg * 14 / 8, rel=1e-3)
@@ -218,9 +218,10 @@ def _synthetic_sweep(ftar, bench, world, bucket, true):
                     continue
                 sweep.append({"topology": topo, "form": form, "chunk_bytes": c, "check": "ok",
                               "ms": bench.predict_ms(ftar, topo, form, c, world, bucket)})
-    for form in ("peer-read", "peer-write", "peer-read-reg", "peer-write-reg:plain"):
-        sweep.append({"topology": "8", "form": form, "chunk_bytes": 0, "check": "ok",
-                      "ms": bench.predict_ms(ftar, "8", form, 0, world, bucket)})
+    for topo in ("8", "2,4", "ring"):   # one-round plans: the peer forms run each
+        for form in ("peer-read", "peer-write", "peer-read-reg") + (("peer-write-reg:plain",) if topo == "8" else ()):
+            sweep.append({"topology": topo, "form": form, "chunk_bytes": 0, "check": "ok",
+                          "ms": bench.predict_ms(ftar, topo, form, 0, world, bucket)})
     sweep.append({"topology": "8", "form": "collective", "chunk_bytes": 16 << 20, "check": "ok",
                   "ms": bench.predict_ms(ftar, "8", "collective", 16 << 20, world, bucket)})
     sweep.append({"topology": "8", "form": "direct", "chunk_bytes": 1 << 20, "check": "MISMATCH (sample)",
@@ -233,7 +234,7 @@ def test_sweep_forms_are_priced_as_their_base_form(model_defaults):
     import bench
     ftar = model_defaults
     assert bench.sweep_form("peer-read-reg:wg16") == ("peer-read", True)
-    assert bench.sweep_form("direct:cus224") == ("direct", False)
+    assert bench.sweep_form("direct:ncclreg") == ("direct", False)
     assert bench.predict_ms(ftar, "8", "direct:ncclreg", 1 << 20, 8, 1 << 30) == \
         bench.predict_ms(ftar, "8", "direct", 1 << 20, 8, 1 << 30)
     assert bench.predict_ms(ftar, "8", "peer-read", 0, 8, 1 << 30) is None   # no peer rate yet
@@ -272,22 +273,87 @@ def test_refit_recovers_the_constants_of_a_synthetic_node(model_defaults, true):
     sweep = _synthetic_sweep(ftar, bench, world, bucket, dict(true, peer_read_gbps=90.0, peer_write_gbps=70.0,
                                                              coll_gbps=300.0))
     fit = bench.refit_cost_model(ftar, sweep, world, bucket, fixed={"issue_us": true["issue_us"]})
-    assert fit["entries"] == 26 and fit["rms_log_err"] < 0.01
+    assert fit["entries"] == 26 and fit["rms_log_err"] < 0.01 and fit["unidentified"] == {}
     assert fit["params"]["alpha_us"] == pytest.approx(true["alpha_us"], rel=0.05)
     assert fit["params"]["link_gbps"] == pytest.approx(true["link_gbps"], rel=0.02)
     for field, forms, want in (("peer_read_gbps", ("peer-read", "peer-read-reg"), 90.0),
-                               ("peer_write_gbps", ("peer-write", "peer-write-reg"), 70.0),
-                               ("coll_gbps", ("collective",), 300.0)):
+                               ("peer_write_gbps", ("peer-write", "peer-write-reg"), 70.0)):
         r = bench.refit_form_rate(ftar, sweep, world, bucket, field, forms)
         if field == "peer_write_gbps":   # the ":plain" entry is a tuning variant, not a fit point
-            assert r["entries"] == 1
-        assert r["value"] == pytest.approx(want, rel=0.02), field
-    assert ftar.cost_get()["coll_gbps"] == pytest.approx(300.0, rel=0.02)   # left on the fitted constants
+            assert r["entries"] == 3
+        assert r["unidentified"] is None and r["value"] == pytest.approx(want, rel=0.02), field
+    # the collective ran once: too few entries to fit a rate -- flagged, the prior (unmeasured: 0) kept
+    r = bench.refit_form_rate(ftar, sweep, world, bucket, "coll_gbps", ("collective",))
+    assert r["entries"] == 1 and r["unidentified"].startswith("entries") and r["value"] == 0.0
+    assert ftar.cost_get()["coll_gbps"] == 0.0
+    assert ftar.cost_get()["peer_write_gbps"] == pytest.approx(70.0, rel=0.02)   # left on the fitted constants
 
 
-def test_refit_needs_three_validated_points(model_defaults):
+def test_refit_with_too_few_points_keeps_the_priors(model_defaults):
+    """Fewer entries than free constants + 2: nothing is fitted, every free constant is flagged and keeps
+    its prior (the value set when the refit started)."""
     import bench
     ftar = model_defaults
-    assert bench.refit_cost_model(ftar, [{"form": "direct", "topology": "8", "chunk_bytes": 1 << 20, "ms": 5.0,
-                                          "check": "ok"}], 8, 1 << 30) is None
+    ftar.cost_set(alpha_us=33.0, link_gbps=44.0, issue_us=22.0)
+    prior = ftar.cost_get()
+    one = [{"form": "direct", "topology": "8", "chunk_bytes": 1 << 20, "ms": 5.0, "check": "ok"}] * 3
+    fit = bench.refit_cost_model(ftar, one, 8, 1 << 30)
+    assert set(fit["unidentified"]) == {"alpha_us", "link_gbps", "issue_us"}
+    assert all(v.startswith("entries") for v in fit["unidentified"].values())
+    assert fit["prior"] == {"alpha_us": 33.0, "link_gbps": 44.0, "issue_us": 22.0}
+    assert ftar.cost_get() == pytest.approx(prior)
+    assert bench.refit_cost_model(ftar, [], 8, 1 << 30) is None
     assert bench.refit_form_rate(ftar, [], 8, 1 << 30, "coll_gbps", ("collective",)) is None
+
+
+def test_refit_flags_a_flat_direction_and_keeps_its_prior(model_defaults):
+    """Issue held at its measured value (as bench.py does), and every piece so small that the link term is
+    a rounding error next to alpha: the predictions do not depend on link, so it is flagged "flat" and keeps
+    its prior; alpha is fitted."""
+    import bench
+    ftar = model_defaults
+    world, bucket = 8, 1 << 30
+    ftar.cost_set(alpha_us=5000.0, link_gbps=60.0, issue_us=25.0)
+    sweep = [{"topology": t, "form": "direct", "chunk_bytes": c, "check": "ok",
+              "ms": bench.predict_ms(ftar, t, "direct", c, world, bucket)}
+             for t in ("8", "2,4", "ring") for c in (256 << 10, 1 << 20)]
+    ftar.cost_set(alpha_us=20.0, link_gbps=54.0, issue_us=25.0)   # the priors
+    fit = bench.refit_cost_model(ftar, sweep, world, bucket, fixed={"issue_us": 25.0})
+    assert fit["unidentified"] == {"link_gbps": "flat"} and fit["prior"] == {"link_gbps": 54.0}
+    assert fit["params"]["link_gbps"] == 54.0 and ftar.cost_get()["link_gbps"] == pytest.approx(54.0)
+    assert fit["params"]["alpha_us"] == pytest.approx(5000.0, rel=0.02)
+
+
+def test_refit_flags_confounded_constants(model_defaults):
+    """Every piece host-issue bound and issue left free: "each piece costs 3 ms" is explained as well by
+    alpha as by issue (and link then does not matter), so no constant is pinned -- all three keep their
+    priors instead of a self-consistent but wrong alpha = 3 ms."""
+    import bench
+    ftar = model_defaults
+    world, bucket = 8, 1 << 30
+    ftar.cost_set(alpha_us=35.0, link_gbps=60.0, issue_us=3000.0)
+    sweep = [{"topology": t, "form": "direct", "chunk_bytes": c, "check": "ok",
+              "ms": bench.predict_ms(ftar, t, "direct", c, world, bucket)}
+             for t in ("8", "2,4", "ring") for c in (256 << 10, 1 << 20)]
+    ftar.cost_set(alpha_us=20.0, link_gbps=54.0, issue_us=25.0)
+    fit = bench.refit_cost_model(ftar, sweep, world, bucket)
+    assert set(fit["unidentified"]) == {"alpha_us", "link_gbps", "issue_us"}
+    assert "confounded" in fit["unidentified"].values()
+    assert (fit["params"]["alpha_us"], fit["params"]["link_gbps"], fit["params"]["issue_us"]) == (20.0, 54.0, 25.0)
+
+
+def test_refit_flags_a_constant_on_its_search_bound(model_defaults):
+    """Timings no link rate in the search box explains (here: far slower than the slowest link) drive link
+    onto its lower bound: flagged "bound", the prior kept -- the loopback rehearsal's link = 0.5 GB/s of
+    round 4 would now read that way."""
+    import bench
+    ftar = model_defaults
+    world, bucket = 8, 1 << 30
+    ftar.cost_set(alpha_us=20.0, link_gbps=0.01, issue_us=25.0)   # 10 MB/s per link
+    sweep = [{"topology": t, "form": f, "chunk_bytes": c, "check": "ok",
+              "ms": bench.predict_ms(ftar, t, f, c, world, bucket)}
+             for t in ("8", "2,4") for f in ("direct", "stages") for c in (4 << 20, 64 << 20)]
+    ftar.cost_set(alpha_us=20.0, link_gbps=54.0, issue_us=25.0)
+    fit = bench.refit_cost_model(ftar, sweep, world, bucket, fixed={"issue_us": 25.0})
+    assert fit["unidentified"].get("link_gbps") == "bound"
+    assert fit["params"]["link_gbps"] == 54.0
