@@ -357,3 +357,36 @@ def test_refit_flags_a_constant_on_its_search_bound(model_defaults):
     fit = bench.refit_cost_model(ftar, sweep, world, bucket, fixed={"issue_us": 25.0})
     assert fit["unidentified"].get("link_gbps") == "bound"
     assert fit["params"]["link_gbps"] == 54.0
+
+
+def test_form_labels_say_what_moved():
+    """Every N > 1 line names its form in words: the one-round ring is a gather plus a
+    fold in the ring's order, the staged ring the reference's own steps."""
+    import bench
+    assert bench.form_label("ring", "direct") == "direct (gather + ring-order fold)"
+    assert bench.form_label("1", "direct") == "direct (gather + ring-order fold)"
+    assert bench.form_label("ring", "stages") == "stages (reference ring steps)"
+    assert bench.form_label("8", "direct") == "direct (gather + tree-order fold)"
+    assert bench.form_label("2,4", "stages") == "stages (reference tree stages)"
+    assert bench.form_label("8", "collective").startswith("collective (gather + tree-order fold")
+    assert bench.form_label("8", "peer-read-reg:plain") == \
+        "peer-read (IPC loads over xGMI + tree-order fold) on registered buffers [plain]"
+    assert bench.form_label("ring", "direct:ncclreg") == "direct (gather + ring-order fold) [ncclreg]"
+
+
+def test_c4_ring_item_labels_each_rccl_form(model_defaults):
+    import bench
+    bucket = 1 << 30
+    sweep = [{"topology": "ring", "form": "direct", "chunk_bytes": c, "ms": ms, "check": "ok"}
+             for c, ms in ((4 << 20, 9.0), (64 << 20, 7.0))]
+    sweep += [{"topology": "ring", "form": "stages", "chunk_bytes": 16 << 20, "ms": 40.0, "check": "ok"},
+              {"topology": "8", "form": "direct", "chunk_bytes": 64 << 20, "ms": 6.0, "check": "ok"},
+              {"topology": "ring", "form": "direct", "chunk_bytes": 1 << 20, "ms": 1.0, "check": "MISMATCH (x)"}]
+    out = bench.c4_ring_by_form(sweep, 8, 8, bucket, lambda r: bench.links_driven(8, r["topology"], r["form"]))
+    assert set(out) == {"direct", "stages"}
+    assert out["direct"]["form_label"] == "direct (gather + ring-order fold)" and out["direct"]["judged"]
+    assert out["direct"]["ms"] == 7.0 and out["direct"]["pieces_swept"] == [1 << 20, 4 << 20, 64 << 20]
+    assert out["stages"]["form_label"] == "stages (reference ring steps)" and not out["stages"]["judged"]
+    assert out["stages"]["roofline"]["peak"] == pytest.approx(76.8) and out["direct"]["roofline"]["peak"] == pytest.approx(7 * 76.8)
+    best = bench.rccl_p2p_best(sweep, 8, 8, bucket, lambda r: bench.links_driven(8, r["topology"], r["form"]))
+    assert best["form_label"] == "direct (gather + tree-order fold)"

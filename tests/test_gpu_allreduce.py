@@ -177,6 +177,39 @@ def test_rccl_single_rank_comm():
         comm.destroy()
 
 
+def test_rccl_comm_refuses_a_cu_masked_reduce_stream(monkeypatch):
+    """The rule of DESIGN §4: on an RCCL communicator the reduce stream stays on every CU -- a CU share is
+    refused with FTAR_ERR_UNSUPPORTED (the setter, and FTAR_REDUCE_CUS at bring-up), 0 is accepted, and the
+    communicator still runs; an in-process group keeps the knob."""
+    import ftar
+    comm = ftar.Comm.init_rank(1, ftar.get_unique_id(), 0, 0)
+    try:
+        for cus in (32, 128, 255):
+            with pytest.raises(ftar.FtarError) as e:
+                comm.reduce_cus = cus
+            assert e.value.status == 2 and "rccl" in str(e.value).lower()
+            assert comm.reduce_cus == 0
+        comm.reduce_cus = 0
+        comm.reduce_cus = 100000   # >= every CU: the same as 0
+        assert comm.reduce_cus == 0
+        x = fi.fill("f32", 2, 0, 4096)
+        s, sp = to_dev(x)
+        d, dp = filled_dev(x.nbytes)
+        assert ftar.MPI_Allreduce_FT(sp, dp, 4096, "MPI_FLOAT", "MPI_SUM", comm) == 0
+        np.testing.assert_array_equal(from_dev(d, np.float32, 4096), x)
+    finally:
+        comm.destroy()
+    monkeypatch.setenv("FTAR_REDUCE_CUS", "64")
+    with pytest.raises(ftar.FtarError) as e:
+        ftar.Comm.init_rank(1, ftar.get_unique_id(), 0, 0)
+    assert e.value.status == 2
+    g = ftar.Comm.init_local(2)   # in-process: the masked stream is allowed
+    try:
+        assert all(c.reduce_cus == 64 for c in g.comms)
+    finally:
+        g.destroy()
+
+
 @pytest.mark.parametrize("P,topo", [(2, "2"), (4, "2,2"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3")])
 @pytest.mark.parametrize("outofplace", [False, True])
 def test_allreduce_collective_allgather(P, topo, outofplace):
