@@ -1,0 +1,148 @@
+// Host buffers on a host-bootstrapped communicator (engine_state.h): the read form piece by piece, H2D /
+// exchange / D2H overlapped (the MPI drop-in's `ipc` transport).  Split out of engine.cpp (round 5); no
+// behaviour change.
+#include <algorithm>
+
+#include "engine_state.h"
+
+using ftar::hip_ignore;
+
+namespace ftar {
+
+constexpr size_t kMaxHostPeerPieces = 1024;  // peer_allreduce_host: pieces per call (a host barrier each)
+
+// Elements per piece of peer_allreduce_host.  Auto: at least 8 pieces per block down to 4 MiB (2 ranks
+// on one GPU, 64 MiB buckets: 4 MiB pieces 16.5 GB/s vs 12.6 with two 16 MiB pieces;
+// profiles/r02/s4/host_ipc/), else the p2p host path's rule; every piece costs a host barrier and two
+// events, so at most kMaxHostPeerPieces pieces per call.
+size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
+  const size_t chunk_bytes =
+      c->host_chunk_bytes
+          ? c->host_chunk_bytes
+          : std::max(split * esz / 64, std::min<size_t>(16u << 20, std::max<size_t>(4u << 20, split * esz / 8)));
+  const size_t floor_elems = (split + kMaxHostPeerPieces - 1) / kMaxHostPeerPieces;
+  return std::max<size_t>({64, (chunk_bytes / esz) & ~size_t(63), (floor_elems + 63) & ~size_t(63)});
+}
+
+// Host buffers on a communicator without point-to-point transfers (ftar_comm_init_host: the MPI
+// drop-in's `ipc` transport), the read form piece by piece, as the p2p host path pipelines its
+// stages.  Piece k is elements [k*chunk, (k+1)*chunk) of every block.
+//   * every piece goes H2D straight into the exchange buffer X on its own stream, all issued up
+//     front, so the copy engines run ahead (no staging buffer, no copy-in pass);
+//   * once every rank's piece k is in (a barrier), the fold of my block's piece k reads the peers'
+//     copies from their X over xGMI and writes my X in place (the plan's fold: same bits);
+//   * once every rank's fold of piece k is done (the next barrier, which also says piece k+1 is in
+//     everywhere), the other owners' final pieces are pulled into my X at their offsets, and piece
+//     k of the whole bucket goes D2H on its own stream while later pieces come in.
+// A peer reads my X only at its own block (fold) and at my block (gather), and I overwrite my X
+// only at my block (fold, before anyone gathers it) and at the others' blocks (gather, after every
+// fold of that piece), so pieces never conflict.  The barriers synchronise the host: m pieces take
+// m + 2 barriers, the last so that no peer still reads my X when the next call's H2D refills it.
+ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t dt, ftar_op_t op, const Plan& plan,
+                                  ftar_comm* c, hipStream_t stream) {
+  const size_t esz = dtype_size(dt), bytes = count * esz;
+  FTAR_RETURN_IF(ensure_xbuf(c, bytes));  // collective, before the first barrier
+  Transport* tp = c->tp.get();
+  char* X = static_cast<char*>(c->xbuf);
+  const std::vector<char*>& Xq = c->xpeers;
+  const Stage& rs = plan.stages[0];
+  const Stage& ag = plan.stages[1];
+  const size_t P = (size_t)c->nranks, split = plan.split;
+  const size_t chunk = host_peer_piece(c, split, esz);
+  const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
+  // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
+  // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
+  // so all of them leave the call at the same barrier instead of some waiting in the next.
+  ftar_status_t st = grow_events(c, 5 + 2 * m);
+  auto work = [&](auto&& fn) {
+    if (st == FTAR_SUCCESS) st = fn();
+  };
+  // a failed call leaves only after its copies stopped touching the caller's host buffers: H2D reads of
+  // io.src and D2H writes of io.dst may still be in flight on their streams
+  auto leave = [&]() -> ftar_status_t {
+    for (hipStream_t s : {c->h2d_s, c->d2h_s, c->comm_s})
+      if (s) hip_ignore(hipStreamSynchronize(s));
+    return st;
+  };
+  auto sync = [&]() -> bool {  // a barrier; false: some rank failed, leave the call
+    bool all_ok = true;
+    const ftar_status_t b = tp->barrier_status(c->comm_s, st == FTAR_SUCCESS, &all_ok);
+    if (b != FTAR_SUCCESS) {  // the host collective itself failed: nothing left to agree with
+      if (st == FTAR_SUCCESS) st = b;
+      return false;
+    }
+    if (!all_ok && st == FTAR_SUCCESS) {
+      set_error("peer_allreduce_host: another rank failed", __FILE__, __LINE__);
+      st = FTAR_ERR_INTERNAL;
+    }
+    return all_ok;
+  };
+  hipEvent_t* ev = c->events.data();
+  auto ev_h = [&](size_t k) { return c->events[5 + 2 * k]; };      // piece k is in my X
+  auto ev_g = [&](size_t k) { return c->events[5 + 2 * k + 1]; };  // piece k is final in my X
+  auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {  // piece k of every block, clipped
+    for (size_t b = 0; b < P; ++b) {
+      const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
+      if (lo < end) FTAR_RETURN_IF(fn(lo, std::min(chunk, end - lo)));
+    }
+    return FTAR_SUCCESS;
+  };
+  work([&]() -> ftar_status_t {
+    ev = c->events.data();
+    FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
+    for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
+    c->nmarks = 0;
+    FTAR_RETURN_IF(mark(c, "start", c->comm_s));
+    for (size_t k = 0; k < m; ++k) {
+      FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
+        return FTAR_SUCCESS;
+      }));
+      FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
+    }
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
+    return FTAR_SUCCESS;
+  });
+  if (!sync()) return leave();  // piece 0 is in everywhere
+  work([&] { return mark(c, "piece 0 in", c->comm_s); });
+  std::vector<Segment> segs;
+  for (size_t k = 0; k < m; ++k) {
+    const size_t lo = k * chunk;
+    work([&]() -> ftar_status_t {
+      for (const ReduceItem& r : rs.reduces)
+        FTAR_RETURN_IF(peer_fold(
+            r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
+            [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
+      if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
+      return FTAR_SUCCESS;
+    });
+    if (!sync()) return leave();  // piece k folded everywhere (and piece k+1 in)
+    work([&]() -> ftar_status_t {
+      segs.clear();
+      for (const Transfer& x : ag.recvs)
+        if (x.len > lo)
+          segs.push_back(
+              {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
+      if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
+      FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
+      FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
+      return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(
+            hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+        return FTAR_SUCCESS;
+      });
+    });
+  }
+  work([&] { return mark(c, "pieces folded and gathered", c->comm_s); });
+  if (!sync()) return leave();  // no peer reads my X after the call
+  if (st != FTAR_SUCCESS) return leave();
+  FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
+  FTAR_RETURN_IF(tp->before_join());
+  FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[2], c->d2h_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[3], c->h2d_s));
+  for (int i = 1; i <= 3; ++i) FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[i], 0));
+  return FTAR_SUCCESS;
+}
+
+}  // namespace ftar
