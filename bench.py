@@ -736,8 +736,10 @@ def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
     measured directly (e.g. {"issue_us": ...}) that the search keeps.  A constant the sweep cannot pin
     (fewer entries than free constants + 2, a search bound, a flat direction) keeps its prior -- the value
     set when the refit started (the probe's, or the default) -- and is listed in "unidentified" with the
-    reason; the others are fitted again with it held.  Leaves the model on the result and returns
-    {"params", "entries", "rms_log_err", "unidentified", "prior"} (None: no validated entry)."""
+    reason; the others are fitted again with it held, and if the result predicts the sweep no better than
+    the prior constants did, the priors are kept whole ("kept_prior").  Leaves the model on the result and
+    returns {"params", "entries", "rms_log_err", "rms_log_err_prior", "unidentified", "prior",
+    "kept_prior"} (None: no validated entry)."""
     import math
     pts = [r for r in sweep if r.get("check") == "ok" and "ms" in r and r.get("form") in ("direct", "stages")]
     if not pts:
@@ -780,11 +782,21 @@ def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
     final = dict(base, **fixed, **{k: base[k] for k in unidentified})
     if free:
         final.update(dict(zip(free, x)))
+    ftar.cost_set(**dict(base, **fixed))
+    sse_prior = _log_sse(ftar, pts, world, bucket)
     params = ftar.cost_set(**final)
     sse = _log_sse(ftar, pts, world, bucket)
-    return {"params": {k: round(v, 3) for k, v in params.items()}, "entries": len(pts),
-            "rms_log_err": round(math.sqrt(sse / len(pts)), 4) if sse < float("inf") else None,
-            "unidentified": unidentified, "prior": {k: round(base[k], 3) for k in unidentified}}
+    kept_prior = bool(free) and not sse < sse_prior
+    if kept_prior:   # the fit explains the sweep no better than the constants it started from: keep those
+        params = ftar.cost_set(**dict(base, **fixed))
+        sse = sse_prior
+
+    def rms(e):
+        return round(math.sqrt(e / len(pts)), 4) if e < float("inf") else None
+    return {"params": {k: round(v, 3) for k, v in params.items()}, "entries": len(pts), "rms_log_err": rms(sse),
+            "rms_log_err_prior": rms(sse_prior), "unidentified": unidentified,
+            "prior": {k: round(base[k], 3) for k in unidentified},
+            "kept_prior": "the refit predicted the sweep no better than the prior constants" if kept_prior else None}
 
 
 def refit_form_rate(ftar, sweep, world, bucket, field, forms):

@@ -390,3 +390,41 @@ def test_c4_ring_item_labels_each_rccl_form(model_defaults):
     assert out["stages"]["roofline"]["peak"] == pytest.approx(76.8) and out["direct"]["roofline"]["peak"] == pytest.approx(7 * 76.8)
     best = bench.rccl_p2p_best(sweep, 8, 8, bucket, lambda r: bench.links_driven(8, r["topology"], r["form"]))
     assert best["form_label"] == "direct (gather + tree-order fold)"
+
+
+def _round4_loopback_line():
+    import json
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "profiles", "r04", "loopback", "dist8_loopback_1GiB.json")
+    with open(path) as f:
+        for line in f:
+            if line.startswith("{"):
+                return json.loads(line)
+    raise AssertionError("no bench line in " + path)
+
+
+def test_refit_of_the_round4_loopback_sweep_leaves_no_constant_on_a_bound(model_defaults):
+    """Round 4's 8-rank RCCL loopback rehearsal (1 GiB per rank, sockets) re-fitted its constants onto
+    link = 0.5 GB/s (the search floor) and peer_write = 4,981 GB/s from 2 entries.  The same sweep through
+    today's refit: link is flagged "bound" and keeps the probe's value, the 2-entry peer rates and the
+    collective rate on its floor keep theirs, and no returned constant sits on a search bound."""
+    import bench
+    ftar = model_defaults
+    d = _round4_loopback_line()
+    cm = d["cost_model"]
+    ftar.cost_set(**cm["constants_probe"])
+    p2p = bench.refit_cost_model(ftar, d["sweep"], 8, 1 << 30, fixed={"issue_us": cm["issue_us_from_enqueue"]})
+    assert p2p["unidentified"] == {"link_gbps": "bound"}
+    assert p2p["params"]["link_gbps"] == pytest.approx(cm["constants_probe"]["link_gbps"])
+    assert p2p["rms_log_err"] < p2p["rms_log_err_prior"]
+    for k, lo, hi in (("alpha_us", 0.1, 1e5), ("link_gbps", 0.5, 5e3)):
+        assert lo * 1.01 < p2p["params"][k] < hi / 1.01, (k, p2p["params"][k])
+    rates = {f: bench.refit_form_rate(ftar, d["sweep"], 8, 1 << 30, f, forms)
+             for f, forms in (("peer_read_gbps", ("peer-read", "peer-read-reg")),
+                              ("peer_write_gbps", ("peer-write", "peer-write-reg")),
+                              ("coll_gbps", ("collective",)))}
+    assert rates["peer_write_gbps"]["unidentified"].startswith("entries")
+    assert rates["peer_write_gbps"]["value"] == pytest.approx(cm["constants_probe"]["peer_write_gbps"])
+    assert rates["coll_gbps"]["unidentified"] == "bound" and rates["coll_gbps"]["value"] == 0.0
+    for r in rates.values():
+        assert r["value"] == 0.0 or 1.01 < r["value"] < 5000 / 1.01

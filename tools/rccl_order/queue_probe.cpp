@@ -7,9 +7,11 @@
 // internal streams (comm, reduce, H2D, D2H) plus a caller stream, and for every ordered pair (X, Y) launches
 // a kernel on X that spins until released (or 2 s pass), then a trivial kernel on Y: if Y's kernel cannot
 // finish within 300 ms while X spins, X and Y share a queue.  Optional extra streams: a CU-masked stream
-// with every CU ("masked"), which the runtime gives a queue of its own, and a high-priority stream ("prio").
+// with every CU ("masked"), which the runtime gives a queue of its own, and a high-priority stream ("prio");
+// the legacy NULL stream ("null", the caller stream of the engine stress driver): a blocking stream such as
+// the masked one also waits for it (and it for them) without sharing a queue, which the pairs show as well.
 //
-// Usage: queue_probe [--comms K] [--masked] [--prio]     (prints "SHARE <x> <y> yes|no" and a summary)
+// Usage: queue_probe [--comms K] [--masked] [--prio] [--null]   (prints "SHARE <x> <y> yes|no" and a summary)
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -48,12 +50,13 @@ __global__ void marker_kernel(int* out) { out[threadIdx.x] = 1; }
 
 int main(int argc, char** argv) {
   int ncomms = 1;
-  bool masked = false, prio = false;
+  bool masked = false, prio = false, null_stream = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "--comms" && i + 1 < argc) ncomms = atoi(argv[++i]);
     else if (a == "--masked") masked = true;
     else if (a == "--prio") prio = true;
+    else if (a == "--null") null_stream = true;
   }
   CHECK(hipSetDevice(0));
   int khz = 0;
@@ -64,6 +67,7 @@ int main(int argc, char** argv) {
   hipStream_t user;
   CHECK(hipStreamCreateWithFlags(&user, hipStreamNonBlocking));
   st.emplace_back("caller", user);
+  if (null_stream) st.emplace_back("null", static_cast<hipStream_t>(nullptr));
   std::vector<ftar_comm_t> comms;
   for (int c = 0; c < ncomms; ++c) {
     ftar_unique_id_t id;
