@@ -33,7 +33,8 @@ def _bench(ranks, extra, env_extra=None):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("ranks,extra", [(2, ["--host-comm"]), (4, ["--host-comm"]), (2, [])])
+@pytest.mark.parametrize("ranks,extra", [(2, ["--host-comm"]), pytest.param(4, ["--host-comm"], marks=pytest.mark.wide),
+                                         (2, [])])
 def test_bench_n_gt_1_rehearsal(ranks, extra):
     d = _bench(ranks, extra)
     assert d["n_gpus"] == ranks and d["check"] == "ok" and d["config"]["form"].startswith("peer-")
@@ -57,7 +58,10 @@ def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
     rank's error and the stage times, and rccl_p2p_best is absent because no RCCL configuration was measured.
     The hang is real: a spinning wave keeps the bench's stream from draining until the run ends,
     and the fallback runs on a fresh stream -- still blocked when the fallback's default was measured."""
-    d = _bench(1, ["--force-dist", "--no-cpu-baseline"], dict(env_extra, FTAR_BENCH_PREFLIGHT_S="5"))
+    # the fallback's sweep is not what is tested here: a short budget (the spinning wave of the hang case
+    # slows every later kernel until the run ends)
+    d = _bench(1, ["--force-dist", "--no-cpu-baseline", "--no-c5"],
+               dict(env_extra, FTAR_BENCH_PREFLIGHT_S="5", FTAR_BENCH_SWEEP_S="5"))
     assert d["check"] == "ok" and d["config"]["form"].startswith("peer-"), d["config"]
     assert why in d["rccl_init_error"], d["rccl_init_error"]
     assert len(d["rccl_error_by_rank"]) == 1 and why in d["rccl_error_by_rank"][0]["error"]
@@ -85,6 +89,16 @@ def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
     assert all("model_ms_refit" in r for r in d["sweep"] if r.get("check") == "ok"), d["sweep"]
     best = d["rccl_p2p_best"]
     assert best and best["form"].split(":")[0] in ("direct", "stages") and best["ms"] > 0, best
+    # every form says in words what moved (a gather never reads as a ring)
+    assert best["form_label"].startswith(best["form"].split(":")[0] + " ("), best
+    assert d["config"]["form_label"].startswith(d["config"]["form"].split(":")[0].replace("-reg", "")), d["config"]
+    for form, item in (d.get("c4_ring") or {}).items():
+        assert item["form_label"] in ("direct (gather + ring-order fold)", "stages (reference ring steps)"), item
+        assert item["judged"] == (form == "direct")
+    # the refit leaves no constant on a search bound: such a constant is flagged and keeps its prior
+    p2p = cm["refit_p2p"]
+    assert p2p is None or all(lo * 1.01 < p2p["params"][k] < hi / 1.01 or k in p2p["unidentified"]
+                              for k, lo, hi in (("alpha_us", 0.1, 1e5), ("link_gbps", 0.5, 5e3))), p2p
     rccl_ok = [r for r in d["sweep"] if r.get("check") == "ok" and r["form"].split(":")[0] in ("direct", "stages",
                                                                                                 "collective")]
     assert rccl_ok and not [r for r in d["sweep"] if r.get("check") == "MISMATCH"], d["sweep"]

@@ -22,14 +22,16 @@ def _run(args, timeout):
     return p
 
 
-def test_in_process_groups():
-    p = _run([500, 5], 240)
+@pytest.mark.parametrize("calls", [200, pytest.param(1500, marks=pytest.mark.wide)])
+def test_in_process_groups(calls):
+    p = _run([calls, 5], 240)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
     stats = json.loads(p.stdout.strip().splitlines()[-1])
-    assert stats["checked"] == stats["calls"] >= 500 and stats["groups"] >= 8 and stats["captured"] > 0, stats
+    assert stats["checked"] == stats["calls"] >= calls and stats["groups"] >= 3 and stats["captured"] > 0, stats
 
 
-@pytest.mark.parametrize("mode,P,calls,seed", [("rccl", 4, 40, 41), ("rccl", 8, 16, 12), ("host", 4, 60, 43)])
+@pytest.mark.parametrize("mode,P,calls,seed", [pytest.param("rccl", 4, 40, 41, marks=pytest.mark.wide), ("rccl", 8, 16, 12),
+                                               ("host", 4, 30, 43), pytest.param("host", 4, 60, 43, marks=pytest.mark.wide)])
 def test_processes(mode, P, calls, seed):
     p = _run([mode, P, calls, seed, 2], 240)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])

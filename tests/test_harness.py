@@ -113,8 +113,9 @@ def test_harness_device_resident_single_rank(tmp_path):
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("ranks,topo,extra", [(2, "2", []), (2, "1", []), (4, "2,2", []), (4, "4", ["--device"]),
-                                              (2, "2", ["--to-file", "--tag", "ipc"])])
+@pytest.mark.parametrize("ranks,topo,extra", [(2, "2", []), pytest.param(2, "1", [], marks=pytest.mark.wide),
+                                              pytest.param(4, "2,2", [], marks=pytest.mark.wide), (4, "4", ["--device"]),
+                                              pytest.param(2, "2", ["--to-file", "--tag", "ipc"], marks=pytest.mark.wide)])
 def test_harness_ranks_sharing_a_gpu_fall_back_to_ipc(tmp_path, ranks, topo, extra):
     """MPI_Allreduce_FT with several MPI ranks on the box's one GPU: RCCL refuses ranks that share a device,
     every rank agrees to fall back (FTAR_MPI_TRANSPORT=auto) to a communicator bootstrapped over MPI itself,
@@ -127,8 +128,11 @@ def test_harness_ranks_sharing_a_gpu_fall_back_to_ipc(tmp_path, ranks, topo, ext
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
-@pytest.mark.parametrize("case_id", ["ar_P2_t1_l0_f32_op0_n1048576_lin", "ar_P8_t8_l0_f32_op0_n65536_lin"])
+@pytest.mark.parametrize("case_id,device", [("ar_P2_t1_l0_f32_op0_n1048576_lin", False),
+                                            pytest.param("ar_P2_t1_l0_f32_op0_n1048576_lin", True, marks=pytest.mark.wide),
+                                            pytest.param("ar_P8_t8_l0_f32_op0_n65536_lin", False, marks=pytest.mark.wide),
+                                            ("ar_P8_t8_l0_f32_op0_n65536_lin", True)],
+                         ids=["C1-host", "C1-device", "P8-host", "P8-device"])
 def test_harness_reproduces_reference_benchmark_output(tmp_path, case_id, device):
     """The reference's own benchmark.cpp workload (data[i] = i*0.1f in place, one call; C1 = 2 ranks, ring,
     2^20 fp32) through MPI_Allreduce_FT (host buffers) or MPI_Allreduce_FT_device in ftar_benchmark, one MPI
@@ -202,8 +206,10 @@ def test_harness_host_buffer_registration(tmp_path, ranks):
 @needs
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks,topo,n,device", [(2, "1", 1, False), (3, "3", 1003, False), (4, "2,2", 65541, True),
-                                                 (4, "4", 17, False), (2, "2", (1 << 20) + 3, True),
-                                                 (3, "1", 300_007, False), (2, "1", 0, False), (3, "3", 0, True)])
+                                                 pytest.param(4, "4", 17, False, marks=pytest.mark.wide),
+                                                 pytest.param(2, "2", (1 << 20) + 3, True, marks=pytest.mark.wide),
+                                                 pytest.param(3, "1", 300_007, False, marks=pytest.mark.wide),
+                                                 (2, "1", 0, False), pytest.param(3, "3", 0, True, marks=pytest.mark.wide)])
 def test_harness_matches_oracle_on_odd_shapes(tmp_path, ranks, topo, n, device):
     """MPI_Allreduce_FT (host buffers) / MPI_Allreduce_FT_device across real MPI processes on ragged sizes and
     3-rank layouts the reference fixtures do not hold: every rank's dumped buffer equals the pinned oracle's
@@ -223,7 +229,8 @@ def test_harness_matches_oracle_on_odd_shapes(tmp_path, ranks, topo, n, device):
 @needs
 @pytest.mark.gpu
 @pytest.mark.parametrize("ranks,topo,n,device", [(2, "1", 1 << 26, False), (2, "2", 1 << 26, True),
-                                                 (8, "8", 1 << 24, False), (4, "2,2", 1 << 24, False)])
+                                                 (8, "8", 1 << 24, False),
+                                                 pytest.param(4, "2,2", 1 << 24, False, marks=pytest.mark.wide)])
 def test_harness_baseline_sizes_match_oracle(tmp_path, ranks, topo, n, device):
     """MPI_Allreduce_FT across real MPI processes at BASELINE sizes: C3's 256 MiB fp32 bucket with 2 ranks (the
     ring and tree(2); host buffers and device-resident), and 8 ranks (C4/C5's width-8 tree) and a 2,2 tree on
@@ -284,8 +291,11 @@ def _loopback_mpmd(ranks, args):
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
-@pytest.mark.parametrize("case_id", ["ar_P2_t1_l0_f32_op0_n1048576_lin", "ar_P8_t8_l0_f32_op0_n65536_lin"])
+@pytest.mark.parametrize("case_id,device", [("ar_P2_t1_l0_f32_op0_n1048576_lin", False),
+                                            pytest.param("ar_P2_t1_l0_f32_op0_n1048576_lin", True, marks=pytest.mark.wide),
+                                            pytest.param("ar_P8_t8_l0_f32_op0_n65536_lin", False, marks=pytest.mark.wide),
+                                            ("ar_P8_t8_l0_f32_op0_n65536_lin", True)],
+                         ids=["C1-host", "C1-device", "P8-host", "P8-device"])
 def test_harness_rccl_transport_reproduces_reference_output(tmp_path, case_id, device):
     """benchmark.cpp's workload (C1 and the 8-rank width-8 tree) through MPI_Allreduce_FT with
     FTAR_MPI_TRANSPORT=rccl: the communicator is RCCL's and every block moves by ncclSend/ncclRecv between
@@ -331,10 +341,10 @@ def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
 @pytest.mark.parametrize("ranks,topo,n,serial", [(2, "1", (1 << 20) + 3, "0"),
                                                  pytest.param(2, "2", 65537, "0", marks=pytest.mark.wide),
                                                  pytest.param(4, "1", 100_003, "0", marks=pytest.mark.wide),
-                                                 (4, "4", 100_003, "0"),
+                                                 pytest.param(4, "4", 100_003, "0", marks=pytest.mark.wide),
                                                  pytest.param(4, "2,2", 4099, "0", marks=pytest.mark.wide),
                                                  pytest.param(2, "1", (1 << 20) + 3, "1", marks=pytest.mark.wide),
-                                                 (4, "2,2", 4099, "1")])
+                                                 pytest.param(4, "2,2", 4099, "1", marks=pytest.mark.wide)])
 def test_harness_rccl_allreduce_captured_in_a_hip_graph(tmp_path, ranks, topo, n, serial):
     """The product's process model under stream capture at P > 1: one MPI process per rank over an RCCL
     communicator (FTAR_MPI_TRANSPORT=rccl, loopback sockets), MPI_Allreduce_FT_device captured once into a
