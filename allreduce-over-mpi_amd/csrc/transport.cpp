@@ -518,7 +518,6 @@ struct LocalHub {
     hipEvent_t ready = nullptr;  // sender-side data ready
     hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
     bool taken = false;
-    int device = -1;  // the sender's device (a same-device receive copies with ftar's own copy kernels)
     ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
       if (ready) hub->give_event(ready);
       if (done) hub->give_event(done);
@@ -708,7 +707,6 @@ class LocalTransport final : public Transport {
       p->buf = o.buf;
       p->bytes = o.bytes;
       p->ready = nullptr;
-      FTAR_CHECK_HIP(hipGetDevice(&p->device));
       FTAR_RETURN_IF(hub_->take_event(&p->ready));
       FTAR_CHECK_HIP(hipEventRecord(p->ready, o.s));
       mine.push_back(p);
@@ -716,14 +714,7 @@ class LocalTransport final : public Transport {
       hub_->wire[{rank_, o.peer}].push_back(p);
     }
     hub_->cv.notify_all();
-    // 2. complete every receive in posting order (per-pair FIFO, like MPI/RCCL).  Every peer published
-    // its sends in its step 1, before any of its receives, so matching them all first cannot wait on a
-    // receive.  A receive from a rank on this device is a copy kernel of ftar's own: the group's receives
-    // on one stream are ONE launch of the multi-segment copy (every peer's block at once; a single one takes
-    // the LDS-staged copy), where the runtime's blit would run them one after another.  A receive from
-    // another device keeps the runtime's copy (peer access may be off).  FTAR_LOCAL_COPY=runtime: the
-    // runtime's copy for every receive (the A/B).
-    std::vector<std::pair<const Op*, std::shared_ptr<LocalHub::Posted>>> got;
+    // 2. complete every receive in posting order (per-pair FIFO, like MPI/RCCL)
     for (auto& o : ops) {
       if (o.is_send) continue;
       std::shared_ptr<LocalHub::Posted> p;
@@ -742,44 +733,18 @@ class LocalTransport final : public Transport {
         return FTAR_ERR_INTERNAL;
       }
       FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
-      got.emplace_back(&o, p);
-    }
-    static const bool runtime_copy = [] {
-      const char* e = getenv("FTAR_LOCAL_COPY");
-      return e && !strcmp(e, "runtime");
-    }();
-    int dev = -1;
-    FTAR_CHECK_HIP(hipGetDevice(&dev));
-    for (size_t i = 0; i < got.size();) {  // runs of receives on one stream
-      const hipStream_t s = got[i].first->s;
-      std::vector<Segment> segs;
-      size_t j = i;
-      for (; j < got.size() && got[j].first->s == s; ++j) {
-        const Op& o = *got[j].first;
-        if (!o.bytes) continue;
-        if (!runtime_copy && got[j].second->device == dev)
-          segs.push_back({got[j].second->buf, o.buf, o.bytes});
-        else
-          FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, got[j].second->buf, o.bytes, hipMemcpyDeviceToDevice, s));
+      if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
+      hipEvent_t done = nullptr;
+      FTAR_RETURN_IF(hub_->take_event(&done));
+      if (hipEventRecord(done, o.s) != hipSuccess) {
+        hub_->give_event(done);
+        set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
+        return FTAR_ERR_HIP;
       }
-      for (size_t a = 0; a < segs.size(); a += FTAR_MAX_K) {
-        const int m = (int)std::min<size_t>(FTAR_MAX_K, segs.size() - a);
-        FTAR_RETURN_IF(m == 1 ? launch_copy(segs[a].src, segs[a].dst, segs[a].bytes, s)
-                              : launch_gather(segs.data() + a, m, s));
-      }
-      for (; i < j; ++i) {
-        hipEvent_t done = nullptr;
-        FTAR_RETURN_IF(hub_->take_event(&done));
-        if (hipEventRecord(done, s) != hipSuccess) {
-          hub_->give_event(done);
-          set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
-          return FTAR_ERR_HIP;
-        }
-        {
-          std::lock_guard<std::mutex> g(hub_->mu);
-          got[i].second->done = done;
-          got[i].second->taken = true;
-        }
+      {
+        std::lock_guard<std::mutex> g(hub_->mu);
+        p->done = done;
+        p->taken = true;
       }
       hub_->cv.notify_all();
     }

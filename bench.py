@@ -329,7 +329,7 @@ def plan_hbm_bytes(ftar, topo, world, count, esz, allgather="direct", reduce_sca
     return total
 
 
-def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8"):
+def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=None):
     """The engine itself on this one GPU, against HBM: P = 8 in-process ranks (the
     local transport, one host thread per rank, its transfers device copies on the comm streams) run the C4
     bucket -- 2^28 fp32 per rank, tree(8) in the direct form, the execution model's piece -- through the
@@ -343,11 +343,11 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8"):
     import ftar
     dev = torch.device("cuda:0")
     esz = 4
-    ch = ftar.exec_choose(world, n * esz, topo_=topo, form="direct")
+    ch = ftar.exec_choose(world, n * esz, topo_=topo, form="direct", chunk_bytes=chunk_bytes)
     g = ftar.Comm.init_local(world)
     try:
         g.set_form("direct")
-        g.set_chunk_bytes(ch.chunk_bytes)
+        g.set_chunk_bytes(ch.chunk_bytes or (n // world) * esz)   # 0 (whole blocks): one piece per block
         gen = torch.Generator(device=dev)
         gen.manual_seed(0xC4)
         xs = [torch.rand(n, device=dev, generator=gen) * 2 - 1 for _ in range(world)]
@@ -384,7 +384,7 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8"):
         hbm = plan_hbm_bytes(ftar, topo, world, n, esz)
         gbps = hbm / (ms * 1e-3) / 1e9
         return {"workload": f"P = {world} in-process ranks on one MI355X, tree({topo}) direct, C4 bucket "
-                            f"(2^28 fp32 per rank), the model's piece",
+                            f"(2^28 fp32 per rank), " + ("the model's piece" if chunk_bytes is None else "piece fixed"),
                 "ranks": world, "elements_per_rank": n, "topology": topo, "form": "direct",
                 "chunk_bytes": ch.chunk_bytes, "model": ch.as_dict(), "ms_median": round(ms, 4),
                 "ms_all": [round(x, 4) for x in per], "wall_s": round(wall, 3),
@@ -1737,7 +1737,8 @@ def bench_distributed(a):
 def main():
     a = parse()
     if a.engine_local_only:   # one line item alone (under rocprofv3: the engine's kernel timeline)
-        print(json.dumps({"engine_local": engine_local(steps=a.steps, warmup=a.warmup)}), flush=True)
+        print(json.dumps({"engine_local": engine_local(steps=a.steps, warmup=a.warmup,
+                                                       chunk_bytes=a.chunk_bytes or None)}), flush=True)
     elif int(os.environ.get("WORLD_SIZE", "1")) > 1 or a.force_dist:
         bench_distributed(a)
     else:

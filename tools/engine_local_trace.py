@@ -6,8 +6,10 @@
     python3 tools/engine_local_trace.py OUT/.../el_kernel_trace.csv [OUT/.../el_memory_copy_trace.csv] \\
         --calls 7 --keep 5 --hbm-bytes <engine_local.hbm_bytes_per_call>
 
-Splits the timeline into the calls (the host synchronises between them, so the calls-1 widest gaps
-separate them), keeps the last `keep`, and reports per call:
+Keeps the engine's own kernels (ftar's copies and folds; the torch kernels that set up the inputs and check
+the sample are left out), splits them into the calls (every call launches the same kernels, and the host
+synchronises between calls, so in start order each consecutive run of len/calls kernels is one call), keeps
+the last `keep`, and reports per call:
   * span, device-busy time (union of every kernel and copy), idle = span - busy;
   * the folds (reduce kernels) and the transfers (device copies: blit kernels or SDMA copies): their busy
     time, and how much of the fold time runs while a transfer is in flight;
@@ -70,16 +72,16 @@ def main():
     ap.add_argument("--keep", type=int, default=5)
     ap.add_argument("--hbm-bytes", type=float, default=0.0)
     a = ap.parse_args()
-    ops = load(a.kernel_csv, "kernel")
+    # the engine's own work only: ftar's kernels (folds, copies) and the runtime's copies (the input setup
+    # and the sample check around the timed calls are torch kernels)
+    ops = [o for o in load(a.kernel_csv, "kernel") if "ftar::" in o["name"]]
     if a.copy_csv:
         ops += load(a.copy_csv, "copy")
     ops.sort(key=lambda o: o["s"])
-    # the calls: split at the calls-1 widest idle gaps of the whole timeline
-    u = union([(o["s"], o["e"]) for o in ops])
-    gaps = sorted(range(1, len(u)), key=lambda i: u[i][0] - u[i - 1][1], reverse=True)[:a.calls - 1]
-    cuts = sorted(u[i][0] for i in gaps)
-    bounds = [u[0][0]] + cuts + [u[-1][1] + 1]
-    calls = [[o for o in ops if lo <= o["s"] < hi] for lo, hi in zip(bounds, bounds[1:])]
+    if len(ops) % a.calls:
+        raise SystemExit(f"{len(ops)} engine ops do not split into {a.calls} equal calls")
+    per = len(ops) // a.calls
+    calls = [ops[i * per:(i + 1) * per] for i in range(a.calls)]
     res = []
     for c in calls[-a.keep:]:
         span = (min(o["s"] for o in c), max(o["e"] for o in c))
