@@ -358,12 +358,15 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
         def call():
             g.allreduce(xs, ys, n, "f32", "sum", topo_=topo, streams=streams)
         for _ in range(warmup):
+            torch.cuda._sleep(64)   # a marker kernel between calls for the trace (tools/engine_local_trace.py)
             call()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         per = []
         t0 = time.perf_counter()
         for _ in range(steps):
+            torch.cuda._sleep(64)
+            torch.cuda.synchronize()
             e0.record(stream)
             call()
             e1.record(stream)
@@ -1031,7 +1034,9 @@ def bench_distributed(a):
                 lib = ftar.bench_lib()
                 lib.ftar_debug_block_stream.restype = ctypes.c_void_p
                 lib.ftar_debug_block_stream.argtypes = [ctypes.c_void_p, ctypes.c_double]
-                state["blocked_flag"] = lib.ftar_debug_block_stream(stream.cuda_stream, 3 * timeout_s + 60)
+                # the wave spins until released at the end of the run, or this limit: past the fallback's
+                # default measurement, which must still find the stream blocked
+                state["blocked_flag"] = lib.ftar_debug_block_stream(stream.cuda_stream, 3 * timeout_s + 10)
             ev = torch.cuda.Event()
             ev.record(stream)
             state["preflight_ev"] = ev

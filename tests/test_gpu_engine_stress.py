@@ -30,7 +30,7 @@ def test_in_process_groups(calls):
     assert stats["checked"] == stats["calls"] >= calls and stats["groups"] >= 3 and stats["captured"] > 0, stats
 
 
-@pytest.mark.parametrize("mode,P,calls,seed", [pytest.param("rccl", 4, 40, 41, marks=pytest.mark.wide), ("rccl", 8, 16, 12),
+@pytest.mark.parametrize("mode,P,calls,seed", [pytest.param("rccl", 4, 40, 41, marks=pytest.mark.wide), ("rccl", 8, 10, 12),
                                                ("host", 4, 30, 43), pytest.param("host", 4, 60, 43, marks=pytest.mark.wide)])
 def test_processes(mode, P, calls, seed):
     p = _run([mode, P, calls, seed, 2], 240)

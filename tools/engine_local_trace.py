@@ -6,10 +6,10 @@
     python3 tools/engine_local_trace.py OUT/.../el_kernel_trace.csv [OUT/.../el_memory_copy_trace.csv] \\
         --calls 7 --keep 5 --hbm-bytes <engine_local.hbm_bytes_per_call>
 
-Keeps the engine's own kernels (ftar's copies and folds; the torch kernels that set up the inputs and check
-the sample are left out), splits them into the calls (every call launches the same kernels, and the host
-synchronises between calls, so in start order each consecutive run of len/calls kernels is one call), keeps
-the last `keep`, and reports per call:
+Keeps the engine's own work (ftar's copies and folds, and the runtime's copy kernels and SDMA copies the
+in-process transport issues), splits it into the calls at the marker kernels bench.py launches before each
+call (torch.cuda._sleep, a "spin" kernel; without markers: consecutive runs of len/calls ops in start
+order), keeps the last `keep`, and reports per call:
   * span, device-busy time (union of every kernel and copy), idle = span - busy;
   * the folds (reduce kernels) and the transfers (device copies: blit kernels or SDMA copies): their busy
     time, and how much of the fold time runs while a transfer is in flight;
@@ -74,14 +74,26 @@ def main():
     a = ap.parse_args()
     # the engine's own work only: ftar's kernels (folds, copies) and the runtime's copies (the input setup
     # and the sample check around the timed calls are torch kernels)
-    ops = [o for o in load(a.kernel_csv, "kernel") if "ftar::" in o["name"]]
+    kern = load(a.kernel_csv, "kernel")
+    marks = sorted(o["s"] for o in kern if "sleep" in o["name"].lower() or "spin" in o["name"].lower())
+    ops = [o for o in kern if "ftar::" in o["name"] or "copyBuffer" in o["name"]]
     if a.copy_csv:
         ops += load(a.copy_csv, "copy")
     ops.sort(key=lambda o: o["s"])
-    if len(ops) % a.calls:
-        raise SystemExit(f"{len(ops)} engine ops do not split into {a.calls} equal calls")
-    per = len(ops) // a.calls
-    calls = [ops[i * per:(i + 1) * per] for i in range(a.calls)]
+    if len(marks) >= a.calls:   # the calls lie between consecutive markers (the last one: up to the next torch op)
+        bounds = marks[-a.calls:] + [max(o["e"] for o in ops) + 1]
+        calls = [[o for o in ops if lo <= o["s"] < hi] for lo, hi in zip(bounds, bounds[1:])]
+        # the last call ends where its ops stop: drop anything after a gap wider than the call itself
+        last = calls[-1]
+        for i in range(1, len(last)):
+            if last[i]["s"] - max(x["e"] for x in last[:i]) > 1e6:   # 1 ms of silence: the sample check
+                calls[-1] = last[:i]
+                break
+    else:
+        if len(ops) % a.calls:
+            raise SystemExit(f"{len(ops)} engine ops do not split into {a.calls} equal calls")
+        per = len(ops) // a.calls
+        calls = [ops[i * per:(i + 1) * per] for i in range(a.calls)]
     res = []
     for c in calls[-a.keep:]:
         span = (min(o["s"] for o in c), max(o["e"] for o in c))
@@ -115,7 +127,7 @@ def main():
     names = {}
     for o in ops:
         names.setdefault(o["name"][:90], []).append(o["e"] - o["s"])
-    summary = {"calls_found": len(calls), "kept": len(res),
+    summary = {"calls_found": len(calls), "kept": len(res), "markers": len(marks),
                "median_span_us": statistics.median(r["span_us"] for r in res),
                "median_idle_us": statistics.median(r["idle_us"] for r in res),
                "median_fold_overlap": statistics.median(r["fold_overlapped_by_transfers"] or 0 for r in res),
