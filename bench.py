@@ -386,6 +386,23 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
         ok = all(bool(torch.equal(y[idx].view(torch.int32), want.view(torch.int32))) for y in ys)
         hbm = plan_hbm_bytes(ftar, topo, world, n, esz)
         gbps = hbm / (ms * 1e-3) / 1e9
+        whole = None
+        if chunk_bytes is None:   # the same calls with whole blocks (one piece per block): nothing to overlap
+            g.set_chunk_bytes(split * esz)   # on one GPU, where every copy and fold shares the one HBM
+            call()
+            wper = []
+            for _ in range(steps):
+                torch.cuda.synchronize()
+                e0.record(stream)
+                call()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                wper.append(e0.elapsed_time(e1))
+            wms = sorted(wper)[len(wper) // 2]
+            whole = {"chunk_bytes": split * esz, "ms_median": round(wms, 4),
+                     "hbm_frac": round(hbm / (wms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "model_ms": round(ftar.exec_choose(world, n * esz, topo_=topo, form="direct",
+                                                        chunk_bytes=split * esz).seconds * 1e3, 4)}
         return {"workload": f"P = {world} in-process ranks on one MI355X, tree({topo}) direct, C4 bucket "
                             f"(2^28 fp32 per rank), " + ("the model's piece" if chunk_bytes is None else "piece fixed"),
                 "ranks": world, "elements_per_rank": n, "topology": topo, "form": "direct",
@@ -393,9 +410,11 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
                 "ms_all": [round(x, 4) for x in per], "wall_s": round(wall, 3),
                 "hbm_bytes_per_call": hbm, "hbm_GBps": round(gbps, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
                 "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4), "check": "bit-exact (4096-element sample, every rank)"
-                if ok else "MISMATCH",
+                if ok else "MISMATCH", "whole_blocks": whole,
                 "note": "HBM bytes from the plans: every received block one device copy (read + write), every "
-                        "fold k sources + 1 destination; all 8 ranks' copies and folds share this GPU's HBM"}
+                        "fold k sources + 1 destination; all 8 ranks' copies and folds share this GPU's HBM. "
+                        "ms = events around the group call, which returns once every rank's stream drained "
+                        "(its host threads' start and join included)"}
     finally:
         g.destroy()
 

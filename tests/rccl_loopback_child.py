@@ -267,9 +267,9 @@ def full_size(comm, res, world, rank):
     res["full"] = []
     odd = 24 * (1 << 20) + 4096
     cases = [((1 << 28), "f32", "1", "direct", 0), ((1 << 28), "f32", "1", "stages", 0),
-             ((1 << 28), "f32", "1", "direct", odd), ((1 << 29), "bf16", str(world), "direct", 0)]
-    if os.environ.get("FTAR_RUN_WIDE") == "1":   # the second odd-piece variant
-        cases.insert(3, ((1 << 28), "f32", "1", "stages", odd))
+             ((1 << 29), "bf16", str(world), "direct", 0)]
+    if os.environ.get("FTAR_RUN_WIDE") == "1":   # pieces that divide no block (in-process at full size by default)
+        cases[2:2] = [((1 << 28), "f32", "1", "direct", odd), ((1 << 28), "f32", "1", "stages", odd)]
     for n, dt, topo, form, chunk in cases:
         tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
         comm.allgather = form

@@ -60,8 +60,8 @@ def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
     and the fallback runs on a fresh stream -- still blocked when the fallback's default was measured."""
     # the fallback's sweep is not what is tested here: a short budget (the spinning wave of the hang case
     # slows every later kernel until the run ends)
-    d = _bench(1, ["--force-dist", "--no-cpu-baseline", "--no-c5"],
-               dict(env_extra, FTAR_BENCH_PREFLIGHT_S="5", FTAR_BENCH_SWEEP_S="5"))
+    d = _bench(1, ["--force-dist", "--no-cpu-baseline", "--no-c5", "--no-host"],
+               dict(env_extra, FTAR_BENCH_PREFLIGHT_S="3", FTAR_BENCH_SWEEP_S="5"))
     assert d["check"] == "ok" and d["config"]["form"].startswith("peer-"), d["config"]
     assert why in d["rccl_init_error"], d["rccl_init_error"]
     assert len(d["rccl_error_by_rank"]) == 1 and why in d["rccl_error_by_rank"][0]["error"]

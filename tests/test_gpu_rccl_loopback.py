@@ -129,4 +129,4 @@ def test_rccl_p2p_baseline_c4_c5_full_size():
     p, res = run_loopback(8, {"FTAR_LOOPBACK_MODE": "full"})
     assert p.returncode == 0 and len(res) == 8, (p.returncode, p.stdout[-3000:], p.stderr[-4000:])
     for r in res:
-        assert not r["fail"] and len(r["full"]) == (5 if os.environ.get("FTAR_RUN_WIDE") == "1" else 4), r
+        assert not r["fail"] and len(r["full"]) == (5 if os.environ.get("FTAR_RUN_WIDE") == "1" else 3), r

@@ -173,7 +173,7 @@ def test_harness_communicator_lifecycle_single_rank(tmp_path):
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra", [[], ["--no-register"]], ids=["registered", "pageable"])
+@pytest.mark.parametrize("extra", [[], pytest.param(["--no-register"], marks=pytest.mark.wide)], ids=["registered", "pageable"])
 def test_harness_communicator_lifecycle_two_ranks(tmp_path, extra):
     """Two ranks: duplicates of MPI_COMM_WORLD (a 2-rank AllReduce) alternate with singleton splits (the
     reference's P <= 1 copy, mpi_mod.hpp:1739) under handles MPICH recycles; with a raw-handle cache the
@@ -317,7 +317,8 @@ def test_harness_rccl_transport_reproduces_reference_output(tmp_path, case_id, d
 
 @needs
 @pytest.mark.gpu
-@pytest.mark.parametrize("ranks,topo,n", [(2, "1", 1 << 24), (4, "2,2", (1 << 22) + 5), (3, "3", 300_007)])
+@pytest.mark.parametrize("ranks,topo,n", [(2, "1", 1 << 24), pytest.param(4, "2,2", (1 << 22) + 5, marks=pytest.mark.wide),
+                                          (3, "3", 300_007)])
 def test_harness_rccl_transport_matches_oracle(tmp_path, ranks, topo, n):
     """The same RCCL transport between MPI processes on larger and ragged buckets (host buffers, the
     piece-pipelined host path over RCCL), each rank's whole buffer against the pinned oracle."""

@@ -76,6 +76,7 @@ def main():
     # and the sample check around the timed calls are torch kernels)
     kern = load(a.kernel_csv, "kernel")
     marks = sorted(o["s"] for o in kern if "sleep" in o["name"].lower() or "spin" in o["name"].lower())
+    mark_end = {o["s"]: o["e"] for o in kern if "sleep" in o["name"].lower() or "spin" in o["name"].lower()}
     ops = [o for o in kern if "ftar::" in o["name"] or "copyBuffer" in o["name"]]
     if a.copy_csv:
         ops += load(a.copy_csv, "copy")
@@ -95,7 +96,8 @@ def main():
         per = len(ops) // a.calls
         calls = [ops[i * per:(i + 1) * per] for i in range(a.calls)]
     res = []
-    for c in calls[-a.keep:]:
+    starts = bounds[:-1] if len(marks) >= a.calls else [None] * len(calls)
+    for c, mk in list(zip(calls, starts))[-a.keep:]:
         span = (min(o["s"] for o in c), max(o["e"] for o in c))
         busy = union([(o["s"], o["e"]) for o in c])
         folds = union([(o["s"], o["e"]) for o in c if is_fold(o["name"])])
@@ -120,6 +122,8 @@ def main():
              "ops": len(c), "fold_ops": sum(is_fold(o["name"]) for o in c),
              "kernel_time_sum_over_span": round(sum(o["e"] - o["s"] for o in c) / (span[1] - span[0]), 2),
              "streams": per_stream}
+        if mk is not None:   # from the marker kernel's end (the call's start on the host) to its first kernel
+            d["lead_us"] = round((span[0] - mark_end[mk]) / 1e3, 1)
         if a.hbm_bytes:
             d["hbm_GBps_over_span"] = round(a.hbm_bytes / (span[1] - span[0]), 1)
             d["hbm_GBps_over_busy"] = round(a.hbm_bytes / length(busy), 1)
@@ -131,6 +135,7 @@ def main():
                "median_span_us": statistics.median(r["span_us"] for r in res),
                "median_idle_us": statistics.median(r["idle_us"] for r in res),
                "median_fold_overlap": statistics.median(r["fold_overlapped_by_transfers"] or 0 for r in res),
+               "median_lead_us": statistics.median(r["lead_us"] for r in res) if "lead_us" in res[0] else None,
                "op_kinds": {k: {"count": len(v), "mean_us": round(statistics.mean(v) / 1e3, 1)}
                             for k, v in sorted(names.items(), key=lambda kv: -sum(kv[1]))[:8]},
                "calls": res}
