@@ -24,8 +24,10 @@
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <tuple>
 
 #include "ftar_internal.h"
@@ -34,7 +36,8 @@ namespace ftar {
 
 namespace {
 std::mutex g_cost_mu;
-ftar_cost_params_t g_set{};  // fields <= 0: default
+ftar_cost_params_t g_set{};   // fields <= 0: default
+ftar_cost_params_t g_file{};  // constants loaded from a calibration file (ftar_cost_load / FTAR_COST_FILE)
 std::atomic<uint64_t> g_generation{0};  // bumped by every set: communicators re-decide their cached choices
 
 // MI355X defaults, used where no run on the node has fitted them (bench.py at N > 1 does):
@@ -55,27 +58,109 @@ double env_or(const char* name, double v) {
   const char* e = getenv(name);
   return e && *e ? atof(e) : v;
 }
+
+// The fields of ftar_cost_params_t by name, in struct order (the calibration file's keys)
+constexpr const char* kFieldNames[9] = {"alpha_us",       "link_gbps",       "hbm_gbps",  "issue_us", "barrier_us",
+                                        "peer_read_gbps", "peer_write_gbps", "copy_gbps", "coll_gbps"};
+double* field(ftar_cost_params_t* p, int i) { return &p->alpha_us + i; }
+static_assert(sizeof(ftar_cost_params_t) == 9 * sizeof(double), "ftar_cost_params_t is nine doubles");
+
+// A calibration file: one "name value" (or "name = value") per line, '#' starts a comment; the names are
+// ftar_cost_params_t's fields, every value a number > 0; fields left out keep their defaults.
+ftar_status_t parse_cost_file(const char* path, ftar_cost_params_t* out) {
+  FILE* f = fopen(path, "r");
+  if (!f) {
+    set_error(std::string("cost file ") + path + ": cannot open", __FILE__, __LINE__);
+    return FTAR_ERR_INVALID_ARG;
+  }
+  ftar_cost_params_t p{};
+  char line[512];
+  int lineno = 0;
+  ftar_status_t st = FTAR_SUCCESS;
+  while (st == FTAR_SUCCESS && fgets(line, sizeof line, f)) {
+    ++lineno;
+    if (char* h = strchr(line, '#')) *h = 0;
+    for (char* q = line; *q; ++q)
+      if (*q == '=') *q = ' ';
+    char name[128];
+    double v = 0;
+    char extra[8];
+    const int got = sscanf(line, "%127s %lf %7s", name, &v, extra);
+    if (got <= 0) continue;  // blank or comment
+    int i = 0;
+    while (i < 9 && strcmp(name, kFieldNames[i])) ++i;
+    if (got != 2 || i == 9 || !(v > 0) || !std::isfinite(v)) {
+      set_error(std::string("cost file ") + path + " line " + std::to_string(lineno) +
+                    ": expected '<field> <value > 0>' with a field of ftar_cost_params_t",
+                __FILE__, __LINE__);
+      st = FTAR_ERR_INVALID_ARG;
+    } else {
+      *field(&p, i) = v;
+    }
+  }
+  fclose(f);
+  if (st == FTAR_SUCCESS) *out = p;
+  return st;
+}
+
+// FTAR_COST_FILE: loaded at the first use of the model constants after it changes (a bad file leaves the
+// constants as they were and fails the next communicator bring-up, cost_file_status)
+std::string g_file_path;
+ftar_status_t g_file_status = FTAR_SUCCESS;
+std::string g_file_error;
+void sync_cost_file() {  // under g_cost_mu
+  const char* e = getenv("FTAR_COST_FILE");
+  const std::string path = e ? e : "";
+  if (path == g_file_path) return;
+  g_file_path = path;
+  g_file_status = FTAR_SUCCESS;
+  g_file = ftar_cost_params_t{};
+  if (!path.empty()) {
+    ftar_cost_params_t p;
+    g_file_status = parse_cost_file(path.c_str(), &p);
+    if (g_file_status == FTAR_SUCCESS) g_file = p;
+    else g_file_error = last_error();
+  }
+  ++g_generation;
+}
 }  // namespace
 
-uint64_t cost_generation() { return g_generation.load(); }
+uint64_t cost_generation() {
+  std::lock_guard<std::mutex> g(g_cost_mu);
+  sync_cost_file();
+  return g_generation.load();
+}
 
+ftar_status_t cost_file_status() {
+  std::lock_guard<std::mutex> g(g_cost_mu);
+  sync_cost_file();
+  if (g_file_status != FTAR_SUCCESS) set_error("FTAR_COST_FILE: " + g_file_error, __FILE__, __LINE__);
+  return g_file_status;
+}
+
+// precedence: FTAR_COST_<FIELD> > ftar_cost_set > the calibration file > the defaults
 CostParams cost_params() {
-  ftar_cost_params_t p;
+  ftar_cost_params_t p, fp;
   {
     std::lock_guard<std::mutex> g(g_cost_mu);
+    sync_cost_file();
     p = g_set;
+    fp = g_file;
   }
-  auto pick = [](double set, double def) { return set > 0 ? set : def; };
+  auto pick = [](double set, double file, double def) { return set > 0 ? set : file > 0 ? file : def; };
   CostParams k;
-  k.alpha = env_or("FTAR_COST_ALPHA_US", pick(p.alpha_us, kDefaults.alpha_us)) * 1e-6;
-  k.link = env_or("FTAR_COST_LINK_GBPS", pick(p.link_gbps, kDefaults.link_gbps)) * 1e9;
-  k.hbm = env_or("FTAR_COST_HBM_GBPS", pick(p.hbm_gbps, kDefaults.hbm_gbps)) * 1e9;
-  k.issue = env_or("FTAR_COST_ISSUE_US", pick(p.issue_us, kDefaults.issue_us)) * 1e-6;
-  k.barrier = env_or("FTAR_COST_BARRIER_US", pick(p.barrier_us, kDefaults.barrier_us)) * 1e-6;
-  k.peer_read = env_or("FTAR_COST_PEER_READ_GBPS", pick(p.peer_read_gbps, kDefaults.peer_read_gbps)) * 1e9;
-  k.peer_write = env_or("FTAR_COST_PEER_WRITE_GBPS", pick(p.peer_write_gbps, kDefaults.peer_write_gbps)) * 1e9;
-  k.copy = env_or("FTAR_COST_COPY_GBPS", pick(p.copy_gbps, kDefaults.copy_gbps)) * 1e9;
-  k.coll = env_or("FTAR_COST_COLL_GBPS", pick(p.coll_gbps, kDefaults.coll_gbps)) * 1e9;
+  k.alpha = env_or("FTAR_COST_ALPHA_US", pick(p.alpha_us, fp.alpha_us, kDefaults.alpha_us)) * 1e-6;
+  k.link = env_or("FTAR_COST_LINK_GBPS", pick(p.link_gbps, fp.link_gbps, kDefaults.link_gbps)) * 1e9;
+  k.hbm = env_or("FTAR_COST_HBM_GBPS", pick(p.hbm_gbps, fp.hbm_gbps, kDefaults.hbm_gbps)) * 1e9;
+  k.issue = env_or("FTAR_COST_ISSUE_US", pick(p.issue_us, fp.issue_us, kDefaults.issue_us)) * 1e-6;
+  k.barrier = env_or("FTAR_COST_BARRIER_US", pick(p.barrier_us, fp.barrier_us, kDefaults.barrier_us)) * 1e-6;
+  k.peer_read =
+      env_or("FTAR_COST_PEER_READ_GBPS", pick(p.peer_read_gbps, fp.peer_read_gbps, kDefaults.peer_read_gbps)) * 1e9;
+  k.peer_write =
+      env_or("FTAR_COST_PEER_WRITE_GBPS", pick(p.peer_write_gbps, fp.peer_write_gbps, kDefaults.peer_write_gbps)) *
+      1e9;
+  k.copy = env_or("FTAR_COST_COPY_GBPS", pick(p.copy_gbps, fp.copy_gbps, kDefaults.copy_gbps)) * 1e9;
+  k.coll = env_or("FTAR_COST_COLL_GBPS", pick(p.coll_gbps, fp.coll_gbps, kDefaults.coll_gbps)) * 1e9;
   return k;
 }
 
@@ -333,6 +418,34 @@ ftar_status_t ftar_cost_set(const ftar_cost_params_t* p) {
   ftar::g_set = *p;
   ++ftar::g_generation;
   return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_cost_load(const char* path) {
+  if (!path) return FTAR_ERR_INVALID_ARG;
+  ftar_cost_params_t p;
+  FTAR_RETURN_IF(ftar::parse_cost_file(path, &p));
+  std::lock_guard<std::mutex> g(ftar::g_cost_mu);
+  ftar::sync_cost_file();  // an FTAR_COST_FILE set later still replaces this (it is read when it changes)
+  ftar::g_file = p;
+  ++ftar::g_generation;
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t ftar_cost_save(const char* path) {
+  if (!path) return FTAR_ERR_INVALID_ARG;
+  ftar_cost_params_t p;
+  FTAR_RETURN_IF(ftar_cost_get(&p));
+  FILE* f = fopen(path, "w");
+  if (!f) {
+    ftar::set_error(std::string("ftar_cost_save: cannot write ") + path, __FILE__, __LINE__);
+    return FTAR_ERR_INVALID_ARG;
+  }
+  fprintf(f, "# ftar execution-model constants (ftar_cost_save; load with FTAR_COST_FILE or ftar_cost_load)\n");
+  for (int i = 0; i < 9; ++i)
+    if (*ftar::field(&p, i) > 0) fprintf(f, "%s %.15g\n", ftar::kFieldNames[i], *ftar::field(&p, i));
+  const bool ok = fclose(f) == 0;
+  if (!ok) ftar::set_error(std::string("ftar_cost_save: write failed: ") + path, __FILE__, __LINE__);
+  return ok ? FTAR_SUCCESS : FTAR_ERR_INVALID_ARG;
 }
 
 ftar_status_t ftar_cost_get(ftar_cost_params_t* p) {

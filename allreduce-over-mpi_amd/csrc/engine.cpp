@@ -163,6 +163,7 @@ ftar_status_t agree_settings(ftar_comm* c, bool failed = false);
 namespace {
 // the local part of a communicator's bring-up: streams, events, settings from the environment
 ftar_status_t comm_setup_local(ftar_comm* c) {
+  FTAR_RETURN_IF(cost_file_status());  // a calibration file that does not parse fails loudly, on every rank
   FTAR_CHECK_HIP(hipSetDevice(c->device));
   FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->comm_s, hipStreamNonBlocking));
   if (const char* rc = getenv("FTAR_REDUCE_CUS")) FTAR_RETURN_IF(set_reduce_cus(c, atoi(rc)));

@@ -75,7 +75,9 @@ struct CostParams {  // seconds and bytes per second
   double alpha, link, hbm, issue, barrier, peer_read, peer_write, copy, coll;
 };
 CostParams cost_params();  // defaults <- ftar_cost_set <- FTAR_COST_* environment
-uint64_t cost_generation();  // changes whenever ftar_cost_set / _set_params is called (cached choices expire)
+uint64_t cost_generation();  // changes whenever the constants may have (cached choices expire)
+// FTAR_COST_FILE's parse status (FTAR_SUCCESS when unset); a failure also sets the error text
+ftar_status_t cost_file_status();
 // every ordered factorization of n into factors >= 2 (cost_model/GetWidth.h:10-47)
 void factorizations(size_t n, std::vector<size_t>& cur, std::vector<std::vector<size_t>>& out);
 // the direct forms run it as one gather-and-fold round plus one all-gather round (schedule.cpp)

@@ -134,6 +134,8 @@ _lib.ftar_cost_set_params.argtypes = [ctypes.c_double] * 3
 _lib.ftar_cost_get_params.argtypes = [ctypes.POINTER(ctypes.c_double)] * 3
 _lib.ftar_cost_set.argtypes = [ctypes.POINTER(CostParams)]
 _lib.ftar_cost_get.argtypes = [ctypes.POINTER(CostParams)]
+_lib.ftar_cost_load.argtypes = [ctypes.c_char_p]
+_lib.ftar_cost_save.argtypes = [ctypes.c_char_p]
 _lib.ftar_cost_predict.argtypes = [ctypes.POINTER(Topo), _int, _sz, _int, _sz, _int]
 _lib.ftar_cost_predict.restype = ctypes.c_double
 _lib.ftar_exec_choose.argtypes = [_int, _sz, _int, ctypes.POINTER(Exec)]
@@ -404,6 +406,18 @@ def cost_set(**kw):
     p = CostParams(**{k: float(v or 0.0) for k, v in kw.items()})
     _check(_lib.ftar_cost_set(ctypes.byref(p)), "ftar_cost_set")
     return cost_get()
+
+
+def cost_load(path):
+    """Load the execution model's constants from a calibration file (ftar_cost_load; FTAR_COST_FILE does the
+    same at first use).  Returns cost_get()."""
+    _check(_lib.ftar_cost_load(os.fsencode(path)), "ftar_cost_load")
+    return cost_get()
+
+
+def cost_save(path):
+    """Write the constants in effect to a calibration file (ftar_cost_save)."""
+    _check(_lib.ftar_cost_save(os.fsencode(path)), "ftar_cost_save")
 
 
 def cost_predict(t, form, chunk_bytes, nranks, nbytes, registered=False):

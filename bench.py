@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--no-engine-local", action="store_true",
                     help="N=1: skip the engine_local line item (P = 8 in-process ranks on this GPU at the C4 bucket)")
+    ap.add_argument("--save-cost", default="",
+                    help="N>1: write the execution model's constants re-fitted on this node to this calibration "
+                         "file (rank 0; load it with FTAR_COST_FILE so every later MPI_Allreduce_FT prices with them)")
     ap.add_argument("--engine-local-only", action="store_true",
                     help="run only the engine_local line item (for a kernel trace of it) and print it")
     ap.add_argument("--force-dist", action="store_true", help="take the torchrun/RCCL path even at WORLD_SIZE=1")
@@ -1617,6 +1620,9 @@ def bench_distributed(a):
     phase("cost model")
     try:
         state["line"]["cost_model"] = validate_model(sweep)
+        if a.save_cost and rank == 0:   # the node's calibration, for FTAR_COST_FILE
+            ftar.cost_save(a.save_cost)
+            state["line"]["cost_model"]["saved_to"] = a.save_cost
     except Exception as e:  # noqa: BLE001  the model's report must not cost the run its line
         state["line"]["cost_model"] = {"error": str(e)[:200]}
 

@@ -178,6 +178,14 @@ typedef struct {
 } ftar_cost_params_t;
 ftar_status_t ftar_cost_set(const ftar_cost_params_t* params);
 ftar_status_t ftar_cost_get(ftar_cost_params_t* params);
+/* Calibration files: the constants a run on the node fitted (bench.py --save-cost), so every later
+ * MPI_Allreduce_FT on that node prices with them.  One "<field> <value>" per line ('#' comments), the
+ * fields named as in ftar_cost_params_t, values > 0; fields left out keep their defaults.  Precedence:
+ * FTAR_COST_<FIELD> > ftar_cost_set > the file > the defaults.  FTAR_COST_FILE=<path> loads one (re-read
+ * when the variable changes; an unreadable or malformed file fails communicator bring-up with
+ * FTAR_ERR_INVALID_ARG).  ftar_cost_save writes the constants in effect. */
+ftar_status_t ftar_cost_load(const char* path);
+ftar_status_t ftar_cost_save(const char* path);
 /* Predicted seconds of one AllReduce of `bytes` per rank: topology, form
  * (not AUTO), piece size (0 = whole blocks); registered != 0 prices the peer
  * forms on registered buffers (no local pass).  < 0: not runnable that way. */

@@ -12,6 +12,7 @@ GiB, MiB = 1 << 30, 1 << 20
 
 @pytest.fixture(autouse=True)
 def _defaults(monkeypatch):
+    monkeypatch.delenv("FTAR_COST_FILE", raising=False)
     for k in ("ALPHA_US", "LINK_GBPS", "HBM_GBPS", "ISSUE_US", "BARRIER_US", "PEER_READ_GBPS", "PEER_WRITE_GBPS",
               "COPY_GBPS", "COLL_GBPS"):
         monkeypatch.delenv("FTAR_COST_" + k, raising=False)
@@ -161,3 +162,54 @@ def test_choice_is_a_pure_function_of_the_constants():
     assert ftar.exec_choose(8, GiB).as_dict() == a
     ftar.cost_set(alpha_us=4000.0)
     assert ftar.exec_choose(8, GiB).as_dict() != a
+
+
+def test_calibration_file_round_trip_and_precedence(tmp_path, monkeypatch):
+    """A run on the node saves its fitted constants (ftar_cost_save, bench.py --save-cost); a later process
+    loads them (ftar_cost_load or FTAR_COST_FILE) and the model prices with them.  Precedence:
+    FTAR_COST_<FIELD> > ftar_cost_set > the file > the defaults."""
+    path = str(tmp_path / "node.cost")
+    ftar.cost_set(alpha_us=33.0, link_gbps=61.5, peer_read_gbps=90.0, issue_us=12.0)
+    fitted = ftar.cost_get()
+    ftar.cost_save(path)
+    ftar.cost_set()
+    assert ftar.cost_get()["peer_read_gbps"] == 0.0
+    assert ftar.cost_load(path) == pytest.approx(fitted)
+    with open(path) as f:
+        assert "alpha_us 33\n" in f.read()
+    # the loaded peer rate makes the peer form a candidate: the choice moves with the file
+    e = ftar.exec_choose(8, GiB)
+    assert ftar.cost_predict("8", "peer-read", 0, 8, GiB) is not None
+    ftar.cost_set(link_gbps=10.0)   # set beats the file
+    assert ftar.cost_get()["link_gbps"] == pytest.approx(10.0) and ftar.cost_get()["alpha_us"] == pytest.approx(33.0)
+    monkeypatch.setenv("FTAR_COST_LINK_GBPS", "7")   # the environment beats both
+    assert ftar.cost_get()["link_gbps"] == pytest.approx(7.0)
+    assert e.seconds > 0
+
+
+def test_cost_file_from_the_environment(tmp_path, monkeypatch):
+    a, b = tmp_path / "a.cost", tmp_path / "b.cost"
+    a.write_text("# node A\nalpha_us = 40\nlink_gbps 70   # per peer\n\n")
+    b.write_text("coll_gbps 300\n")
+    monkeypatch.setenv("FTAR_COST_FILE", str(a))
+    k = ftar.cost_get()
+    assert k["alpha_us"] == pytest.approx(40.0) and k["link_gbps"] == pytest.approx(70.0) and k["coll_gbps"] == 0.0
+    monkeypatch.setenv("FTAR_COST_FILE", str(b))   # re-read when the variable changes
+    k = ftar.cost_get()
+    assert k["alpha_us"] == pytest.approx(20.0) and k["coll_gbps"] == pytest.approx(300.0)
+    monkeypatch.delenv("FTAR_COST_FILE")
+    assert ftar.cost_get()["coll_gbps"] == 0.0
+
+
+@pytest.mark.parametrize("text", ["alpha_us 0\n", "alpha_us -3\n", "not_a_field 5\n", "link_gbps 5 6\n",
+                                  "link_gbps fast\n", "link_gbps nan\n"])
+def test_malformed_cost_files_are_refused(tmp_path, text):
+    p = tmp_path / "bad.cost"
+    p.write_text("issue_us 10\n" + text)
+    before = ftar.cost_get()
+    with pytest.raises(ftar.FtarError) as e:
+        ftar.cost_load(str(p))
+    assert e.value.status == 1 and "line 2" in str(e.value)
+    assert ftar.cost_get() == before   # nothing of the file applied
+    with pytest.raises(ftar.FtarError):
+        ftar.cost_load(str(tmp_path / "missing.cost"))

@@ -210,6 +210,38 @@ def test_rccl_comm_refuses_a_cu_masked_reduce_stream(monkeypatch):
         g.destroy()
 
 
+def test_cost_file_at_bring_up(tmp_path, monkeypatch):
+    """FTAR_COST_FILE: a calibration file that does not parse fails communicator bring-up loudly (every rank
+    reads the same environment); a good one sets the constants the engine's choices use."""
+    import ftar
+    bad = tmp_path / "bad.cost"
+    bad.write_text("link_gbps -1\n")
+    monkeypatch.setenv("FTAR_COST_FILE", str(bad))
+    with pytest.raises(ftar.FtarError) as e:
+        ftar.Comm.init_local(2)
+    assert e.value.status == 1 and "FTAR_COST_FILE" in str(e.value)
+    good = tmp_path / "good.cost"
+    # a node with cheap pieces and fast links: a 16 MiB bucket is cut into 4 MiB pieces (the defaults keep
+    # whole blocks there)
+    good.write_text("alpha_us 0.05\nissue_us 0.05\nlink_gbps 700\n")
+    monkeypatch.setenv("FTAR_COST_FILE", str(good))
+    g = ftar.Comm.init_local(2)
+    try:
+        n = 1 << 22
+        ins = [fi.fill("f32", 3, r, n) for r in range(2)]
+        send = [to_dev(x) for x in ins]
+        recv = [filled_dev(x.nbytes) for x in ins]
+        g.allreduce([p for _, p in send], [p for _, p in recv], n, "f32", "sum", topo_="2")
+        ref = oracle_lib.allreduce(ins, "2", outofplace=True)
+        for r in range(2):
+            np.testing.assert_array_equal(from_dev(recv[r][0], np.float32, n).view(np.uint32), ref[r].view(np.uint32))
+        assert g.comms[0].last_exec()["chunk_bytes"] == 4 << 20, g.comms[0].last_exec()
+    finally:
+        g.destroy()
+        monkeypatch.delenv("FTAR_COST_FILE")
+        ftar.cost_set()
+
+
 @pytest.mark.parametrize("P,topo", [(2, "2"), (4, "2,2"), (8, "8"), (8, "2,4"), (8, "2,2,2"), (9, "3,3")])
 @pytest.mark.parametrize("outofplace", [False, True])
 def test_allreduce_collective_allgather(P, topo, outofplace):

@@ -71,13 +71,14 @@ def test_bench_rccl_failure_paths_at_world_size_one(env_extra, why):
 
 
 @pytest.mark.parametrize("ranks", [2, pytest.param(4, marks=pytest.mark.wide)])
-def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
+def test_bench_n_gt_1_rehearsal_over_rccl(ranks, tmp_path):
     """The same N > 1 run with RCCL itself carrying the default configuration and every RCCL form of the sweep
     (--rccl-loopback: one NCCL_HOSTID per rank, ncclSend/ncclRecv over loopback sockets, the ranks sharing the
     box's GPU): no fallback is taken, the default configuration is RCCL p2p and validates, and rccl_p2p_best is
     in the line with a validated entry -- the fields the driver's 8-GPU run reports, produced by a real
     multi-rank RCCL communicator."""
-    d = _bench(ranks, ["--rccl-loopback", "--no-cpu-baseline"], {"FTAR_BENCH_BUDGET_S": "160"})
+    cost_file = str(tmp_path / "node.cost")
+    d = _bench(ranks, ["--rccl-loopback", "--no-cpu-baseline", "--save-cost", cost_file], {"FTAR_BENCH_BUDGET_S": "160"})
     assert d["n_gpus"] == ranks and d["check"] == "ok" and "watchdog" not in d, d
     assert "rccl_init_error" not in d and "rccl_error_by_rank" not in d, d.get("rccl_init_error")
     # the default configuration is the execution model's: form "auto", which ran the one-round RCCL forms
@@ -103,3 +104,9 @@ def test_bench_n_gt_1_rehearsal_over_rccl(ranks):
                                                                                                 "collective")]
     assert rccl_ok and not [r for r in d["sweep"] if r.get("check") == "MISMATCH"], d["sweep"]
     assert "RCCL over loopback" in d["config"]["parallelism"], d["config"]
+    # the node's calibration file: the re-fitted constants, in the format FTAR_COST_FILE loads
+    assert cm["saved_to"] == cost_file
+    with open(cost_file) as f:
+        saved = dict((ln.split()[0], float(ln.split()[1])) for ln in f if ln.strip() and not ln.startswith("#"))
+    for k, v in saved.items():
+        assert v == pytest.approx(cm["constants_refit"][k], rel=1e-3, abs=1e-3), (k, v, cm["constants_refit"])
