@@ -406,6 +406,35 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
                      "hbm_frac": round(hbm / (wms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "model_ms": round(ftar.exec_choose(world, n * esz, topo_=topo, form="direct",
                                                         chunk_bytes=split * esz).seconds * 1e3, 4)}
+        peer = None
+        if chunk_bytes is None:
+            # the peer-read form on registered buffers, the IPC form a node may pick: the fold reads the 8
+            # inputs where they lie, the gather pulls the 7 final blocks -- no scratch pass: 9 + 14 block
+            # passes per rank instead of 37 (the same kernels read peers' HBM over xGMI on a node)
+            ids = g.register(xs, n * esz) + g.register(ys, n * esz)
+            try:
+                g.set_peer_direct("read")
+                call()
+                pper = []
+                for _ in range(steps):
+                    torch.cuda.synchronize()
+                    e0.record(stream)
+                    call()
+                    e1.record(stream)
+                    torch.cuda.synchronize()
+                    pper.append(e0.elapsed_time(e1))
+                pms = sorted(pper)[len(pper) // 2]
+                pbytes = world * ((world + 1) + 2 * (world - 1)) * split * esz
+                pok = all(bool(torch.equal(y[idx].view(torch.int32), want.view(torch.int32))) for y in ys)
+                ran = g.comms[0].last_exec()["form"]
+                peer = {"form": ran, "ms_median": round(pms, 4), "hbm_bytes_per_call": pbytes,
+                        "hbm_GBps": round(pbytes / (pms * 1e-3) / 1e9, 1),
+                        "hbm_frac": round(pbytes / (pms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                        "check": "bit-exact (the same sample)" if pok else "MISMATCH"}
+            finally:
+                g.set_peer_direct(0)
+                g.deregister(ids[:world])
+                g.deregister(ids[world:])
         return {"workload": f"P = {world} in-process ranks on one MI355X, tree({topo}) direct, C4 bucket "
                             f"(2^28 fp32 per rank), " + ("the model's piece" if chunk_bytes is None else "piece fixed"),
                 "ranks": world, "elements_per_rank": n, "topology": topo, "form": "direct",
@@ -413,7 +442,7 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
                 "ms_all": [round(x, 4) for x in per], "wall_s": round(wall, 3),
                 "hbm_bytes_per_call": hbm, "hbm_GBps": round(gbps, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
                 "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4), "check": "bit-exact (4096-element sample, every rank)"
-                if ok else "MISMATCH", "whole_blocks": whole,
+                if ok else "MISMATCH", "whole_blocks": whole, "peer_read_registered": peer,
                 "note": "HBM bytes from the plans: every received block one device copy (read + write), every "
                         "fold k sources + 1 destination; all 8 ranks' copies and folds share this GPU's HBM. "
                         "ms = events around the group call, which returns once every rank's stream drained "
