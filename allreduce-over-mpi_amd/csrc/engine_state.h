@@ -1,5 +1,6 @@
 // The communicator's state and the engine's interfaces between its translation units (not the C ABI):
-//   engine.cpp       communicator lifecycle and settings, the two-stream executor, the C API
+//   engine.cpp       communicator lifecycle and settings, the two-stream executor
+//   engine_api.cpp   the C ABI (bring-up, setters, entry points, in-process group calls)
 //   engine_peer.cpp  the peer-direct forms (IPC-mapped exchange buffers over xGMI) and the xGMI probe
 //   engine_host.cpp  host buffers on a host-bootstrapped communicator, the piece-pipelined read form
 #pragma once
@@ -120,6 +121,23 @@ ftar_status_t mark(ftar_comm* c, const std::string& name, hipStream_t s);
 ftar_status_t grow_events(ftar_comm* c, size_t n);
 // FTAR_ERR_UNSUPPORTED (with a message) when a buffer would grow under stream capture
 ftar_status_t refuse_growth_under_capture(const ftar_comm* c, const char* what);
+
+// ---- engine.cpp -----------------------------------------------------------------------------------------
+// Host mode piece per block: 0 = auto (auto_host_chunk)
+constexpr size_t kDefaultHostChunkBytes = 0;
+struct HostIO;
+// bring-up of a communicator whose transport is set (streams, settings from the environment; a
+// host-bootstrapped one agrees on them here), and its teardown (false: it must not be freed)
+ftar_status_t comm_setup(ftar_comm* c);
+bool comm_teardown(ftar_comm* c);
+// one call on a communicator (device buffers, or host ones when `host` is set)
+ftar_status_t allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dt, ftar_op_t op,
+                        const ftar_topo_t* topo, ftar_comm* c, hipStream_t stream, const HostIO* host = nullptr);
+// the reduce stream on `cus` CUs (0 = all); refused on RCCL communicators
+ftar_status_t set_reduce_cus(ftar_comm* c, int cus);
+// the form the explicit settings describe (ftar_form_t), or -2; set_form applies one
+int form_of(const ftar_comm* c);
+void set_form(ftar_comm* c, int form);
 
 // ---- engine_peer.cpp ------------------------------------------------------------------------------------
 // a one-round plan the peer kernels can run (one block per peer each way, all-gather straight into recvbuf)
