@@ -51,7 +51,8 @@ def fmt(x, nd=1):
 def report(d):
     c, roof = d.get("config", {}), d.get("roofline") or {}
     print(f"== N={d['n_gpus']}: value {fmt(d.get('value'))} GB/s, {fmt(d.get('ms_per_step'), 3)} ms/call "
-          f"[{c.get('form')} topo {c.get('topology')} chunk {c.get('chunk_bytes')}] check {d.get('check')}")
+          f"[{c.get('form_label') or c.get('form')} topo {c.get('topology')} chunk {c.get('chunk_bytes')}] "
+          f"check {d.get('check')}")
     print(f"   busBW {fmt(d.get('busbw_GBps_per_rank'))} GB/s/rank; roofline {roof.get('bound')} frac {roof.get('frac')}"
           f" (probe {roof.get('frac_of_probe')})  selection: {d.get('config_selection')}")
     if d.get("watchdog"):
@@ -65,6 +66,9 @@ def report(d):
         print(f"   rccl_p2p_best: {rb['form']} topo {rb['topology']} chunk {rb['chunk_bytes']}: {rb['ms']} ms, "
               f"busBW {rb['busbw_GBps_per_rank']} (frac {(rb.get('roofline') or {}).get('frac')})"
               f"{' = headline' if rb.get('is_headline') else ''}")
+    for form, item in (d.get("c4_ring") or {}).items():
+        print(f"   c4_ring {item.get('form_label')}: {item.get('ms')} ms, busBW {item.get('busbw_GBps_per_rank')} "
+              f"(frac {(item.get('roofline') or {}).get('frac')}){'  <- judged (>= 70 % target)' if item.get('judged') else ''}")
     best = {}
     for r in d.get("sweep") or []:
         if r.get("check") == "ok" and "ms" in r:
@@ -89,10 +93,21 @@ def report(d):
     if isinstance(fit, dict) and "fitted" in fit:
         print(f"   cost model fitted {fit['fitted']} -> {fit.get('choice_fitted')} (reference model: "
               f"{fit.get('choice_reference_model')})")
+    cm = d.get("cost_model")
+    if isinstance(cm, dict) and "constants_refit" in cm:
+        p2p = cm.get("refit_p2p") or {}
+        print(f"   cost model refit {cm['constants_refit']}; unidentified (prior kept): {p2p.get('unidentified')}"
+              f"{'; kept the prior whole' if p2p.get('kept_prior') else ''}; regret {cm.get('regret_refit')}"
+              f"{'; saved to ' + cm['saved_to'] if cm.get('saved_to') else ''}")
+        for f, r in (cm.get("refit_rates") or {}).items():
+            if r and r.get("unidentified"):
+                print(f"     {f}: unidentified ({r['unidentified']}), prior {r.get('value')} kept")
     c5 = d.get("c5_bf16")
     if isinstance(c5, dict) and "ms" in c5:
         ow = ", ".join(f"{k} {v.get('ms')}ms" for k, v in (c5.get("other_widths") or {}).items())
-        print(f"   C5 bf16: {c5['topology']} {c5['ms']} ms ({c5.get('check')}); other widths: {ow}")
+        tie = (f"; the model's width was a tie of {c5.get('model_tied')} broken by {c5.get('model_tie_broken_by')}"
+               if (c5.get("model_tied") or 1) > 1 else "")
+        print(f"   C5 bf16: {c5['topology']} {c5['ms']} ms ({c5.get('check')}){tie}; other widths: {ow}")
     he = d.get("host_e2e")
     if isinstance(he, dict) and "ms" in he:
         print(f"   host e2e: {he['ms']} ms = {he.get('algbw_GBps_per_rank')} GB/s/rank ({he.get('check')})")
