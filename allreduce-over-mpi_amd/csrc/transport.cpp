@@ -518,6 +518,7 @@ struct LocalHub {
     hipEvent_t ready = nullptr;  // sender-side data ready
     hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
     bool taken = false;
+    int device = -1;  // the sender's device
     ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
       if (ready) hub->give_event(ready);
       if (done) hub->give_event(done);
@@ -707,6 +708,7 @@ class LocalTransport final : public Transport {
       p->buf = o.buf;
       p->bytes = o.bytes;
       p->ready = nullptr;
+      FTAR_CHECK_HIP(hipGetDevice(&p->device));
       FTAR_RETURN_IF(hub_->take_event(&p->ready));
       FTAR_CHECK_HIP(hipEventRecord(p->ready, o.s));
       mine.push_back(p);
@@ -733,7 +735,16 @@ class LocalTransport final : public Transport {
         return FTAR_ERR_INTERNAL;
       }
       FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
-      if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
+      // FTAR_LOCAL_COPY=kernel (A/B): a receive from a rank on this device is ftar's own copy kernel
+      // (launch_copy: the LDS-staged copy when co-aligned), one launch per receive
+      static const bool kernel_copy = [] {
+        const char* e = getenv("FTAR_LOCAL_COPY");
+        return e && !strcmp(e, "kernel");
+      }();
+      int dev = -1;
+      if (kernel_copy) FTAR_CHECK_HIP(hipGetDevice(&dev));
+      if (o.bytes && kernel_copy && p->device == dev) FTAR_RETURN_IF(launch_copy(p->buf, o.buf, o.bytes, o.s));
+      else if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
       hipEvent_t done = nullptr;
       FTAR_RETURN_IF(hub_->take_event(&done));
       if (hipEventRecord(done, o.s) != hipSuccess) {
