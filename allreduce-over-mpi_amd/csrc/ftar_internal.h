@@ -74,7 +74,7 @@ void from_topology(const Topology& t, ftar_topo_t* out);
 struct CostParams {  // seconds and bytes per second
   double alpha, link, hbm, issue, barrier, peer_read, peer_write, copy, coll;
 };
-CostParams cost_params();  // defaults <- ftar_cost_set <- FTAR_COST_* environment
+CostParams cost_params();  // defaults <- calibration file <- ftar_cost_set <- FTAR_COST_* environment
 uint64_t cost_generation();  // changes whenever the constants may have (cached choices expire)
 // FTAR_COST_FILE's parse status (FTAR_SUCCESS when unset); a failure also sets the error text
 ftar_status_t cost_file_status();

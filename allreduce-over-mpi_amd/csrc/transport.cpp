@@ -735,11 +735,15 @@ class LocalTransport final : public Transport {
         return FTAR_ERR_INTERNAL;
       }
       FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
-      // FTAR_LOCAL_COPY=kernel (A/B): a receive from a rank on this device is ftar's own copy kernel
-      // (launch_copy: the LDS-staged copy when co-aligned), one launch per receive
+      // A receive from a rank on this device is ftar's own copy kernel, one launch per receive (launch_copy:
+      // the LDS-staged copy when co-aligned): 5-6 % faster than the runtime's blit at the C4 bucket with 8
+      // ranks on one GPU (profiles/r05/engine_local/ab2_*, 3 interleaved rounds); one launch per piece group
+      // instead lost 2 % (it filled the GPU, and the folds stopped overlapping the copies).  A receive from
+      // another device keeps the runtime's copy (peer access may be off).  FTAR_LOCAL_COPY=runtime: the
+      // runtime's copy for every receive (the A/B).
       static const bool kernel_copy = [] {
         const char* e = getenv("FTAR_LOCAL_COPY");
-        return e && !strcmp(e, "kernel");
+        return !(e && !strcmp(e, "runtime"));
       }();
       int dev = -1;
       if (kernel_copy) FTAR_CHECK_HIP(hipGetDevice(&dev));
