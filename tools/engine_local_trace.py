@@ -61,7 +61,9 @@ def intersect(a, b):
 
 
 def is_fold(name):
-    return "reduce_lds_kernel" in name or "reduce_vec_kernel" in name or "reduce_tree" in name
+    """a reduce kernel of k >= 2 sources; the k = 1 instance (kernarg Srcs<1>) is launch_copy, a transfer"""
+    return ("reduce_lds_kernel" in name or "reduce_vec_kernel" in name or "reduce_tree" in name) and \
+        "Srcs<1>" not in name
 
 
 def main():
