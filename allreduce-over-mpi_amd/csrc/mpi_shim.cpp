@@ -221,12 +221,31 @@ int check_env_topo(int nranks) {
   return last_rc;
 }
 
+// FTAR_COST_FILE (the node's calibration, ftar.h): a file that does not parse fails the call with
+// MPI_ERR_ARG on every rank before anything is brought up, rather than the auto transport taking it for an
+// RCCL failure; the last verdict per path is kept
+int check_cost_file() {
+  const char* f = getenv("FTAR_COST_FILE");
+  if (!f || !*f) return MPI_SUCCESS;
+  static std::mutex mu;
+  static std::string last;
+  static int last_rc = MPI_SUCCESS;
+  std::lock_guard<std::mutex> g(mu);
+  if (last != f) {
+    last = f;
+    last_rc = ftar_cost_load(f) == FTAR_SUCCESS ? MPI_SUCCESS : MPI_ERR_ARG;
+  }
+  return last_rc;
+}
+
 // before the communicator's bring-up, as get_stages precedes everything in the
-// reference's call: a bad FT_TOPO fails every rank alike, GPU or not
+// reference's call: a bad FT_TOPO fails every rank alike, GPU or not (and so
+// does a calibration file that does not parse)
 int check_topo_first(MPI_Comm comm) {
   int size = 1;
   if (MPI_Comm_size(comm, &size) != MPI_SUCCESS) return MPI_ERR_COMM;
-  return check_env_topo(size);
+  const int rc = check_env_topo(size);
+  return rc != MPI_SUCCESS ? rc : check_cost_file();
 }
 
 int status_to_mpi(ftar_status_t st) {

@@ -79,6 +79,26 @@ def test_harness_invalid_ft_topo_fails_every_rank(tmp_path, ranks, topo, lonely)
 
 
 @needs
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_harness_bad_cost_file_fails_every_rank(tmp_path, ranks):
+    """FTAR_COST_FILE naming a calibration file that does not parse: MPI_Allreduce_FT returns MPI_ERR_ARG on
+    every rank before anything is brought up (no GPU involved), like an invalid FT_TOPO; a good file runs."""
+    bad = tmp_path / "bad.cost"
+    bad.write_text("link_gbps fast\n")
+    base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY", "FTAR_COST_FILE")}
+    p = subprocess.run([MPIEXEC, "-n", str(ranks), BIN, "--size", "4096", "--repeat", "2", "--check"], cwd=tmp_path,
+                       env=dict(base, FTAR_COST_FILE=str(bad), FT_TOPO="1"), capture_output=True, text=True, timeout=120)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0 and f"FAILED: allreduce failed on {ranks} of {ranks} ranks" in out, out
+    if ranks == 1:
+        good = tmp_path / "good.cost"
+        good.write_text("alpha_us 30\n")
+        p = subprocess.run([MPIEXEC, "-n", "1", BIN, "--size", "1000", "--repeat", "2", "--check"], cwd=tmp_path,
+                           env=dict(base, FTAR_COST_FILE=str(good)), capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0 and "(test passed)" in p.stdout, p.stdout + p.stderr
+
+
+@needs
 def test_harness_ft_topo_valid_single_rank(tmp_path):
     """The valid spellings at one rank (the ring "1", unset) still copy: the P <= 1 path."""
     base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY")}
