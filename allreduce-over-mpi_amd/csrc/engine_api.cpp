@@ -171,18 +171,21 @@ ftar_status_t ftar_comm_set_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter
 
 ftar_status_t ftar_comm_get_reduce_scatter(ftar_comm_t comm, ftar_reduce_scatter_t* mode) {
   if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *mode = static_cast<ftar_reduce_scatter_t>(comm->reduce_scatter);
   return FTAR_SUCCESS;
 }
 
 ftar_status_t ftar_comm_get_allgather(ftar_comm_t comm, ftar_allgather_t* mode) {
   if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *mode = static_cast<ftar_allgather_t>(comm->allgather);
   return FTAR_SUCCESS;
 }
 
 ftar_status_t ftar_comm_get_chunk_bytes(ftar_comm_t comm, size_t* bytes) {
   if (!comm || !bytes) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *bytes = comm->chunk_bytes;
   return FTAR_SUCCESS;
 }
@@ -269,6 +272,7 @@ ftar_status_t ftar_debug_set_peer_dma(ftar_comm_t comm, int dma) {
 
 ftar_status_t ftar_comm_get_peer_direct(ftar_comm_t comm, int* mode) {
   if (!comm || !mode) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *mode = comm->peer_direct;
   return FTAR_SUCCESS;
 }
@@ -358,6 +362,7 @@ ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus) {
 
 ftar_status_t ftar_comm_get_reduce_cus(ftar_comm_t comm, int* cus) {
   if (!comm || !cus) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *cus = comm->reduce_cus;
   return FTAR_SUCCESS;
 }
@@ -371,6 +376,7 @@ ftar_status_t ftar_comm_set_host_chunk_bytes(ftar_comm_t comm, size_t bytes) {
 
 ftar_status_t ftar_comm_get_host_chunk_bytes(ftar_comm_t comm, size_t* bytes) {
   if (!comm || !bytes) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
   *bytes = comm->host_chunk_bytes;
   return FTAR_SUCCESS;
 }
