@@ -1,8 +1,15 @@
 // The C ABI of the engine (include/ftar.h): communicator bring-up and teardown, the setters and getters,
 // the AllReduce entry points and the in-process group calls.  Split out of engine.cpp (round 5); no
 // behaviour change.
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -391,13 +398,83 @@ ftar_status_t ftar_rccl_allreduce(const void* sendbuf, void* recvbuf, size_t cou
 }
 
 namespace {
+// Host threads for the ranks of the in-process group calls, kept from call to call instead of one
+// std::thread per rank per call (their start and join sat inside every call's time).  The ranks of a call
+// meet in the transport, so they must all run at once: every job is handed to a worker that is free at
+// that moment, and a call that finds fewer free workers than ranks starts more (the pool only grows; its
+// workers wait on a condition variable between calls).  Leaked on purpose -- the workers are detached.
+class RankPool {
+ public:
+  static RankPool& get() {
+    static std::atomic<RankPool*> pool{nullptr};
+    RankPool* p = pool.load();
+    if (!p || p->pid_ != getpid()) {  // first use, or a forked child (the parent's workers are not here)
+      RankPool* fresh = new RankPool;
+      if (pool.compare_exchange_strong(p, fresh)) return *fresh;
+      delete fresh;  // another thread installed one first
+      return *pool.load();
+    }
+    return *p;
+  }
+  // fn(0) ... fn(n - 1), all at once on pool workers; returns when every one has returned
+  void run(int n, const std::function<void(int)>& fn) {
+    Latch done{n};
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      const int take = std::min(free_, n);
+      free_ -= take;
+      for (int i = take; i < n; ++i) std::thread([this] { work(); }).detach();
+      for (int r = 0; r < n; ++r) q_.push_back({&fn, r, &done});
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lk(done.mu);
+    done.cv.wait(lk, [&] { return done.left == 0; });
+  }
+
+ private:
+  struct Latch {
+    int left;
+    std::mutex mu;
+    std::condition_variable cv;
+  };
+  struct Job {
+    const std::function<void(int)>* fn;
+    int rank;
+    Latch* done;
+  };
+  // a worker is started for a job already counted against it, and counts itself free again only once
+  // its job has returned: so every queued job has a worker that is not busy with anything else
+  void work() {
+    for (;;) {
+      Job j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !q_.empty(); });
+        j = q_.front();
+        q_.pop_front();
+      }
+      (*j.fn)(j.rank);
+      {
+        std::lock_guard<std::mutex> g(j.done->mu);
+        if (--j.done->left == 0) j.done->cv.notify_all();
+      }
+      std::lock_guard<std::mutex> g(mu_);
+      ++free_;
+    }
+  }
+  const pid_t pid_ = getpid();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Job> q_;
+  int free_ = 0;
+};
+
 ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size_t count, ftar_dtype_t dtype,
                         ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms, int nranks,
                         void* const* streams, bool host) {
   if (!recvbufs || !comms || nranks <= 0) return FTAR_ERR_INVALID_ARG;
   std::vector<ftar_status_t> st(nranks, FTAR_SUCCESS);
   std::vector<std::string> why(nranks);
-  std::vector<std::thread> th;
   // Capturing streams (the caller's capture stream for every rank): the ranks' threads take turns issuing
   // (Transport::capture_enter), and nobody synchronises; the caller ends the capture.
   bool capturing = false;
@@ -419,20 +496,19 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
                         __FILE__, __LINE__);
         return FTAR_ERR_UNSUPPORTED;
       }
-  for (int r = 0; r < nranks; ++r)
-    th.emplace_back([&, r] {
-      hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;
-      const void* sb = sendbufs ? sendbufs[r] : nullptr;
-      if (capturing) comms[r]->tp->capture_enter();
-      st[r] = host ? ftar_allreduce_host(sb, recvbufs[r], count, dtype, op, topo, comms[r], s)
-                   : ftar::allreduce(sb, recvbufs[r], count, dtype, op, topo, comms[r], s);
-      if (capturing) comms[r]->tp->capture_leave();
-      if (!capturing && st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
-          hipStreamSynchronize(s) != hipSuccess)
-        st[r] = FTAR_ERR_HIP;
-      if (st[r] != FTAR_SUCCESS) why[r] = ftar::last_error();  // the error text is per thread
-    });
-  for (auto& t : th) t.join();
+  auto rank_call = [&](int r) {
+    hipStream_t s = streams ? static_cast<hipStream_t>(streams[r]) : nullptr;
+    const void* sb = sendbufs ? sendbufs[r] : nullptr;
+    if (capturing) comms[r]->tp->capture_enter();
+    st[r] = host ? ftar_allreduce_host(sb, recvbufs[r], count, dtype, op, topo, comms[r], s)
+                 : ftar::allreduce(sb, recvbufs[r], count, dtype, op, topo, comms[r], s);
+    if (capturing) comms[r]->tp->capture_leave();
+    if (!capturing && st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
+        hipStreamSynchronize(s) != hipSuccess)
+      st[r] = FTAR_ERR_HIP;
+    if (st[r] != FTAR_SUCCESS) why[r] = ftar::last_error();  // the error text is per thread
+  };
+  RankPool::get().run(nranks, rank_call);
   for (int r = 0; r < nranks; ++r)
     if (st[r] != FTAR_SUCCESS) {
       ftar::set_error("rank " + std::to_string(r) + ": " + why[r], __FILE__, __LINE__);  // to the caller's thread
@@ -441,6 +517,27 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
   return FTAR_SUCCESS;
 }
 }  // namespace
+
+// Test hook (not in ftar.h): `rounds` calls of the group thread pool, each of n jobs that meet at a
+// rendezvous the way a group call's ranks meet in the transport -- a job left waiting for a worker would
+// hang it, so it waits at most a second.  Returns how many rendezvous were complete, out of rounds.
+int ftar_debug_rank_pool(int n, int rounds) {
+  if (n <= 0 || rounds <= 0) return -1;
+  int complete = 0;
+  for (int i = 0; i < rounds; ++i) {
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    std::atomic<int> met{0};
+    RankPool::get().run(n, [&](int) {
+      std::unique_lock<std::mutex> lk(mu);
+      if (++arrived == n) cv.notify_all();
+      if (cv.wait_for(lk, std::chrono::seconds(1), [&] { return arrived == n; })) ++met;
+    });
+    complete += met.load() == n;
+  }
+  return complete;
+}
 
 ftar_status_t ftar_allreduce_group(const void* const* sendbufs, void* const* recvbufs, size_t count,
                                    ftar_dtype_t dtype, ftar_op_t op, const ftar_topo_t* topo, ftar_comm_t* comms,

@@ -282,3 +282,26 @@ def test_stress_drivers_are_built_against_the_product_library():
         assert os.access(path, os.X_OK), path
         deps = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
         assert "libftar.so" in deps and os.path.join(lib, "libftar.so") in deps, deps
+
+
+def test_group_thread_pool_runs_every_rank_at_once():
+    """The in-process group calls' host threads are pooled (engine_api.cpp RankPool): the ranks of a call
+    meet in the transport, so every job of a call must start at once even while other callers' jobs hold
+    workers.  Four caller threads, group sizes 1..8, each job waiting at a rendezvous of its call."""
+    import ctypes
+    import threading
+    import ftar
+    fn = ftar.lib().ftar_debug_rank_pool
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_int, ctypes.c_int]
+    assert fn(0, 1) == -1
+    got = {}
+
+    def caller(i):
+        got[i] = [(n, fn(n, 20)) for n in (8, 1, 3, 7, 2, 5)]
+    th = [threading.Thread(target=caller, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert all(not t.is_alive() for t in th)
+    assert all(done == 20 for runs in got.values() for _, done in runs), got
