@@ -511,19 +511,28 @@ struct LocalHub {
   // Per-message and barrier events are recycled through a pool, never
   // destroyed before the hub: a stream capture may still refer to an event
   // after both sides dropped the message.
+  // A pooled event shared by the messages of one flush: the sends of a flush on one stream share their
+  // data-ready event, the receives of a flush on one stream their copies-done event (one record each
+  // instead of one per message); the last holder gives it back to the pool.
+  using Ev = std::shared_ptr<hipEvent_t>;
   struct Posted {
-    LocalHub* hub = nullptr;
     const void* buf;
     size_t bytes;
-    hipEvent_t ready = nullptr;  // sender-side data ready
-    hipEvent_t done = nullptr;  // receiver-side copy finished (set by receiver)
+    Ev ready;     // sender-side data ready
+    Ev done;      // receiver-side copy finished (set by the receiver)
     bool taken = false;
     int device = -1;  // the sender's device
-    ~Posted() {  // both sides hold a reference until their stream waits/records are enqueued
-      if (ready) hub->give_event(ready);
-      if (done) hub->give_event(done);
-    }
+    int sender = -1;
   };
+  ftar_status_t take_shared(Ev* out) {
+    Ev e(new hipEvent_t(nullptr), [this](hipEvent_t* p) {
+      if (*p) give_event(*p);
+      delete p;
+    });
+    FTAR_RETURN_IF(take_event(e.get()));
+    *out = std::move(e);
+    return FTAR_SUCCESS;
+  }
   // During a capture (this thread holds the issue lock) every record gets a
   // fresh event and used ones retire until the next uncaptured use: an event
   // re-recorded inside one capture -- on another rank's stream after a peer
@@ -562,10 +571,12 @@ struct LocalHub {
     pool.clear();
     retired.clear();
   }
-  // cv wait that lets the other ranks' threads issue meanwhile when this one
-  // holds the issue lock (lock order: issue before mu)
+  // Rank `rank` waits on its own condition variable (a message for it, its message taken, a rendezvous
+  // complete), so a notification wakes the one thread it concerns rather than every rank's.  The wait lets
+  // the other ranks' threads issue meanwhile when this one holds the issue lock (lock order: issue before mu).
   template <class Pred>
-  bool wait(std::unique_lock<std::mutex>& g, Pred pred) {
+  bool wait(std::unique_lock<std::mutex>& g, int rank, Pred pred) {
+    std::condition_variable& cv = rcv[rank];
     if (!t_issue_held) return cv.wait_for(g, std::chrono::seconds(120), pred);
     if (pred()) return true;
     g.unlock();
@@ -582,7 +593,8 @@ struct LocalHub {
     std::vector<const void*> ptr;
     std::vector<std::shared_ptr<hipEvent_t>> ev;
   };
-  explicit LocalHub(int n) : nranks(n), pending(std::make_shared<Round>()) {
+  void notify(int rank) { rcv[rank].notify_all(); }
+  explicit LocalHub(int n) : nranks(n), rcv(new std::condition_variable[n]), pending(std::make_shared<Round>()) {
     pending->ptr.resize(n);
     pending->ev.resize(n);
   }
@@ -601,8 +613,8 @@ struct LocalHub {
       pending->ev.resize(nranks);
       arrived = 0;
       ++gen;
-      cv.notify_all();
-    } else if (!wait(g, [&] { return gen != my_gen; })) {
+      for (int q = 0; q < nranks; ++q) rcv[q].notify_all();
+    } else if (!wait(g, rank, [&] { return gen != my_gen; })) {
       set_error("local transport: rendezvous timed out", __FILE__, __LINE__);
       return FTAR_ERR_TIMEOUT;
     }
@@ -611,7 +623,7 @@ struct LocalHub {
   }
   int nranks;
   std::mutex mu;
-  std::condition_variable cv;
+  std::unique_ptr<std::condition_variable[]> rcv;  // one per rank
   std::map<std::pair<int, int>, std::deque<std::shared_ptr<Posted>>> wire;  // (from, to)
   std::shared_ptr<Round> pending, done;
   int arrived = 0;
@@ -698,32 +710,52 @@ class LocalTransport final : public Transport {
   ftar_status_t flush() {
     std::vector<Op> ops;
     ops.swap(ops_);
-    // 1. publish every send, with an event marking its data ready on the sender's stream
+    using Ev = LocalHub::Ev;
+    // the event of a stream within this flush (sends: data ready; receives: copies done), recorded once
+    auto per_stream = [](std::vector<std::pair<hipStream_t, Ev>>& v, hipStream_t st) -> Ev* {
+      for (auto& x : v)
+        if (x.first == st) return &x.second;
+      v.emplace_back(st, nullptr);
+      return &v.back().second;
+    };
+    // 1. publish every send, with an event marking its data ready on the sender's stream (one per stream)
+    std::vector<std::pair<hipStream_t, Ev>> ready;
     std::vector<std::shared_ptr<LocalHub::Posted>> mine;
+    int dev = -1;
+    FTAR_CHECK_HIP(hipGetDevice(&dev));
     for (auto& o : ops) {
       if (!o.is_send) continue;
       if (o.peer == rank_ || o.peer < 0 || o.peer >= hub_->nranks) return FTAR_ERR_INVALID_ARG;
+      Ev* e = per_stream(ready, o.s);
+      if (!*e) {
+        FTAR_RETURN_IF(hub_->take_shared(e));
+        FTAR_CHECK_HIP(hipEventRecord(**e, o.s));
+      }
       auto p = std::make_shared<LocalHub::Posted>();
-      p->hub = hub_.get();
       p->buf = o.buf;
       p->bytes = o.bytes;
-      p->ready = nullptr;
-      FTAR_CHECK_HIP(hipGetDevice(&p->device));
-      FTAR_RETURN_IF(hub_->take_event(&p->ready));
-      FTAR_CHECK_HIP(hipEventRecord(p->ready, o.s));
+      p->ready = *e;
+      p->device = dev;
+      p->sender = rank_;
       mine.push_back(p);
-      std::lock_guard<std::mutex> g(hub_->mu);
-      hub_->wire[{rank_, o.peer}].push_back(p);
+      {
+        std::lock_guard<std::mutex> g(hub_->mu);
+        hub_->wire[{rank_, o.peer}].push_back(p);
+      }
+      hub_->notify(o.peer);
     }
-    hub_->cv.notify_all();
-    // 2. complete every receive in posting order (per-pair FIFO, like MPI/RCCL)
+    // 2. issue every receive in posting order (per-pair FIFO, like MPI/RCCL): wait for the sender's data,
+    // copy; then one copies-done event per receiving stream, handed to every sender of this flush
+    std::vector<std::pair<hipStream_t, Ev>> done;
+    std::vector<std::pair<std::shared_ptr<LocalHub::Posted>, hipStream_t>> got;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> waited;  // (stream, event) already waited on
     for (auto& o : ops) {
       if (o.is_send) continue;
       std::shared_ptr<LocalHub::Posted> p;
       {
         std::unique_lock<std::mutex> g(hub_->mu);
         auto& q = hub_->wire[{o.peer, rank_}];
-        if (!hub_->wait(g, [&] { return !q.empty(); })) {
+        if (!hub_->wait(g, rank_, [&] { return !q.empty(); })) {
           set_error("local transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
           return FTAR_ERR_TIMEOUT;
         }
@@ -734,7 +766,11 @@ class LocalTransport final : public Transport {
         set_error("local transport: message size mismatch", __FILE__, __LINE__);
         return FTAR_ERR_INTERNAL;
       }
-      FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, p->ready, 0));
+      const std::pair<hipStream_t, hipEvent_t> w{o.s, *p->ready};
+      if (std::find(waited.begin(), waited.end(), w) == waited.end()) {
+        FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, *p->ready, 0));
+        waited.push_back(w);
+      }
       // A receive from a rank on this device is ftar's own copy kernel, one launch per receive (launch_copy:
       // the LDS-staged copy when co-aligned): 5-6 % faster than the runtime's blit at the C4 bucket with 8
       // ranks on one GPU (profiles/r05/engine_local/ab2_*, 3 interleaved rounds); one launch per piece group
@@ -745,40 +781,48 @@ class LocalTransport final : public Transport {
         const char* e = getenv("FTAR_LOCAL_COPY");
         return !(e && !strcmp(e, "runtime"));
       }();
-      int dev = -1;
-      if (kernel_copy) FTAR_CHECK_HIP(hipGetDevice(&dev));
       if (o.bytes && kernel_copy && p->device == dev) FTAR_RETURN_IF(launch_copy(p->buf, o.buf, o.bytes, o.s));
       else if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
-      hipEvent_t done = nullptr;
-      FTAR_RETURN_IF(hub_->take_event(&done));
-      if (hipEventRecord(done, o.s) != hipSuccess) {
-        hub_->give_event(done);
+      got.emplace_back(std::move(p), o.s);
+    }
+    for (auto& x : got) {
+      Ev* e = per_stream(done, x.second);
+      if (*e) continue;
+      FTAR_RETURN_IF(hub_->take_shared(e));
+      if (hipEventRecord(**e, x.second) != hipSuccess) {
         set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
         return FTAR_ERR_HIP;
       }
-      {
-        std::lock_guard<std::mutex> g(hub_->mu);
-        p->done = done;
-        p->taken = true;
-      }
-      hub_->cv.notify_all();
     }
+    {
+      std::lock_guard<std::mutex> g(hub_->mu);
+      for (auto& x : got) {
+        x.first->done = *per_stream(done, x.second);
+        x.first->taken = true;
+      }
+    }
+    for (auto& x : got) hub_->notify(x.first->sender);
     // 3. the sender's stream may not move on (and overwrite the source) before the copy
+    waited.clear();
     size_t i = 0;
     for (auto& o : ops) {
       if (!o.is_send) continue;
       auto& p = mine[i++];
-      hipEvent_t done;
+      Ev d;
       {
         std::unique_lock<std::mutex> g(hub_->mu);
-        if (!hub_->wait(g, [&] { return p->taken; })) {
+        if (!hub_->wait(g, rank_, [&] { return p->taken; })) {
           set_error("local transport: send to rank " + std::to_string(o.peer) + " never received", __FILE__,
                     __LINE__);
           return FTAR_ERR_TIMEOUT;
         }
-        done = p->done;
+        d = p->done;
       }
-      FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, done, 0));
+      const std::pair<hipStream_t, hipEvent_t> w{o.s, *d};
+      if (std::find(waited.begin(), waited.end(), w) == waited.end()) {
+        FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, *d, 0));
+        waited.push_back(w);
+      }
     }
     return FTAR_SUCCESS;
   }
