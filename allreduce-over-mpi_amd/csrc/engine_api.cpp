@@ -503,7 +503,9 @@ ftar_status_t run_group(const void* const* sendbufs, void* const* recvbufs, size
     st[r] = host ? ftar_allreduce_host(sb, recvbufs[r], count, dtype, op, topo, comms[r], s)
                  : ftar::allreduce(sb, recvbufs[r], count, dtype, op, topo, comms[r], s);
     if (capturing) comms[r]->tp->capture_leave();
-    if (!capturing && st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
+    // device buffers: the call returns once every rank's work is enqueued on its stream (stream order, as
+    // ftar_allreduce and RCCL's group calls); host buffers: once they hold the result
+    if (host && !capturing && st[r] == FTAR_SUCCESS && hipSetDevice(comms[r]->device) == hipSuccess &&
         hipStreamSynchronize(s) != hipSuccess)
       st[r] = FTAR_ERR_HIP;
     if (st[r] != FTAR_SUCCESS) why[r] = ftar::last_error();  // the error text is per thread

@@ -775,7 +775,8 @@ class LocalGroup:
 
     def allreduce(self, sendbufs, recvbufs, count, dtype="f32", op="sum", topo_=None, lonely=0, streams=None,
                   host=False):
-        """Every rank at once; host=True: the buffers are host memory (ftar_allreduce_host_group)."""
+        """Every rank at once, enqueued on each rank's stream (None: the NULL stream), returning once enqueued;
+        host=True: the buffers are host memory (ftar_allreduce_host_group), returning once they hold the result."""
         P = len(self.comms)
         t = None if topo_ is None else ctypes.byref(topo(topo_, lonely))
         sb = None if sendbufs is None else (_vp * P)(*[_ptr(x) for x in sendbufs])

@@ -445,8 +445,8 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
                 if ok else "MISMATCH", "whole_blocks": whole, "peer_read_registered": peer,
                 "note": "HBM bytes from the plans: every received block one device copy (read + write), every "
                         "fold k sources + 1 destination; all 8 ranks' copies and folds share this GPU's HBM. "
-                        "ms = events around the group call, which returns once every rank's stream drained "
-                        "(its host threads' start and join included)"}
+                        "ms = events around the group call on the ranks' stream (the call returns once every "
+                        "rank's work is enqueued; the enqueue itself is inside the events)"}
     finally:
         g.destroy()
 

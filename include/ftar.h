@@ -359,7 +359,11 @@ ftar_status_t ftar_comm_deregister(ftar_comm_t comm, int reg);
 ftar_status_t ftar_allreduce(const void* sendbuf, void* recvbuf, size_t count, ftar_dtype_t dtype, ftar_op_t op,
                              const ftar_topo_t* topo, ftar_comm_t comm, void* stream);
 /* Drive every rank of an ftar_comm_init_local group from this one call
- * (one internal host thread per rank); blocks until all ranks are done.
+ * (pooled host threads, one per rank at once); returns once every rank's
+ * work is enqueued on its stream (streams == NULL: each device's NULL
+ * stream), like ftar_allreduce -- synchronize the streams before reading
+ * the results from the host.  ftar_allreduce_host_group returns once the
+ * host buffers hold the result.
  * Under stream capture pass the capture stream itself for every rank (the
  * call is then captured serially, one graph chain); streams forked per rank
  * from the capture are refused with FTAR_ERR_UNSUPPORTED, as HIP's

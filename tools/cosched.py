@@ -55,7 +55,8 @@ for chunk in [int(c) for c in a.chunks.split(",")]:
         ts = []
         for _ in range(a.iters):
             t0 = time.perf_counter()
-            g.allreduce(xs, ys, n, "f32", "sum", topo_=topo)   # the group call synchronises every rank's stream
+            g.allreduce(xs, ys, n, "f32", "sum", topo_=topo)
+            torch.cuda.synchronize()   # the group call returns once enqueued
             ts.append((time.perf_counter() - t0) * 1e3)
         print(json.dumps({"ranks": P, "topo": topo, "elements": n, "chunk_bytes": chunk,
                           "reduce_cus": cus or "all", "ms_best": round(min(ts), 3),

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Wall time of the in-process group call (ftar_allreduce_group) on one GPU, small buckets to large: P ranks
-on cuda:0, tree(P) direct, fp32, the call returning once every rank's stream drained.  At small buckets this
-is the host path itself -- the ranks' threads, the transport's rendezvous, the event plumbing.
+on cuda:0, tree(P) direct, fp32, from the call to its completion (torch.cuda.synchronize after it), and to the
+call's return (it returns once enqueued).  At small buckets this is the host path itself -- the ranks' threads,
+the transport's rendezvous, the event plumbing.
 
     python3 tools/group_latency.py [--ranks 8] [--calls 200]      # FTAR_LIB=<other libftar.so> for an A/B
 """
@@ -36,17 +37,22 @@ def main():
             calls = a.calls if nbytes <= (4 << 20) else max(10, a.calls // 10)
             for _ in range(5):
                 g.allreduce(xs, ys, n, "f32", "sum", topo_=str(a.ranks), streams=streams)
-            per = []
+            per, enq = [], []
+            torch.cuda.synchronize()
             for _ in range(calls):
                 t0 = time.perf_counter()
                 g.allreduce(xs, ys, n, "f32", "sum", topo_=str(a.ranks), streams=streams)
+                enq.append(time.perf_counter() - t0)
+                torch.cuda.synchronize()   # the group call returns once enqueued (since round 5)
                 per.append(time.perf_counter() - t0)
+            enq.sort()
             want = a.ranks * (a.ranks + 1) / 2
             ok = all(bool((y == want).all()) for y in ys)
             per.sort()
             out["rows"].append({"bytes": nbytes, "calls": calls, "us_median": round(per[len(per) // 2] * 1e6, 1),
                                 "us_p10": round(per[len(per) // 10] * 1e6, 1),
-                                "us_p90": round(per[9 * len(per) // 10] * 1e6, 1), "check": ok})
+                                "us_p90": round(per[9 * len(per) // 10] * 1e6, 1),
+                                "us_enqueue_median": round(enq[len(enq) // 2] * 1e6, 1), "check": ok})
             del xs, ys
     finally:
         g.destroy()
