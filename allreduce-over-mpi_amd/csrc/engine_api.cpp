@@ -443,7 +443,8 @@ class RankPool {
     Latch* done;
   };
   // a worker is started for a job already counted against it, and counts itself free again only once
-  // its job has returned: so every queued job has a worker that is not busy with anything else
+  // its job has returned: so every queued job has a worker that is not busy with anything else.  It
+  // counts itself free before it reports the job done, so the caller's next call finds it free.
   void work() {
     for (;;) {
       Job j;
@@ -455,11 +456,11 @@ class RankPool {
       }
       (*j.fn)(j.rank);
       {
-        std::lock_guard<std::mutex> g(j.done->mu);
-        if (--j.done->left == 0) j.done->cv.notify_all();
+        std::lock_guard<std::mutex> g(mu_);
+        ++free_;
       }
-      std::lock_guard<std::mutex> g(mu_);
-      ++free_;
+      std::lock_guard<std::mutex> g(j.done->mu);
+      if (--j.done->left == 0) j.done->cv.notify_all();
     }
   }
   const pid_t pid_ = getpid();
