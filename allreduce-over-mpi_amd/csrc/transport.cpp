@@ -749,6 +749,28 @@ class LocalTransport final : public Transport {
     std::vector<std::pair<hipStream_t, Ev>> done;
     std::vector<std::pair<std::shared_ptr<LocalHub::Posted>, hipStream_t>> got;
     std::vector<std::pair<hipStream_t, hipEvent_t>> waited;  // (stream, event) already waited on
+    // hand every message taken so far back to its sender: with its stream's copies-done event, or none if
+    // this rank failed (the sender then fails too, at once, instead of waiting out the timeout)
+    auto publish = [&](ftar_status_t st) -> ftar_status_t {
+      for (auto& x : got) {
+        Ev* e = per_stream(done, x.second);
+        if (st != FTAR_SUCCESS || *e) continue;
+        st = hub_->take_shared(e);
+        if (st == FTAR_SUCCESS && hipEventRecord(**e, x.second) != hipSuccess) {
+          set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
+          st = FTAR_ERR_HIP;
+        }
+      }
+      {
+        std::lock_guard<std::mutex> g(hub_->mu);
+        for (auto& x : got) {
+          if (st == FTAR_SUCCESS) x.first->done = *per_stream(done, x.second);
+          x.first->taken = true;
+        }
+      }
+      for (auto& x : got) hub_->notify(x.first->sender);
+      return st;
+    };
     for (auto& o : ops) {
       if (o.is_send) continue;
       std::shared_ptr<LocalHub::Posted> p;
@@ -756,19 +778,24 @@ class LocalTransport final : public Transport {
         std::unique_lock<std::mutex> g(hub_->mu);
         auto& q = hub_->wire[{o.peer, rank_}];
         if (!hub_->wait(g, rank_, [&] { return !q.empty(); })) {
+          g.unlock();
           set_error("local transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
-          return FTAR_ERR_TIMEOUT;
+          return publish(FTAR_ERR_TIMEOUT);
         }
         p = q.front();
         q.pop_front();
       }
+      got.emplace_back(p, o.s);
       if (p->bytes != o.bytes) {
         set_error("local transport: message size mismatch", __FILE__, __LINE__);
-        return FTAR_ERR_INTERNAL;
+        return publish(FTAR_ERR_INTERNAL);
       }
       const std::pair<hipStream_t, hipEvent_t> w{o.s, *p->ready};
       if (std::find(waited.begin(), waited.end(), w) == waited.end()) {
-        FTAR_CHECK_HIP(hipStreamWaitEvent(o.s, *p->ready, 0));
+        if (hipStreamWaitEvent(o.s, *p->ready, 0) != hipSuccess) {
+          set_error("local transport: hipStreamWaitEvent failed", __FILE__, __LINE__);
+          return publish(FTAR_ERR_HIP);
+        }
         waited.push_back(w);
       }
       // A receive from a rank on this device is ftar's own copy kernel, one launch per receive (launch_copy:
@@ -781,27 +808,15 @@ class LocalTransport final : public Transport {
         const char* e = getenv("FTAR_LOCAL_COPY");
         return !(e && !strcmp(e, "runtime"));
       }();
-      if (o.bytes && kernel_copy && p->device == dev) FTAR_RETURN_IF(launch_copy(p->buf, o.buf, o.bytes, o.s));
-      else if (o.bytes) FTAR_CHECK_HIP(hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s));
-      got.emplace_back(std::move(p), o.s);
-    }
-    for (auto& x : got) {
-      Ev* e = per_stream(done, x.second);
-      if (*e) continue;
-      FTAR_RETURN_IF(hub_->take_shared(e));
-      if (hipEventRecord(**e, x.second) != hipSuccess) {
-        set_error("local transport: hipEventRecord failed", __FILE__, __LINE__);
-        return FTAR_ERR_HIP;
+      ftar_status_t cst = FTAR_SUCCESS;
+      if (o.bytes && kernel_copy && p->device == dev) cst = launch_copy(p->buf, o.buf, o.bytes, o.s);
+      else if (o.bytes && hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s) != hipSuccess) {
+        set_error("local transport: hipMemcpyAsync failed", __FILE__, __LINE__);
+        cst = FTAR_ERR_HIP;
       }
+      if (cst != FTAR_SUCCESS) return publish(cst);
     }
-    {
-      std::lock_guard<std::mutex> g(hub_->mu);
-      for (auto& x : got) {
-        x.first->done = *per_stream(done, x.second);
-        x.first->taken = true;
-      }
-    }
-    for (auto& x : got) hub_->notify(x.first->sender);
+    FTAR_RETURN_IF(publish(FTAR_SUCCESS));
     // 3. the sender's stream may not move on (and overwrite the source) before the copy
     waited.clear();
     size_t i = 0;
@@ -817,6 +832,10 @@ class LocalTransport final : public Transport {
           return FTAR_ERR_TIMEOUT;
         }
         d = p->done;
+      }
+      if (!d) {
+        set_error("local transport: rank " + std::to_string(o.peer) + " failed to receive", __FILE__, __LINE__);
+        return FTAR_ERR_INTERNAL;
       }
       const std::pair<hipStream_t, hipEvent_t> w{o.s, *d};
       if (std::find(waited.begin(), waited.end(), w) == waited.end()) {
