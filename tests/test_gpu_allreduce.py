@@ -708,3 +708,40 @@ def test_random_soak_host_buffers(seed):
         for r in range(c["P"]):
             assert outs[r].tobytes() == c["ref"][r].tobytes(), (c["P"], c["topo"], c["lonely"], c["n"], c["dtype"],
                                                                 form, chunk, pinned, r)
+
+
+def test_local_transport_size_mismatch_fails_both_ranks_at_once():
+    """Two in-process ranks called with different counts (a caller error): each receive finds a message of
+    the wrong size, hands it back to its sender as failed, and both calls fail within seconds rather than
+    one of them waiting out the transport's 120 s timeout."""
+    import threading
+    import time
+
+    import torch
+    import ftar
+    g = ftar.Comm.init_local(2)
+    try:
+        g.set_form("direct")
+        g.set_chunk_bytes(1 << 30)   # one piece per block on both ranks, whatever the count
+        n = 1 << 12
+        bufs = [torch.ones(n * (r + 1), device="cuda") for r in range(2)]
+        errs = [None, None]
+
+        def run(r):
+            try:
+                g[r].allreduce(None, bufs[r], n * (r + 1), "f32", "sum", topo_="2")
+            except ftar.FtarError as e:
+                errs[r] = e
+        t0 = time.time()
+        th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not any(t.is_alive() for t in th)
+        assert time.time() - t0 < 30, time.time() - t0
+        assert all(e is not None for e in errs), errs
+        assert any("size mismatch" in str(e) for e in errs), errs
+        torch.cuda.synchronize()
+    finally:
+        g.destroy()
