@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--sweep", action="store_true", help="N=1: also report k=1..16 (vector_add.cu:182)")
     ap.add_argument("--no-engine-local", action="store_true",
                     help="N=1: skip the engine_local line item (P = 8 in-process ranks on this GPU at the C4 bucket)")
+    ap.add_argument("--no-host-local", action="store_true",
+                    help="N=1: skip the host_local line item (P = 2 in-process ranks, pinned host buckets of C3)")
     ap.add_argument("--save-cost", default="",
                     help="N>1: write the execution model's constants re-fitted on this node to this calibration "
                          "file (rank 0; load it with FTAR_COST_FILE so every later MPI_Allreduce_FT prices with them)")
@@ -314,6 +316,12 @@ def bench_single(a):
             res["engine_local"] = engine_local(steps=5, warmup=2)
         except Exception as e:   # a line item: its failure must not cost the headline
             res["engine_local"] = {"error": str(e)[:300]}
+    if not a.no_host_local:
+        torch.cuda.empty_cache()
+        try:
+            res["host_local"] = host_local()
+        except Exception as e:   # a line item: its failure must not cost the headline
+            res["host_local"] = {"error": str(e)[:300]}
     if not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(k, n, a.cpu_seconds)
     print(json.dumps(res), flush=True)
@@ -447,6 +455,56 @@ def engine_local(steps=5, warmup=2, world=8, n=1 << 28, topo="8", chunk_bytes=No
                         "fold k sources + 1 destination; all 8 ranks' copies and folds share this GPU's HBM. "
                         "ms = events around the group call on the ranks' stream (the call returns once every "
                         "rank's work is enqueued; the enqueue itself is inside the events)"}
+    finally:
+        g.destroy()
+
+
+def host_local(steps=10, warmup=1, world=2, n=1 << 26, topo="2"):
+    """The reference's own setting on this one GPU (MPI_Allreduce_FT on host buffers,
+    mpi_mod.hpp:1723-1778, benchmark.cpp:125-131): P = 2 in-process ranks, a pinned host bucket each (the C3
+    bucket, 2^26 fp32 = 256 MiB), ftar_allreduce_host_group -- H2D, the exchange and D2H pipelined per piece,
+    the path MPI_Allreduce_FT takes.  Both ranks' copies share this GPU's one PCIe link (on a node each rank
+    has its own).  The call returns once the host buckets hold the result: wall time.  Checked bit-identical
+    to the device path on the same inputs."""
+    import torch
+
+    import ftar
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0xC3)
+    xd = [torch.rand(n, device=dev, generator=gen) * 2 - 1 for _ in range(world)]
+    hx = [x.cpu().pin_memory() for x in xd]
+    hy = [torch.empty_like(h).pin_memory() for h in hx]
+    g = ftar.Comm.init_local(world)
+    try:
+        g.set_form("direct")
+
+        def call():
+            g.allreduce(hx, hy, n, "f32", "sum", topo_=topo, host=True)
+        for _ in range(warmup):
+            call()
+        per = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            call()
+            per.append((time.perf_counter() - t0) * 1e3)
+        ms = sorted(per)[len(per) // 2]
+        best = min(per)
+        yd = [torch.empty_like(x) for x in xd]
+        g.allreduce(xd, yd, n, "f32", "sum", topo_=topo)   # the device path, same inputs and plan
+        torch.cuda.synchronize()
+        same = all(torch.equal(hy[r], yd[r].cpu()) for r in range(world))
+        bucket = n * 4
+        return {"workload": f"P = {world} in-process ranks on one MI355X, pinned host buckets of 2^26 fp32 "
+                            f"(C3), tree({topo}) direct, ftar_allreduce_host_group (the MPI_Allreduce_FT path)",
+                "ranks": world, "elements_per_rank": n, "ms_median": round(ms, 3), "ms_best": round(best, 3),
+                "ms_all": [round(x, 3) for x in per],
+                "algbw_GBps_per_rank": round(bucket / (ms * 1e-3) / 1e9, 2),
+                "algbw_GBps_per_rank_best": round(bucket / (best * 1e-3) / 1e9, 2),
+                "pcie_GBps_both_directions": round(2 * world * bucket / (ms * 1e-3) / 1e9, 2),
+                "check": "bit-identical to the device path" if same else "MISMATCH",
+                "note": "both ranks' H2D and D2H share this GPU's one PCIe link (57 GB/s per direction alone, "
+                        "48.6 each with both at once, DESIGN §6); with one rank per GPU each has its own"}
     finally:
         g.destroy()
 
