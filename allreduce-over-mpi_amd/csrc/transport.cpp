@@ -594,6 +594,17 @@ struct LocalHub {
     std::vector<std::shared_ptr<hipEvent_t>> ev;
   };
   void notify(int rank) { rcv[rank].notify_all(); }
+  // whether kernels on device `dev` may read device `peer`'s memory (ftar_comm_init_local enables peer
+  // access between every pair that supports it), cached per pair
+  bool can_reach(int dev, int peer) {
+    std::lock_guard<std::mutex> g(pool_mu);
+    auto it = reach.find({dev, peer});
+    if (it != reach.end()) return it->second;
+    int can = 0;
+    const bool ok = hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can;
+    reach[{dev, peer}] = ok;
+    return ok;
+  }
   explicit LocalHub(int n) : nranks(n), rcv(new std::condition_variable[n]), pending(std::make_shared<Round>()) {
     pending->ptr.resize(n);
     pending->ev.resize(n);
@@ -631,6 +642,7 @@ struct LocalHub {
   std::mutex issue;  // capture of the group: one issuing thread at a time
   std::mutex pool_mu;
   std::vector<hipEvent_t> pool, retired;
+  std::map<std::pair<int, int>, bool> reach;  // can_reach, under pool_mu
 };
 
 std::shared_ptr<LocalHub> make_local_hub(int nranks) { return std::make_shared<LocalHub>(nranks); }
@@ -749,6 +761,14 @@ class LocalTransport final : public Transport {
     std::vector<std::pair<hipStream_t, Ev>> done;
     std::vector<std::pair<std::shared_ptr<LocalHub::Posted>, hipStream_t>> got;
     std::vector<std::pair<hipStream_t, hipEvent_t>> waited;  // (stream, event) already waited on
+    std::vector<std::pair<hipStream_t, std::vector<Segment>>> gathers;  // batched receives per stream
+    auto per_stream_segs = [&](std::vector<std::pair<hipStream_t, std::vector<Segment>>>& v,
+                               hipStream_t st) -> std::vector<Segment>* {
+      for (auto& x : v)
+        if (x.first == st) return &x.second;
+      v.emplace_back(st, std::vector<Segment>());
+      return &v.back().second;
+    };
     // hand every message taken so far back to its sender: with its stream's copies-done event, or none if
     // this rank failed (the sender then fails too, at once, instead of waiting out the timeout)
     auto publish = [&](ftar_status_t st) -> ftar_status_t {
@@ -801,21 +821,35 @@ class LocalTransport final : public Transport {
       // A receive from a rank on this device is ftar's own copy kernel, one launch per receive (launch_copy:
       // the LDS-staged copy when co-aligned): 5-6 % faster than the runtime's blit at the C4 bucket with 8
       // ranks on one GPU (profiles/r05/engine_local/ab2_*, 3 interleaved rounds); one launch per piece group
-      // instead lost 2 % (it filled the GPU, and the folds stopped overlapping the copies).  A receive from
-      // another device keeps the runtime's copy (peer access may be off).  FTAR_LOCAL_COPY=runtime: the
-      // runtime's copy for every receive (the A/B).
-      static const bool kernel_copy = [] {
+      // instead lost 2 % (it filled the GPU, and the folds stopped overlapping the copies).  The receives
+      // from other devices this device can reach go into one multi-segment copy per stream, launched once
+      // every one of them is waited for: its workgroups interleave the segments, so every peer's link
+      // streams at once (one runtime copy after another would use one link at a time); without peer access
+      // the runtime copies.  FTAR_LOCAL_COPY=runtime: the runtime's copy for every receive; =gather: the
+      // multi-segment copy for every receive, same device included (the A/Bs, and the test of that path on
+      // a one-GPU box).
+      static const int copy_mode = [] {
         const char* e = getenv("FTAR_LOCAL_COPY");
-        return !(e && !strcmp(e, "runtime"));
+        return e && !strcmp(e, "runtime") ? 0 : e && !strcmp(e, "gather") ? 2 : 1;
       }();
       ftar_status_t cst = FTAR_SUCCESS;
-      if (o.bytes && kernel_copy && p->device == dev) cst = launch_copy(p->buf, o.buf, o.bytes, o.s);
-      else if (o.bytes && hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s) != hipSuccess) {
+      if (!o.bytes) {
+      } else if (copy_mode == 2 || (copy_mode == 1 && p->device != dev && hub_->can_reach(dev, p->device))) {
+        per_stream_segs(gathers, o.s)->push_back({p->buf, o.buf, o.bytes});
+      } else if (copy_mode == 1 && p->device == dev) {
+        cst = launch_copy(p->buf, o.buf, o.bytes, o.s);
+      } else if (hipMemcpyAsync(o.buf, p->buf, o.bytes, hipMemcpyDeviceToDevice, o.s) != hipSuccess) {
         set_error("local transport: hipMemcpyAsync failed", __FILE__, __LINE__);
         cst = FTAR_ERR_HIP;
       }
       if (cst != FTAR_SUCCESS) return publish(cst);
     }
+    for (auto& g : gathers)
+      for (size_t i = 0; i < g.second.size(); i += FTAR_MAX_K) {
+        const int m = (int)std::min<size_t>(FTAR_MAX_K, g.second.size() - i);
+        const ftar_status_t gst = launch_gather(g.second.data() + i, m, g.first);
+        if (gst != FTAR_SUCCESS) return publish(gst);
+      }
     FTAR_RETURN_IF(publish(FTAR_SUCCESS));
     // 3. the sender's stream may not move on (and overwrite the source) before the copy
     waited.clear();

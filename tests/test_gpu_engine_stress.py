@@ -16,8 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "allreduce-over-mpi_amd", "lib", "ftar_engine_stress")
 
 
-def _run(args, timeout):
-    env = dict(os.environ, NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+def _run(args, timeout, **extra_env):
+    env = dict(os.environ, NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", **extra_env)
     p = subprocess.run([EXE] + [str(a) for a in args], capture_output=True, text=True, timeout=timeout, env=env)
     return p
 
@@ -28,6 +28,16 @@ def test_in_process_groups(calls):
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
     stats = json.loads(p.stdout.strip().splitlines()[-1])
     assert stats["checked"] == stats["calls"] >= calls and stats["groups"] >= 3 and stats["captured"] > 0, stats
+
+
+def test_in_process_groups_multi_segment_receives():
+    """The in-process transport's batched receive (one multi-segment copy per stream and flush: the path
+    receives from other devices take on a multi-GPU box) on every receive, forced by FTAR_LOCAL_COPY=gather
+    on this one-GPU box: the same random calls, every result checked, captures included."""
+    p = _run([120, 7], 240, FTAR_LOCAL_COPY="gather")
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    stats = json.loads(p.stdout.strip().splitlines()[-1])
+    assert stats["checked"] == stats["calls"] >= 120 and stats["captured"] > 0, stats
 
 
 @pytest.mark.parametrize("mode,P,calls,seed", [pytest.param("rccl", 4, 40, 41, marks=pytest.mark.wide), ("rccl", 8, 10, 12),
