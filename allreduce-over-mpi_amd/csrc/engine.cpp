@@ -795,10 +795,16 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   FTAR_CHECK_HIP(hipStreamWaitEvent(c->red_s, ev[0], 0));
   c->nmarks = 0;
   FTAR_RETURN_IF(mark(c, "start", c->comm_s));
-  if (host) {  // all pieces in, in order, on their own stream (the DMA engines run ahead)
-    FTAR_CHECK_HIP(hipStreamWaitEvent(c->h2d_s, ev[0], 0));
-    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev[0], 0));
-    for (size_t k = 0; k < nchunks; ++k) {
+  // Host mode: the pieces go in, in order, on their own stream, issued kHostLookahead pieces ahead of the
+  // steps that read them rather than all up front.  The copy stream then runs ahead of the exchange by
+  // that many pieces either way, and a stream that shares its hardware queue with it (8 streams of two
+  // in-process ranks on HIP's 4 queues, or a caller's own streams) waits behind those few pieces, not
+  // behind the whole bucket: with every piece issued first, two ranks on one GPU started the exchange only
+  // once the last piece was in, and H2D and D2H never overlapped (profiles/r05/host_local/).
+  size_t h2d_issued = 0;
+  auto issue_h2d = [&](size_t upto) -> ftar_status_t {  // pieces [h2d_issued, upto] of every block
+    for (; h2d_issued <= upto && h2d_issued < nchunks; ++h2d_issued) {
+      const size_t k = h2d_issued;
       FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
         FTAR_CHECK_HIP(hipMemcpyAsync(bufs[BUF_DST] + lo * esz, host->src + lo * esz, n * esz,
                                       hipMemcpyHostToDevice, c->h2d_s));
@@ -806,6 +812,12 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
       }));
       FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
     }
+    return FTAR_SUCCESS;
+  };
+  if (host) {
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->h2d_s, ev[0], 0));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev[0], 0));
+    FTAR_RETURN_IF(issue_h2d(kHostLookahead));
   }
   std::vector<char> comm_has_input(host ? nchunks : 0), red_has_input(host ? nchunks : 0);
   std::vector<const void*> srcs;
@@ -815,6 +827,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
   for (const auto& step : order) {
     const size_t s = step.first, k = step.second, lo = k * chunk;
     const Stage& st = plan.stages[s];
+    if (host) FTAR_RETURN_IF(issue_h2d(k + kHostLookahead));
     if (moves[s]) {
       if (host && !comm_has_input[k]) {
         FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k), 0));
@@ -871,6 +884,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
       }));
     }
   }
+  if (host) FTAR_RETURN_IF(issue_h2d(nchunks - 1));  // (every piece is read by a step; kept for safety)
   if (plan.allgather == FTAR_AG_COLLECTIVE) {  // the whole all-gather phase as one collective, in place
     const long last_red = nst ? (reduces[nst - 1] ? (long)nst - 1 : prev_red[nst - 1]) : -1;
     if (last_red >= 0) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_r((size_t)last_red, nchunks - 1), 0));

@@ -125,6 +125,8 @@ ftar_status_t refuse_growth_under_capture(const ftar_comm* c, const char* what);
 // ---- engine.cpp -----------------------------------------------------------------------------------------
 // Host mode piece per block: 0 = auto (auto_host_chunk)
 constexpr size_t kDefaultHostChunkBytes = 0;
+// host mode (p2p transports): H2D pieces issued ahead of the step that first reads them
+constexpr size_t kHostLookahead = 2;
 struct HostIO;
 // bring-up of a communicator whose transport is set (streams, settings from the environment; a
 // host-bootstrapped one agrees on them here), and its teardown (false: it must not be freed)
