@@ -11,7 +11,9 @@
 // the legacy NULL stream ("null", the caller stream of the engine stress driver): a blocking stream such as
 // the masked one also waits for it (and it for them) without sharing a queue, which the pairs show as well.
 //
-// Usage: queue_probe [--comms K] [--masked] [--prio] [--null]   (prints "SHARE <x> <y> yes|no" and a summary)
+// Usage: queue_probe [--comms K] [--masked] [--prio [N]] [--extra N] [--null]
+//   --prio N: N high-priority streams; --extra N: N plain streams created after the communicators (as the
+//   host path's H2D / D2H streams are, at the first host-buffer call).  Prints "SHARE <x> <y> yes|no" and a summary.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -50,12 +52,14 @@ __global__ void marker_kernel(int* out) { out[threadIdx.x] = 1; }
 
 int main(int argc, char** argv) {
   int ncomms = 1;
-  bool masked = false, prio = false, null_stream = false;
+  bool masked = false, null_stream = false;
+  int prio = 0, extra = 0;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "--comms" && i + 1 < argc) ncomms = atoi(argv[++i]);
     else if (a == "--masked") masked = true;
-    else if (a == "--prio") prio = true;
+    else if (a == "--prio") prio = (i + 1 < argc && argv[i + 1][0] != '-') ? atoi(argv[++i]) : 1;
+    else if (a == "--extra" && i + 1 < argc) extra = atoi(argv[++i]);
     else if (a == "--null") null_stream = true;
   }
   CHECK(hipSetDevice(0));
@@ -92,12 +96,17 @@ int main(int argc, char** argv) {
     CHECK(hipExtStreamCreateWithCUMask(&m, (uint32_t)mask.size(), mask.data()));
     st.emplace_back("masked_all", m);
   }
-  if (prio) {
+  for (int e = 0; e < extra; ++e) {
+    hipStream_t x;
+    CHECK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    st.emplace_back("extra" + std::to_string(e), x);
+  }
+  for (int e = 0; e < prio; ++e) {
     int lo = 0, hi = 0;
     CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     hipStream_t p;
     CHECK(hipStreamCreateWithPriority(&p, hipStreamNonBlocking, hi));
-    st.emplace_back("prio_high", p);
+    st.emplace_back(prio == 1 ? std::string("prio_high") : "prio_high" + std::to_string(e), p);
   }
 
   int* flag = nullptr;
