@@ -27,8 +27,9 @@ size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
 // Host buffers on a communicator without point-to-point transfers (ftar_comm_init_host: the MPI
 // drop-in's `ipc` transport), the read form piece by piece, as the p2p host path pipelines its
 // stages.  Piece k is elements [k*chunk, (k+1)*chunk) of every block.
-//   * every piece goes H2D straight into the exchange buffer X on its own stream, all issued up
-//     front, so the copy engines run ahead (no staging buffer, no copy-in pass);
+//   * every piece goes H2D straight into the exchange buffer X on its own stream, kHostPeerLookahead
+//     pieces ahead of the fold that needs it, so the copy engines run ahead while the host waits at
+//     the barriers (no staging buffer, no copy-in pass);
 //   * once every rank's piece k is in (a barrier), the fold of my block's piece k reads the peers'
 //     copies from their X over xGMI and writes my X in place (the plan's fold: same bits);
 //   * once every rank's fold of piece k is done (the next barrier, which also says piece k+1 is in
@@ -54,6 +55,40 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
   // so all of them leave the call at the same barrier instead of some waiting in the next.
   ftar_status_t st = grow_events(c, 5 + 2 * m);
+  hipEvent_t* ev = c->events.data();
+  auto ev_h = [&](size_t k) { return c->events[5 + 2 * k]; };      // piece k is in my X
+  auto ev_g = [&](size_t k) { return c->events[5 + 2 * k + 1]; };  // piece k is final in my X
+  auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {  // piece k of every block, clipped
+    for (size_t b = 0; b < P; ++b) {
+      const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
+      if (lo < end) FTAR_RETURN_IF(fn(lo, std::min(chunk, end - lo)));
+    }
+    return FTAR_SUCCESS;
+  };
+  // Order matters when the copy streams share a hardware queue with the comm stream (HIP's 4 queues
+  // per process): commands of a shared queue run in issue order, and a barrier waits for the
+  // comm stream.  So every H2D piece is issued after the fold commands of an earlier piece (never all
+  // up front: the first barrier then waited for the whole bucket), and the D2H of piece k after the
+  // fold of piece k + 1 (else that fold, and the barrier after it, waited for the D2H).
+  size_t h2d_issued = 0;
+  auto issue_h2d = [&](size_t upto) -> ftar_status_t {  // pieces [h2d_issued, upto]
+    for (; h2d_issued <= upto && h2d_issued < m; ++h2d_issued) {
+      const size_t k = h2d_issued;
+      FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
+        FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
+        return FTAR_SUCCESS;
+      }));
+      FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
+    }
+    return FTAR_SUCCESS;
+  };
+  auto issue_d2h = [&](size_t k) -> ftar_status_t {  // piece k of the whole bucket, once it is final here
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
+    return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+      FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+      return FTAR_SUCCESS;
+    });
+  };
   auto work = [&](auto&& fn) {
     if (st == FTAR_SUCCESS) st = fn();
   };
@@ -77,29 +112,13 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     }
     return all_ok;
   };
-  hipEvent_t* ev = c->events.data();
-  auto ev_h = [&](size_t k) { return c->events[5 + 2 * k]; };      // piece k is in my X
-  auto ev_g = [&](size_t k) { return c->events[5 + 2 * k + 1]; };  // piece k is final in my X
-  auto for_piece = [&](size_t k, auto&& fn) -> ftar_status_t {  // piece k of every block, clipped
-    for (size_t b = 0; b < P; ++b) {
-      const size_t lo = b * split + k * chunk, end = std::min(count, (b + 1) * split);
-      if (lo < end) FTAR_RETURN_IF(fn(lo, std::min(chunk, end - lo)));
-    }
-    return FTAR_SUCCESS;
-  };
   work([&]() -> ftar_status_t {
     ev = c->events.data();
     FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
     for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
     c->nmarks = 0;
     FTAR_RETURN_IF(mark(c, "start", c->comm_s));
-    for (size_t k = 0; k < m; ++k) {
-      FTAR_RETURN_IF(for_piece(k, [&](size_t lo, size_t n) -> ftar_status_t {
-        FTAR_CHECK_HIP(hipMemcpyAsync(X + lo * esz, io.src + lo * esz, n * esz, hipMemcpyHostToDevice, c->h2d_s));
-        return FTAR_SUCCESS;
-      }));
-      FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
-    }
+    FTAR_RETURN_IF(issue_h2d(kHostPeerLookahead));
     FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
     return FTAR_SUCCESS;
   });
@@ -114,6 +133,8 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
             r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
             [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
       if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
+      FTAR_RETURN_IF(issue_h2d(k + 1 + kHostPeerLookahead));  // after this fold's commands (see above)
+      if (k > 0) FTAR_RETURN_IF(issue_d2h(k - 1));            // likewise
       return FTAR_SUCCESS;
     });
     if (!sync()) return leave();  // piece k folded everywhere (and piece k+1 in)
@@ -125,12 +146,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
               {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
       if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
       FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
-      FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
-      return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
-        FTAR_CHECK_HIP(
-            hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
-        return FTAR_SUCCESS;
-      });
+      return k + 1 == m ? issue_d2h(k) : FTAR_SUCCESS;  // the others after the next fold
     });
   }
   work([&] { return mark(c, "pieces folded and gathered", c->comm_s); });

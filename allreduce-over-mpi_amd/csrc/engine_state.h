@@ -127,6 +127,9 @@ ftar_status_t refuse_growth_under_capture(const ftar_comm* c, const char* what);
 constexpr size_t kDefaultHostChunkBytes = 0;
 // host mode (p2p transports): H2D pieces issued ahead of the step that first reads them
 constexpr size_t kHostLookahead = 2;
+// host mode on a host-bootstrapped communicator (peer_allreduce_host): H2D pieces issued ahead of the fold
+// that reads them (the host waits at a barrier after every fold)
+constexpr size_t kHostPeerLookahead = 3;
 struct HostIO;
 // bring-up of a communicator whose transport is set (streams, settings from the environment; a
 // host-bootstrapped one agrees on them here), and its teardown (false: it must not be freed)
