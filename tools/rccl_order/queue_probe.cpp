@@ -11,7 +11,9 @@
 // the legacy NULL stream ("null", the caller stream of the engine stress driver): a blocking stream such as
 // the masked one also waits for it (and it for them) without sharing a queue, which the pairs show as well.
 //
-// Usage: queue_probe [--comms K] [--masked] [--prio [N]] [--extra N] [--null]
+// Usage: queue_probe [--comms K] [--masked] [--prio [N]] [--extra N] [--null] [--host-call] [--ipc]
+//   --host-call: one host-buffer call on each communicator first, so its H2D / D2H streams exist;
+//   --ipc: host-bootstrapped 1-rank communicators (the MPI drop-in's ipc transport) instead of RCCL ones.
 //   --prio N: N high-priority streams; --extra N: N plain streams created after the communicators (as the
 //   host path's H2D / D2H streams are, at the first host-buffer call).  Prints "SHARE <x> <y> yes|no" and a summary.
 #include <hip/hip_ext.h>
@@ -54,12 +56,15 @@ int main(int argc, char** argv) {
   int ncomms = 1;
   bool masked = false, null_stream = false;
   int prio = 0, extra = 0;
+  bool host_call = false, ipc = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "--comms" && i + 1 < argc) ncomms = atoi(argv[++i]);
     else if (a == "--masked") masked = true;
     else if (a == "--prio") prio = (i + 1 < argc && argv[i + 1][0] != '-') ? atoi(argv[++i]) : 1;
     else if (a == "--extra" && i + 1 < argc) extra = atoi(argv[++i]);
+    else if (a == "--host-call") host_call = true;
+    else if (a == "--ipc") ipc = true;
     else if (a == "--null") null_stream = true;
   }
   CHECK(hipSetDevice(0));
@@ -76,11 +81,26 @@ int main(int argc, char** argv) {
   for (int c = 0; c < ncomms; ++c) {
     ftar_unique_id_t id;
     ftar_comm_t comm = nullptr;
-    if (ftar_get_unique_id(&id) != FTAR_SUCCESS || ftar_comm_init_rank(&comm, 1, id, 0, 0) != FTAR_SUCCESS) {
+    auto one_rank_allgather = [](const void* mine, void* all, size_t bytes, void*) -> int {
+      memcpy(all, mine, bytes);
+      return 0;
+    };
+    const ftar_status_t made = ipc ? ftar_comm_init_host(&comm, 1, 0, 0, one_rank_allgather, nullptr)
+                                   : ftar_get_unique_id(&id) == FTAR_SUCCESS ? ftar_comm_init_rank(&comm, 1, id, 0, 0)
+                                                                             : FTAR_ERR_INTERNAL;
+    if (made != FTAR_SUCCESS) {
       fprintf(stderr, "communicator %d: %s\n", c, ftar_last_error());
       return 2;
     }
     comms.push_back(comm);
+    if (host_call) {  // creates the communicator's H2D / D2H streams
+      float hx = 1.f;
+      if (ftar_allreduce_host(nullptr, &hx, 1, FTAR_FLOAT32, FTAR_SUM, nullptr, comm, user) != FTAR_SUCCESS) {
+        fprintf(stderr, "host call %d: %s\n", c, ftar_last_error());
+        return 2;
+      }
+      CHECK(hipStreamSynchronize(user));
+    }
     void* s4[4] = {};
     ftar_debug_comm_streams(comm, s4);
     const char* names[4] = {"comm", "reduce", "h2d", "d2h"};
