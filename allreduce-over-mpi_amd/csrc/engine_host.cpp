@@ -51,6 +51,11 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   const size_t P = (size_t)c->nranks, split = plan.split;
   const size_t chunk = host_peer_piece(c, split, esz);
   const size_t m = std::max<size_t>(1, (split + chunk - 1) / chunk);
+  // The D2H pieces go on the reduce stream, which this path leaves idle (its folds and gathers run on
+  // the comm stream): on 4 hardware queues the H2D and D2H streams of a host-bootstrapped communicator
+  // share one queue (tools/rccl_order/queue_probe --ipc --host-call, profiles/r05/queues/), and copies
+  // on one queue run in issue order, so the two directions never overlapped.
+  hipStream_t d2h = c->red_s;
   // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
   // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
   // so all of them leave the call at the same barrier instead of some waiting in the next.
@@ -83,9 +88,9 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     return FTAR_SUCCESS;
   };
   auto issue_d2h = [&](size_t k) -> ftar_status_t {  // piece k of the whole bucket, once it is final here
-    FTAR_CHECK_HIP(hipStreamWaitEvent(c->d2h_s, ev_g(k), 0));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(d2h, ev_g(k), 0));
     return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
-      FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, c->d2h_s));
+      FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, d2h));
       return FTAR_SUCCESS;
     });
   };
@@ -95,7 +100,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // a failed call leaves only after its copies stopped touching the caller's host buffers: H2D reads of
   // io.src and D2H writes of io.dst may still be in flight on their streams
   auto leave = [&]() -> ftar_status_t {
-    for (hipStream_t s : {c->h2d_s, c->d2h_s, c->comm_s})
+    for (hipStream_t s : {c->h2d_s, d2h, c->comm_s})
       if (s) hip_ignore(hipStreamSynchronize(s));
     return st;
   };
@@ -115,7 +120,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   work([&]() -> ftar_status_t {
     ev = c->events.data();
     FTAR_CHECK_HIP(hipEventRecord(ev[0], stream));
-    for (hipStream_t s : {c->comm_s, c->h2d_s, c->d2h_s}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
+    for (hipStream_t s : {c->comm_s, c->h2d_s, d2h}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
     c->nmarks = 0;
     FTAR_RETURN_IF(mark(c, "start", c->comm_s));
     FTAR_RETURN_IF(issue_h2d(kHostPeerLookahead));
@@ -155,7 +160,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
-  FTAR_CHECK_HIP(hipEventRecord(ev[2], c->d2h_s));
+  FTAR_CHECK_HIP(hipEventRecord(ev[2], d2h));
   FTAR_CHECK_HIP(hipEventRecord(ev[3], c->h2d_s));
   for (int i = 1; i <= 3; ++i) FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[i], 0));
   return FTAR_SUCCESS;
