@@ -474,3 +474,19 @@ def test_mpi_drop_in_random_calls(tmp_path, transport, ranks, calls, seed):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     reports = [ln for ln in p.stdout.splitlines() if ln.startswith('{"rank"')]
     assert len(reports) == ranks and all(f'"checked": {calls}' in r for r in reports), p.stdout[-2000:]
+
+
+@pytest.mark.gpu
+@needs
+def test_harness_ipc_host_pipeline_beats_whole_bucket_copies(tmp_path):
+    """The MPI drop-in's ipc host path (2 MPI ranks on the box's GPU, host buffers of 2^26 fp32) overlaps
+    H2D, the exchange and D2H piece by piece; whole-bucket copies (FTAR_HOST_PEER_PIPELINE=0) do not.  When
+    its copy streams shared hardware queues the pipeline fell to the whole-bucket time (20.2 vs 20.5 ms,
+    DESIGN §6, profiles/r05/ipc_host/); since the fix it takes 14-16 ms.  A loose bound, min of 10 calls."""
+    def min_ms(pipe):
+        rc, out = run(2, ["--size", str(1 << 26), "--repeat", "10", "--warmup", "2", "--check"], tmp_path,
+                      {"FT_TOPO": "1", "FTAR_MPI_TRANSPORT": "ipc", "FTAR_HOST_PEER_PIPELINE": pipe})
+        assert rc == 0 and "(test passed)" in out, out[-2000:]
+        return float(re.search(r"min time: (\S+)", out).group(1)) * 1e3
+    whole, pipe = min_ms("0"), min_ms("1")
+    assert pipe < 0.9 * whole, (pipe, whole)
