@@ -4,7 +4,7 @@
 bucket in 16 MiB pieces (hipMemcpyAsync), all streams at once.  Per case, 10 repetitions: wall time and the
 rate per direction.  Cases: 1 or 2 ranks with both directions, 2 ranks with H2D only and D2H only.
 
-    python3 tools/copy_streams.py
+    python3 tools/copy_streams.py [--gate]     # --gate: each copy stream first waits on another stream's event
 """
 import json
 import time
@@ -23,9 +23,21 @@ def make(ranks):
             for _ in range(ranks)]
 
 
+GATE = {"on": False}   # --gate: every copy stream first waits for an event of another stream (as the host path's do)
+gate_stream = torch.cuda.Stream()
+
+
 def once(rs, h2d, d2h):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if GATE["on"]:
+        ev = torch.cuda.Event()
+        with torch.cuda.stream(gate_stream):
+            torch.cuda._sleep(1)
+            ev.record(gate_stream)
+        for r in rs:
+            r["sh"].wait_event(ev)
+            r["sd"].wait_event(ev)
     for i in range(0, N, PIECE):
         for r in rs:
             if h2d:
@@ -39,12 +51,14 @@ def once(rs, h2d, d2h):
 
 
 def main():
+    import sys
+    GATE["on"] = "--gate" in sys.argv
     for ranks, h2d, d2h in [(1, True, True), (2, True, True), (2, True, False), (2, False, True), (1, True, False)]:
         rs = make(ranks)
         once(rs, h2d, d2h)
         ms = [once(rs, h2d, d2h) for _ in range(10)]
         per_dir = ranks * TOTAL / (sorted(ms)[5] * 1e-3) / 1e9
-        print(json.dumps({"ranks": ranks, "h2d": h2d, "d2h": d2h, "ms_all": [round(m, 2) for m in ms],
+        print(json.dumps({"gate": GATE["on"], "ranks": ranks, "h2d": h2d, "d2h": d2h, "ms_all": [round(m, 2) for m in ms],
                           "ms_median": round(sorted(ms)[5], 2),
                           "GBps_per_direction_median": round(per_dir, 1)}), flush=True)
         del rs
