@@ -1,0 +1,65 @@
+"""The trace analyser behind DESIGN §6's engine_local numbers (tools/engine_local_trace.py), on a small synthetic
+rocprofv3 kernel trace whose answers are known: calls split at the marker kernels, span / busy / idle, fold
+time overlapped by transfers, per-stream gaps, the lead from a marker's end to the call's first kernel, and
+the HBM rate over the span."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "tools", "engine_local_trace.py")
+
+FOLD = "void ftar::(anonymous namespace)::reduce_lds_kernel<ftar::(anonymous namespace)::F32Sum, 8>(Srcs<8>)"
+COPY = "void ftar::(anonymous namespace)::reduce_lds_kernel<ftar::(anonymous namespace)::SwarSum<u>(Srcs<1>)"
+MARK = "void at::native::sleep_kernel(long)"
+
+
+def write_trace(path):
+    """Two calls.  Each: a marker ending 10 us before the call's first op; a copy on stream 1 (0-100 us after
+    the call start), a fold on stream 2 (50-150 us: half of it under the copy), a second copy on stream 1
+    (200-300 us: 50 us of idle device before it).  Times in ns."""
+    rows = []
+
+    def add(name, sid, s, e):
+        rows.append({"Kernel_Name": name, "Stream_Id": sid, "Start_Timestamp": s, "End_Timestamp": e})
+    for base in (1_000_000, 2_000_000):
+        add(MARK, 0, base - 20_000, base - 10_000)
+        add(COPY, 1, base, base + 100_000)
+        add(FOLD, 2, base + 50_000, base + 150_000)
+        add(COPY, 1, base + 200_000, base + 300_000)
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0]))
+        w.writeheader()
+        w.writerows(rows)
+
+
+def test_engine_local_trace_on_a_known_trace(tmp_path):
+    p = tmp_path / "k.csv"
+    write_trace(p)
+    out = subprocess.run([sys.executable, TOOL, str(p), "--calls", "2", "--keep", "2", "--hbm-bytes", "300000"],
+                         capture_output=True, text=True, check=True).stdout
+    d = json.loads(out)
+    assert d["calls_found"] == 2 and d["kept"] == 2 and d["markers"] == 2
+    for c in d["calls"]:
+        assert c["span_us"] == 300.0 and c["busy_us"] == 250.0 and c["idle_us"] == 50.0
+        assert c["fold_busy_us"] == 100.0 and c["transfer_busy_us"] == 200.0
+        assert c["fold_overlapped_by_transfers"] == 0.5        # 50 of the fold's 100 us under the first copy
+        assert c["ops"] == 3 and c["fold_ops"] == 1 and c["lead_us"] == 10.0
+        assert c["hbm_GBps_over_span"] == 1.0                   # 300,000 B over 300 us
+        by = {s["stream"]: s for s in c["streams"]}
+        assert by["1"]["gaps_us"] == [100.0] and by["2"]["folds"] == 1
+    assert d["median_idle_us"] == 50.0 and d["median_fold_overlap"] == 0.5
+
+
+def test_scale_report_on_the_rehearsed_n8_line():
+    """tools/scale_report.py, which reads the driver's N > 1 lines, on the P = 8 line rehearsed over RCCL
+    loopback on round 5's final tree (profiles/r05/loopback_final/dist8.json): every section it prints."""
+    line = os.path.join(ROOT, "profiles", "r05", "loopback_final", "dist8.json")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale_report.py"), line],
+                         capture_output=True, text=True, check=True).stdout
+    for needle in ("== N=8:", "rccl_p2p_best:", "c4_ring direct (gather + ring-order fold)", "<- judged",
+                   "xGMI probe", "cost model refit", "unidentified", "C5 bf16:", "a tie of 6 broken by stages",
+                   "host e2e:", "bit-identical to the device path", "stages (s):"):
+        assert needle in out, (needle, out[:3000])
