@@ -37,7 +37,9 @@ namespace ftar {
 namespace {
 std::mutex g_cost_mu;
 ftar_cost_params_t g_set{};   // fields <= 0: default
-ftar_cost_params_t g_file{};  // constants loaded from a calibration file (ftar_cost_load / FTAR_COST_FILE)
+ftar_cost_params_t g_loaded{};   // constants from ftar_cost_load
+ftar_cost_params_t g_envfile{};  // constants from the file FTAR_COST_FILE names (kept apart: clearing the
+                                 // variable drops these and leaves an explicit load in effect)
 std::atomic<uint64_t> g_generation{0};  // bumped by every set: communicators re-decide their cached choices
 
 // MI355X defaults, used where no run on the node has fitted them (bench.py at N > 1 does):
@@ -103,8 +105,10 @@ ftar_status_t parse_cost_file(const char* path, ftar_cost_params_t* out) {
   return st;
 }
 
-// FTAR_COST_FILE: loaded at the first use of the model constants after it changes (a bad file leaves the
-// constants as they were and fails the next communicator bring-up, cost_file_status)
+// FTAR_COST_FILE: read at the first use of the model constants after the variable changes.  A file that
+// parses replaces the previous file's constants; one that does not leaves them as they were (it is parsed
+// into a temporary) and fails the next communicator bring-up (cost_file_status); an unset variable drops
+// the file's constants and leaves ftar_cost_load's in effect.
 std::string g_file_path;
 ftar_status_t g_file_status = FTAR_SUCCESS;
 std::string g_file_error;
@@ -114,11 +118,12 @@ void sync_cost_file() {  // under g_cost_mu
   if (path == g_file_path) return;
   g_file_path = path;
   g_file_status = FTAR_SUCCESS;
-  g_file = ftar_cost_params_t{};
-  if (!path.empty()) {
+  if (path.empty()) {
+    g_envfile = ftar_cost_params_t{};
+  } else {
     ftar_cost_params_t p;
     g_file_status = parse_cost_file(path.c_str(), &p);
-    if (g_file_status == FTAR_SUCCESS) g_file = p;
+    if (g_file_status == FTAR_SUCCESS) g_envfile = p;
     else g_file_error = last_error();
   }
   ++g_generation;
@@ -138,14 +143,16 @@ ftar_status_t cost_file_status() {
   return g_file_status;
 }
 
-// precedence: FTAR_COST_<FIELD> > ftar_cost_set > the calibration file > the defaults
+// precedence: FTAR_COST_<FIELD> > ftar_cost_set > FTAR_COST_FILE's file > ftar_cost_load's > the defaults
 CostParams cost_params() {
   ftar_cost_params_t p, fp;
   {
     std::lock_guard<std::mutex> g(g_cost_mu);
     sync_cost_file();
     p = g_set;
-    fp = g_file;
+    fp = g_loaded;
+    for (int i = 0; i < 9; ++i)
+      if (*field(&g_envfile, i) > 0) *field(&fp, i) = *field(&g_envfile, i);
   }
   auto pick = [](double set, double file, double def) { return set > 0 ? set : file > 0 ? file : def; };
   CostParams k;
@@ -421,12 +428,10 @@ ftar_status_t ftar_cost_set(const ftar_cost_params_t* p) {
 }
 
 ftar_status_t ftar_cost_load(const char* path) {
-  if (!path) return FTAR_ERR_INVALID_ARG;
-  ftar_cost_params_t p;
-  FTAR_RETURN_IF(ftar::parse_cost_file(path, &p));
+  ftar_cost_params_t p{};  // path == NULL: forget the loaded constants
+  if (path) FTAR_RETURN_IF(ftar::parse_cost_file(path, &p));
   std::lock_guard<std::mutex> g(ftar::g_cost_mu);
-  ftar::sync_cost_file();  // an FTAR_COST_FILE set later still replaces this (it is read when it changes)
-  ftar::g_file = p;
+  ftar::g_loaded = p;
   ++ftar::g_generation;
   return FTAR_SUCCESS;
 }

@@ -149,9 +149,21 @@ void set_form(ftar_comm* c, int form) {
 }
 
 // the host-buffer path's copy streams, created at the first host-buffer call (see comm_setup_local)
+// FTAR_DEBUG_HOST_COPY_PRIORITY=1 (diagnostic, tools/host_comm_stress.py): both at the highest priority,
+// which the runtime puts on hardware queues of their own -- the configuration of round 5's one
+// c4_host_read mismatch
 ftar_status_t ensure_host_streams(ftar_comm* c) {
-  if (!c->h2d_s) FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->h2d_s, hipStreamNonBlocking));
-  if (!c->d2h_s) FTAR_CHECK_HIP(hipStreamCreateWithFlags(&c->d2h_s, hipStreamNonBlocking));
+  static const bool prio = getenv("FTAR_DEBUG_HOST_COPY_PRIORITY") && atoi(getenv("FTAR_DEBUG_HOST_COPY_PRIORITY"));
+  for (hipStream_t* s : {&c->h2d_s, &c->d2h_s}) {
+    if (*s) continue;
+    if (prio) {
+      int least = 0, greatest = 0;
+      FTAR_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      FTAR_CHECK_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, greatest));
+    } else {
+      FTAR_CHECK_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    }
+  }
   return FTAR_SUCCESS;
 }
 

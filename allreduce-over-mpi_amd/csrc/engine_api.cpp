@@ -360,6 +360,20 @@ ftar_status_t ftar_debug_xgmi_probe_cap(ftar_comm_t comm, size_t bytes_per_peer,
   return ftar::xgmi_probe(comm, bytes_per_peer, iters, gbps, n, wg_per_peer);
 }
 
+// Test hook (not in ftar.h): rank `peer`'s exchange buffer as this process maps it (peer == own rank: its
+// own) and its size; null and 0 before the first peer-form call.  The full-size host-comm tests poison their
+// own buffer between cases and compare every rank's view of every mapping page by page.
+ftar_status_t ftar_debug_exchange_buffer(ftar_comm_t comm, int peer, void** ptr, size_t* bytes) {
+  if (!comm || !ptr || !bytes || peer < 0 || peer >= comm->nranks) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  *ptr = nullptr;
+  *bytes = 0;
+  if (!comm->xbuf || comm->xpeers.size() != (size_t)comm->nranks) return FTAR_SUCCESS;
+  *ptr = peer == comm->rank ? comm->xbuf : comm->xpeers[(size_t)peer];
+  *bytes = comm->xbuf_bytes;
+  return FTAR_SUCCESS;
+}
+
 ftar_status_t ftar_comm_set_reduce_cus(ftar_comm_t comm, int cus) {
   if (!comm) return FTAR_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> g(comm->mu);

@@ -55,7 +55,17 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // the comm stream): on 4 hardware queues the H2D and D2H streams of a host-bootstrapped communicator
   // share one queue (tools/rccl_order/queue_probe --ipc --host-call, profiles/r05/queues/), and copies
   // on one queue run in issue order, so the two directions never overlapped.
-  hipStream_t d2h = c->red_s;
+  // Diagnostics (tools/host_comm_stress.py): FTAR_DEBUG_HOST_D2H_STREAM=1 puts the D2H pieces back on the
+  // host D2H stream, FTAR_DEBUG_HOST_LOOKAHEAD=n issues the H2D pieces n ahead (large: all up front, as
+  // round 5's one c4_host_read mismatch ran)
+  static const bool d2h_own = getenv("FTAR_DEBUG_HOST_D2H_STREAM") && atoi(getenv("FTAR_DEBUG_HOST_D2H_STREAM"));
+  static const size_t lookahead =
+      getenv("FTAR_DEBUG_HOST_LOOKAHEAD") ? (size_t)atol(getenv("FTAR_DEBUG_HOST_LOOKAHEAD")) : kHostPeerLookahead;
+  hipStream_t d2h = d2h_own ? c->d2h_s : c->red_s;
+  // FTAR_DEBUG_HOST_GATHER_FENCE (diagnostic): 1 an empty kernel after each gather, before the event the D2H
+  // waits on; 2 the gather's workgroups end with a system-scope release; 3 the gather with temporal stores
+  static const int gather_fence =
+      getenv("FTAR_DEBUG_HOST_GATHER_FENCE") ? atoi(getenv("FTAR_DEBUG_HOST_GATHER_FENCE")) : 0;
   // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
   // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
   // so all of them leave the call at the same barrier instead of some waiting in the next.
@@ -123,7 +133,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     for (hipStream_t s : {c->comm_s, c->h2d_s, d2h}) FTAR_CHECK_HIP(hipStreamWaitEvent(s, ev[0], 0));
     c->nmarks = 0;
     FTAR_RETURN_IF(mark(c, "start", c->comm_s));
-    FTAR_RETURN_IF(issue_h2d(kHostPeerLookahead));
+    FTAR_RETURN_IF(issue_h2d(lookahead));
     FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(0), 0));
     return FTAR_SUCCESS;
   });
@@ -138,7 +148,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
             r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
             [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
       if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
-      FTAR_RETURN_IF(issue_h2d(k + 1 + kHostPeerLookahead));  // after this fold's commands (see above)
+      FTAR_RETURN_IF(issue_h2d(k + 1 + lookahead));  // after this fold's commands (see above)
       if (k > 0) FTAR_RETURN_IF(issue_d2h(k - 1));            // likewise
       return FTAR_SUCCESS;
     });
@@ -149,18 +159,32 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
         if (x.len > lo)
           segs.push_back(
               {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
-      if (!segs.empty()) FTAR_RETURN_IF(peer_copy(c, segs));
+      if (!segs.empty()) {
+        if (gather_fence == 2 || gather_fence == 3)
+          FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, gather_fence == 2 && c->peer_nt,
+                                       c->peer_wg_cap, gather_fence == 2));
+        else
+          FTAR_RETURN_IF(peer_copy(c, segs));
+        if (gather_fence == 1) FTAR_RETURN_IF(launch_noop(c->comm_s));
+      }
       FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
       return k + 1 == m ? issue_d2h(k) : FTAR_SUCCESS;  // the others after the next fold
     });
   }
-  work([&] { return mark(c, "pieces folded and gathered", c->comm_s); });
-  if (!sync()) return leave();  // no peer reads my X after the call
+  work([&]() -> ftar_status_t {
+    FTAR_RETURN_IF(mark(c, "pieces folded and gathered", c->comm_s));
+    // the last barrier also waits for my D2H pieces: after it nothing of this call reads my X, my own
+    // copies included, so a peer's next call may write into it at once (the write form scatters into
+    // the peers' X before its first barrier)
+    FTAR_CHECK_HIP(hipEventRecord(ev[2], d2h));
+    FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev[2], 0));
+    return FTAR_SUCCESS;
+  });
+  if (!sync()) return leave();  // no peer reads my X after the call, and my D2H is done
   if (st != FTAR_SUCCESS) return leave();
   FTAR_RETURN_IF(mark(c, "barrier", c->comm_s));
   FTAR_RETURN_IF(tp->before_join());
   FTAR_CHECK_HIP(hipEventRecord(ev[1], c->comm_s));
-  FTAR_CHECK_HIP(hipEventRecord(ev[2], d2h));
   FTAR_CHECK_HIP(hipEventRecord(ev[3], c->h2d_s));
   for (int i = 1; i <= 3; ++i) FTAR_CHECK_HIP(hipStreamWaitEvent(stream, ev[i], 0));
   return FTAR_SUCCESS;

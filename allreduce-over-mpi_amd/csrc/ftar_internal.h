@@ -172,9 +172,13 @@ struct Segment {
   size_t bytes;
 };
 // nt: nontemporal loads and stores (the default: cold copies, data not
-// re-read soon); false keeps both in the caches.
+// re-read soon); false keeps both in the caches.  release_system: every
+// workgroup ends with a system-scope release fence, so its stores are in
+// memory before it retires (the host path's gather -> D2H hand-off).
 ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true,
-                            size_t max_wg_per_seg = 0);
+                            size_t max_wg_per_seg = 0, bool release_system = false);
+// An empty kernel: a stream-order point after the kernel before it (diagnostics).
+ftar_status_t launch_noop(hipStream_t stream);
 // One local device copy (k = 1 reduces, the P = 1 AllReduce, the peer forms' local copy-in/out): the
 // LDS-staged kernel when source and destination share their 16-byte alignment, else the copy kernel.
 ftar_status_t launch_copy(const void* src, void* dst, size_t bytes, hipStream_t stream);  // 0: enough workgroups for one pass

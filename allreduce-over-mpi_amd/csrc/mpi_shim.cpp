@@ -238,14 +238,27 @@ int check_cost_file() {
   return last_rc;
 }
 
+// FTAR_REDUCE_CUS (a CU share for the reduce stream) is refused on RCCL communicators (ftar.h), so with a
+// transport that may be RCCL (rccl, or auto) it fails the call with MPI_ERR_ARG on every rank before the
+// bring-up -- else the RCCL communicator's init would fail and auto would take that for an RCCL failure and
+// switch every rank to ipc.  With FTAR_MPI_TRANSPORT=ipc the knob applies.
+int check_reduce_cus() {
+  const char* cus = getenv("FTAR_REDUCE_CUS");
+  if (!cus || !*cus || atoi(cus) == 0) return MPI_SUCCESS;
+  const char* m = getenv("FTAR_MPI_TRANSPORT");
+  return m && !strcmp(m, "ipc") ? MPI_SUCCESS : MPI_ERR_ARG;
+}
+
 // before the communicator's bring-up, as get_stages precedes everything in the
 // reference's call: a bad FT_TOPO fails every rank alike, GPU or not (and so
-// does a calibration file that does not parse)
+// does a calibration file that does not parse, or a CU share RCCL refuses)
 int check_topo_first(MPI_Comm comm) {
   int size = 1;
   if (MPI_Comm_size(comm, &size) != MPI_SUCCESS) return MPI_ERR_COMM;
-  const int rc = check_env_topo(size);
-  return rc != MPI_SUCCESS ? rc : check_cost_file();
+  int rc = check_env_topo(size);
+  if (rc == MPI_SUCCESS) rc = check_cost_file();
+  if (rc == MPI_SUCCESS && size > 1) rc = check_reduce_cus();
+  return rc;
 }
 
 int status_to_mpi(ftar_status_t st) {

@@ -676,7 +676,7 @@ struct SegArgs {
   size_t bytes[FTAR_MAX_K];
 };
 
-template <bool NT>
+template <bool NT, bool REL = false>
 __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   const int sgi = (int)(blockIdx.x % (unsigned)m);
   const size_t bid = blockIdx.x / (unsigned)m, nb = gridDim.x / (unsigned)m;
@@ -687,6 +687,7 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   const uintptr_t ms = reinterpret_cast<uintptr_t>(src) & 15, md = reinterpret_cast<uintptr_t>(dst) & 15;
   if (ms != md) {
     for (size_t i = tid; i < n; i += nthr) dst[i] = src[i];
+    if constexpr (REL) __threadfence_system();
     return;
   }
   size_t head = ms ? 16 - ms : 0;
@@ -704,6 +705,7 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
     st16<NT>(d4 + v + kThreads, x1);
   }
   if (v < nvec) st16<NT>(d4 + v, ld16<NT>(s4 + v));
+  if constexpr (REL) __threadfence_system();  // this workgroup's stores reach memory before it retires
 }
 
 // ---------------------------------------------------------------------------

@@ -29,7 +29,8 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
   return false;
 }
 
-ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt, size_t max_wg_per_seg) {
+ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt, size_t max_wg_per_seg,
+                            bool release_system) {
   if (nsegs < 0 || nsegs > FTAR_MAX_K) return FTAR_ERR_INVALID_ARG;
   SegArgs a{};
   int m = 0;
@@ -46,10 +47,25 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, 
   size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
   bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
   if (max_wg_per_seg) bx = std::min(bx, max_wg_per_seg);
-  if (nt)
-    FTAR_LAUNCH(gather_kernel<true>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+  const dim3 grid((unsigned)(bx * (size_t)m));
+  if (release_system && nt)
+    FTAR_LAUNCH((gather_kernel<true, true>), grid, dim3(kThreads), 0, stream, a, m);
+  else if (release_system)
+    FTAR_LAUNCH((gather_kernel<false, true>), grid, dim3(kThreads), 0, stream, a, m);
+  else if (nt)
+    FTAR_LAUNCH(gather_kernel<true>, grid, dim3(kThreads), 0, stream, a, m);
   else
-    FTAR_LAUNCH(gather_kernel<false>, dim3((unsigned)(bx * (size_t)m)), dim3(kThreads), 0, stream, a, m);
+    FTAR_LAUNCH(gather_kernel<false>, grid, dim3(kThreads), 0, stream, a, m);
+  FTAR_CHECK_HIP(hipGetLastError());
+  return FTAR_SUCCESS;
+}
+
+namespace {
+__global__ void noop_kernel() {}
+}  // namespace
+
+ftar_status_t launch_noop(hipStream_t stream) {
+  FTAR_LAUNCH(noop_kernel, dim3(1), dim3(64), 0, stream);
   FTAR_CHECK_HIP(hipGetLastError());
   return FTAR_SUCCESS;
 }

@@ -161,6 +161,7 @@ _lib.ftar_debug_set_peer_tuning.argtypes = [_vp, _int, _int]
 _lib.ftar_debug_set_peer_dma.argtypes = [_vp, _int]
 _lib.ftar_debug_set_rccl_register.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_wg_cap.argtypes = [_vp, _sz]
+_lib.ftar_debug_exchange_buffer.argtypes = [_vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz)]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
@@ -410,8 +411,8 @@ def cost_set(**kw):
 
 def cost_load(path):
     """Load the execution model's constants from a calibration file (ftar_cost_load; FTAR_COST_FILE does the
-    same at first use).  Returns cost_get()."""
-    _check(_lib.ftar_cost_load(os.fsencode(path)), "ftar_cost_load")
+    same at first use, and takes precedence); None forgets the loaded ones.  Returns cost_get()."""
+    _check(_lib.ftar_cost_load(None if path is None else os.fsencode(path)), "ftar_cost_load")
     return cost_get()
 
 
@@ -637,6 +638,14 @@ class Comm:
             _check(_lib.ftar_xgmi_probe(self.handle, bytes_per_peer, iters, out, k), "ftar_xgmi_probe")
         return dict(zip(("local_copy", "read_one_peer", "read_all_peers", "write_one_peer", "write_all_peers",
                          "dma_read_all_peers", "dma_write_all_peers"), (round(v, 2) for v in out)))
+
+    def exchange_buffer(self, peer):
+        """Test hook (ftar_debug_exchange_buffer): (device pointer, bytes) of rank `peer`'s exchange buffer as
+        this process maps it (peer == this rank: its own); (0, 0) before the first peer-form call."""
+        p, n = _vp(), _sz()
+        _check(_lib.ftar_debug_exchange_buffer(self.handle, int(peer), ctypes.byref(p), ctypes.byref(n)),
+               "exchange_buffer")
+        return (p.value or 0), n.value
 
     @property
     def reduce_cus(self):

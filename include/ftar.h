@@ -181,9 +181,11 @@ ftar_status_t ftar_cost_get(ftar_cost_params_t* params);
 /* Calibration files: the constants a run on the node fitted (bench.py --save-cost), so every later
  * MPI_Allreduce_FT on that node prices with them.  One "<field> <value>" per line ('#' comments), the
  * fields named as in ftar_cost_params_t, values > 0; fields left out keep their defaults.  Precedence:
- * FTAR_COST_<FIELD> > ftar_cost_set > the file > the defaults.  FTAR_COST_FILE=<path> loads one (re-read
- * when the variable changes; an unreadable or malformed file fails communicator bring-up with
- * FTAR_ERR_INVALID_ARG).  ftar_cost_save writes the constants in effect. */
+ * FTAR_COST_<FIELD> > ftar_cost_set > FTAR_COST_FILE's file > ftar_cost_load's file > the defaults.
+ * FTAR_COST_FILE=<path> loads one (re-read when the variable changes; an unreadable or malformed file
+ * leaves the constants as they were and fails communicator bring-up with FTAR_ERR_INVALID_ARG; unsetting
+ * the variable drops its file's constants, not ftar_cost_load's).  ftar_cost_load(NULL) forgets the loaded
+ * constants; a malformed file loads nothing.  ftar_cost_save writes the constants in effect. */
 ftar_status_t ftar_cost_load(const char* path);
 ftar_status_t ftar_cost_save(const char* path);
 /* Predicted seconds of one AllReduce of `bytes` per rank: topology, form

@@ -1,0 +1,162 @@
+"""The full-size cases on eight processes of a host-bootstrapped communicator -- TEST INFRASTRUCTURE shared by
+tests/test_gpu_full_size.py (one pass) and tools/host_comm_stress.py (many, under diagnostic settings).
+
+Every rank runs the same cases in the same order on cuda:0.  Around each case:
+  * its own exchange buffer X is filled with a NaN poison (0xFF bytes) between two barriers, so a later read
+    of a range nobody wrote in this case shows as "poison", not as the previous case's data;
+  * after the case every rank fingerprints every rank's X as this process maps it, 2 MiB page by page
+    (gpu_util.exchange_fingerprints), and the fingerprints are compared across ranks: a mapping that shows
+    other memory than its owner's is named (viewer, owner, pages);
+  * a wrong result is explained (whole_fold.explain): bad (block, piece) cells, runs, and what the values are.
+Every rank reports; nothing stops at the first bad rank.
+"""
+import os
+
+# (name, n, dtype, topology, peer form, host buffers)
+CASES = [("c4_read", 1 << 28, "f32", "1", "read", False),
+         ("c5_write", 1 << 29, "bf16", "8", "write", False),
+         ("c4_host_read", 1 << 28, "f32", "1", "read", True),     # peer_allreduce_host, piece-pipelined
+         ("c5_host_write", 1 << 29, "bf16", "8", "write", True)]  # whole bucket in, exchange, out
+WIDE = [("c4_write", 1 << 28, "f32", "1", "write", False), ("c5_read", 1 << 29, "bf16", "8", "read", False)]
+POISON = {"f32": 0xFFFFFFFF, "bf16": 0xFFFF}
+HOST_PIECE_BYTES = 16 << 20   # the auto host piece at C4 (engine_host.cpp host_peer_piece): explain()'s unit
+
+
+def inputs(P, n, tdt, seed, dev):
+    import torch
+    xs = []
+    for r in range(P):
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed + r)
+        xs.append((torch.rand(n, generator=gen, device=dev) * 2 - 1).to(tdt))
+    return xs
+
+
+def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
+    """One rank: `cycles` passes over `cases`; puts (rank, {"results": [...], "error": ...}) on q, one result
+    per (cycle, case): name, cycle, ran (the form that ran), bad (whole_fold.explain or None), maps (mapping
+    mismatches, [] if every page agrees), ms (the call's host time)."""
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
+    import torch
+    import torch.distributed as dist
+
+    import ftar
+    import ftar.dist
+    import gpu_util
+    import whole_fold
+    out = {"results": []}
+    if os.environ.get("FTAR_STRESS_PIDMAP"):   # tools/host_order_check.py: which trace is which rank
+        with open(os.environ["FTAR_STRESS_PIDMAP"], "a") as f:
+            f.write(f"{rank} {os.getpid()}\n")
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        comm = ftar.dist.init_host_comm(device=0)
+        for cyc in range(cycles):
+            for name, n, dt, topo, form, host in cases:
+                tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
+                dist.barrier()                       # nobody reads my X any more
+                gpu_util.poison_exchange(comm)
+                dist.barrier()                       # everyone's X is poisoned before anyone starts
+                xs = inputs(world, n, tdt, seed, dev)
+                exp = whole_fold.fold(xs, n, "ring" if topo == "1" else "tree")
+                x = xs[rank]
+                xs.clear()
+                comm.peer_direct = form
+                t0 = time.perf_counter()
+                if host:
+                    h = x.cpu().pin_memory()
+                    del x
+                    comm.allreduce_host(None, h, n, dt, "sum", topo_=topo)
+                    torch.cuda.synchronize()
+                    ms = (time.perf_counter() - t0) * 1e3
+                    y = h.to(dev)
+                    del h
+                else:
+                    y = torch.empty_like(x)
+                    comm.allreduce(x, y, n, dt, "sum", topo_=topo)
+                    torch.cuda.synchronize()
+                    ms = (time.perf_counter() - t0) * 1e3
+                    del x
+                ran = comm.last_exec()["form"]
+                bad = None
+                if whole_fold.first_mismatch(y, exp) is not None:
+                    xs = inputs(world, n, tdt, seed, dev)
+                    piece = HOST_PIECE_BYTES // (2 if dt == "bf16" else 4)
+                    bad = whole_fold.explain(y, exp, xs, rank, "ring" if topo == "1" else "tree", piece,
+                                             poison=POISON[dt])
+                    xs.clear()
+                del y, exp
+                torch.cuda.empty_cache()
+                dist.barrier()                       # every rank's call and check are done: X is quiet
+                fps = gpu_util.exchange_fingerprints(comm)
+                allfp = [None] * world
+                dist.all_gather_object(allfp, fps)
+                maps = []
+                for owner in range(world):
+                    if owner == rank:
+                        continue
+                    pages = [i for i, (a, b) in enumerate(zip(fps[owner], allfp[owner][owner])) if a != b]
+                    if pages or len(fps[owner]) != len(allfp[owner][owner]):
+                        maps.append({"owner": owner, "pages": pages[:16], "npages": len(pages)})
+                out["results"].append({"name": name, "cycle": cyc, "ran": ran, "bad": bad, "maps": maps,
+                                       "ms": round(ms, 2)})
+                if rank == 0 and cycles > 1:
+                    print(f"cycle {cyc} {name}: {ms:.1f} ms, {'BAD' if bad else 'ok'}", flush=True)
+        dist.barrier()
+        comm.destroy()
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001  report, don't hang the parent
+        import traceback
+        out["error"] = traceback.format_exc()
+    q.put((rank, out))
+
+
+def run(cases, world=8, cycles=1, env=None, timeout=240):
+    """Start `world` spawned ranks, return {rank: report}."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=worker, args=(r, world, port, q, cases, cycles, 6161, env)) for r in range(world)]
+    for p in ps:
+        p.start()
+    try:
+        res = dict(q.get(timeout=timeout) for _ in range(world))
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+def failures(res, world=8):
+    """Every rank's problems, as lines: errors, wrong forms, wrong results (explained), bad mappings."""
+    import whole_fold
+    lines = []
+    for r in range(world):
+        rep = res.get(r, {"error": "no report"})
+        if "error" in rep:
+            lines.append(f"rank {r}: error: {rep['error']}")
+        for x in rep.get("results", []):
+            tag = f"rank {r} cycle {x['cycle']} {x['name']}"
+            form = next(c[4] for c in CASES + WIDE if c[0] == x["name"])
+            if x["ran"] != "peer-" + form:
+                lines.append(f"{tag}: ran {x['ran']}")
+            if x["bad"] is not None:
+                lines.append(f"{tag}: {whole_fold.describe(x['bad'])}")
+            for mm in x["maps"]:
+                lines.append(f"{tag}: mapping of rank {mm['owner']}'s exchange buffer differs from the owner's "
+                             f"view in {mm['npages']} 2 MiB pages, first {mm['pages']}")
+    return lines

@@ -18,8 +18,10 @@ def _defaults(monkeypatch):
         monkeypatch.delenv("FTAR_COST_" + k, raising=False)
     monkeypatch.delenv("FTAR_COST_MODEL", raising=False)
     ftar.cost_set()
+    ftar.cost_load(None)
     yield
     ftar.cost_set()
+    ftar.cost_load(None)
 
 
 def _piece(e):
@@ -199,6 +201,28 @@ def test_cost_file_from_the_environment(tmp_path, monkeypatch):
     assert k["alpha_us"] == pytest.approx(20.0) and k["coll_gbps"] == pytest.approx(300.0)
     monkeypatch.delenv("FTAR_COST_FILE")
     assert ftar.cost_get()["coll_gbps"] == 0.0
+
+
+def test_cost_file_variable_and_explicit_load_are_kept_apart(tmp_path, monkeypatch):
+    """a malformed FTAR_COST_FILE leaves the previous file's constants in effect (and fails bring-up,
+    cost_file_status); unsetting the variable drops its file's constants but not ftar_cost_load's; the
+    variable's file beats the explicit load field by field."""
+    a, bad, loaded = tmp_path / "a.cost", tmp_path / "bad.cost", tmp_path / "l.cost"
+    a.write_text("alpha_us 40\n")
+    bad.write_text("alpha_us fast\n")
+    loaded.write_text("alpha_us 11\nissue_us 13\n")
+    ftar.cost_load(str(loaded))
+    assert ftar.cost_get()["alpha_us"] == pytest.approx(11.0)
+    monkeypatch.setenv("FTAR_COST_FILE", str(a))
+    k = ftar.cost_get()
+    assert k["alpha_us"] == pytest.approx(40.0) and k["issue_us"] == pytest.approx(13.0)
+    monkeypatch.setenv("FTAR_COST_FILE", str(bad))
+    assert ftar.cost_get()["alpha_us"] == pytest.approx(40.0)   # a's constants stay
+    monkeypatch.delenv("FTAR_COST_FILE")
+    k = ftar.cost_get()
+    assert k["alpha_us"] == pytest.approx(11.0) and k["issue_us"] == pytest.approx(13.0)   # the load stays
+    ftar.cost_load(None)
+    assert ftar.cost_get()["alpha_us"] == pytest.approx(20.0)
 
 
 @pytest.mark.parametrize("text", ["alpha_us 0\n", "alpha_us -3\n", "not_a_field 5\n", "link_gbps 5 6\n",

@@ -10,8 +10,6 @@ the oracle by tests/test_whole_fold.py).  Some cases use pipeline pieces that do
 piece; in host mode the (stage, piece) steps also run skewed (engine.cpp step_order).  Every data-movement form
 runs at C4 (direct, stages, collective, peer-read, peer-write, auto), the peer forms at C5 too.
 """
-import os
-
 import pytest
 
 import whole_fold
@@ -164,96 +162,19 @@ def test_host_allreduce_full_size_whole_bucket(P, n, dt, topo, piece):
         torch.cuda.empty_cache()
 
 
-# (name, n, dtype, topology, peer form, host buffers)
-HOST_COMM_CASES = [("c4_read", 1 << 28, "f32", "1", "read", False),
-                   ("c5_write", 1 << 29, "bf16", "8", "write", False),
-                   ("c4_host_read", 1 << 28, "f32", "1", "read", True),     # peer_allreduce_host, piece-pipelined
-                   ("c5_host_write", 1 << 29, "bf16", "8", "write", True)]  # whole bucket in, exchange, out
-if os.environ.get("FTAR_RUN_WIDE") == "1":   # the other form at each size
-    HOST_COMM_CASES += [("c4_write", 1 << 28, "f32", "1", "write", False), ("c5_read", 1 << 29, "bf16", "8", "read", False)]
-
-
-def _host_comm_worker(rank, world, port, q):
-    """One rank of an 8-process host-bootstrapped communicator (the MPI drop-in's `ipc` transport, no RCCL) on
-    cuda:0: each case's P inputs are regenerated from their seeds on every rank, the reference's fold of them is
-    this rank's expected result, and the rank reports only the mismatch count."""
-    import os
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "allreduce-over-mpi_amd"), os.path.join(root, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch
-    import torch.distributed as dist
-
-    import ftar
-    import ftar.dist
-    out = {}
-    try:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
-        dev = torch.device("cuda", 0)
-        comm = ftar.dist.init_host_comm(device=0)
-        for name, n, dt, topo, form, host in HOST_COMM_CASES:
-            tdt = {"f32": torch.float32, "bf16": torch.bfloat16}[dt]
-            xs = _inputs(world, n, tdt, 6161, dev)
-            exp = whole_fold.fold(xs, n, "ring" if topo == "1" else "tree")
-            x = xs[rank]
-            xs.clear()
-            comm.peer_direct = form
-            if host:
-                h = x.cpu().pin_memory()
-                del x
-                comm.allreduce_host(None, h, n, dt, "sum", topo_=topo)
-                torch.cuda.synchronize()
-                y = h.to(dev)
-            else:
-                y = torch.empty_like(x)
-                comm.allreduce(x, y, n, dt, "sum", topo_=topo)
-                torch.cuda.synchronize()
-                del x
-            ran = comm.last_exec()["form"]
-            bad = whole_fold.first_mismatch(y, exp)
-            out[name] = (ran, bad)
-            del y, exp
-            torch.cuda.empty_cache()
-            dist.barrier()
-        comm.destroy()
-        dist.destroy_process_group()
-    except Exception:  # noqa: BLE001  report, don't hang the parent
-        import traceback
-        out["error"] = traceback.format_exc()
-    q.put((rank, out))
-
-
 def test_host_comm_peer_forms_full_size_whole_bucket():
     """C4 and C5 on eight PROCESSES of a host-bootstrapped communicator (IPC-mapped exchange buffers across the
     process boundary, the machinery the peer forms use between the GPUs of a node): peer read and write on
-    device buffers, and the host-buffer paths; every rank's whole bucket equals the reference's fold."""
-    import socket
-
-    import torch.multiprocessing as mp
-    world = 8
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_host_comm_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    try:
-        res = dict(q.get(timeout=240) for _ in range(world))
-    finally:
-        for p in ps:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
-    for r in range(world):
-        assert "error" not in res[r], res[r]["error"]
-        for name, _, _, _, form, _ in HOST_COMM_CASES:
-            ran, bad = res[r][name]
-            assert ran == "peer-" + form, (name, r, ran)
-            assert bad is None, f"{name}: rank {r}: {bad[0]} elements differ from the reference's fold, first at {bad[1]}"
+    device buffers, and the host-buffer paths; every rank's whole bucket equals the reference's fold.  Each
+    case starts on NaN-poisoned exchange buffers, every rank's view of every mapping is compared page by page
+    after it, and every rank's failures are reported, localised and classified (tests/host_comm_cases.py)."""
+    import host_comm_cases as hc
+    cases = hc.CASES + hc.WIDE   # read and write forms at both sizes (ADVICE r5: keep both in the default suite)
+    res = hc.run(cases)
+    bad = hc.failures(res)
+    assert not bad, "\n".join(bad)
+    for r in range(8):
+        assert [x["name"] for x in res[r]["results"]] == [c[0] for c in cases], r
 
 
 @pytest.mark.parametrize("topo", ["1", "2"])

@@ -99,6 +99,28 @@ def test_harness_bad_cost_file_fails_every_rank(tmp_path, ranks):
 
 
 @needs
+@pytest.mark.parametrize("transport", [None, "rccl", "auto"])
+def test_harness_reduce_cus_refused_before_rccl_bring_up(tmp_path, transport):
+    """FTAR_REDUCE_CUS (a CU share RCCL communicators refuse) with a transport that may be RCCL: every rank's
+    MPI_Allreduce_FT returns MPI_ERR_ARG before bring-up (no GPU involved) instead of the auto transport taking
+    the refusal for an RCCL failure and switching every rank to ipc; a 0 share is no share."""
+    base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY", "FTAR_MPI_TRANSPORT")}
+    env = dict(base, FTAR_REDUCE_CUS="64", FT_TOPO="1")
+    if transport:
+        env["FTAR_MPI_TRANSPORT"] = transport
+    p = subprocess.run([MPIEXEC, "-n", "2", BIN, "--size", "4096", "--repeat", "2", "--check"], cwd=tmp_path,
+                       env=env, capture_output=True, text=True, timeout=120)
+    out = p.stdout + p.stderr
+    assert p.returncode != 0 and "FAILED: allreduce failed on 2 of 2 ranks" in out, out
+    for r in range(2):
+        # MPI_ERR_ARG (12 in MPICH), not the MPI_ERR_OTHER a failed bring-up would give
+        assert re.search(rf"\[rank {r}\] allreduce failed \(timed call\): MPI error 12\b", out), out
+    p = subprocess.run([MPIEXEC, "-n", "1", BIN, "--size", "1000", "--repeat", "2", "--check"], cwd=tmp_path,
+                       env=dict(env, FTAR_REDUCE_CUS="0"), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "(test passed)" in p.stdout, p.stdout + p.stderr
+
+
+@needs
 def test_harness_ft_topo_valid_single_rank(tmp_path):
     """The valid spellings at one rank (the ring "1", unset) still copy: the P <= 1 path."""
     base = {k: v for k, v in os.environ.items() if k not in ("FT_TOPO", "FT_LONELY")}

@@ -63,3 +63,58 @@ def test_scale_report_on_the_rehearsed_n8_line():
                    "xGMI probe", "cost model refit", "unidentified", "C5 bf16:", "a tie of 6 broken by stages",
                    "host e2e:", "bit-identical to the device path", "stages (s):"):
         assert needle in out, (needle, out[:3000])
+
+
+HOST_ORDER = os.path.join(ROOT, "tools", "host_order_check.py")
+GATHER = "void ftar::(anonymous namespace)::gather_kernel(ftar::(anonymous namespace)::SegArgs, int)"
+BLIT = "__amd_rocclr_copyBuffer"
+
+
+def write_host_call(d, P=4, m=3, late=None):
+    """A well-ordered peer_allreduce_host call of P ranks and m pieces, one rocprofv3 kernel + memory-copy
+    trace per pid (100 + rank), in us steps: piece k's H2D copies at [10k, 10k+5), every fold at
+    [100k+20, 100k+30), every gather at [100k+40, 100k+50), the D2H blits at [100k+60, 100k+65).  late =
+    (rank, piece): that rank's D2H of that piece starts before its gather ends (the violation to find)."""
+    os.makedirs(d, exist_ok=True)
+    us = 1000
+    with open(os.path.join(d, "pidmap.txt"), "w") as f:
+        for r in range(P):
+            f.write(f"{r} {100 + r}\n")
+    for r in range(P):
+        ks, ms = [], []
+        for k in range(m):
+            t = 100 * k
+            ks.append({"Kernel_Name": FOLD, "Stream_Id": 1, "Start_Timestamp": (t + 20) * us, "End_Timestamp": (t + 30) * us})
+            ks.append({"Kernel_Name": GATHER, "Stream_Id": 1, "Start_Timestamp": (t + 40) * us, "End_Timestamp": (t + 50) * us})
+            d2h0 = t + (45 if late == (r, k) else 60)
+            for b in range(P):
+                ms.append({"Direction": "MEMORY_COPY_HOST_TO_DEVICE", "Stream_Id": 3,
+                           "Start_Timestamp": (10 * k) * us + b, "End_Timestamp": (10 * k + 5) * us + b})
+                ks.append({"Kernel_Name": BLIT, "Stream_Id": 2, "Start_Timestamp": d2h0 * us + b,
+                           "End_Timestamp": (d2h0 + 5) * us + b})
+        for rows, kind in ((ks, "kernel"), (ms, "memory_copy")):
+            with open(os.path.join(d, f"{100 + r}_{kind}_trace.csv"), "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=list(rows[0]))
+                w.writeheader()
+                w.writerows(rows)
+
+
+def test_host_order_check_on_known_calls(tmp_path):
+    good = tmp_path / "good"
+    write_host_call(str(good))
+    r = subprocess.run([sys.executable, HOST_ORDER, str(good), "--pidmap", str(good / "pidmap.txt")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["ok"] and d["ranks"] == 4 and d["pieces"] == 3
+    e = d["edges"]
+    assert e["h2d->fold"]["count"] == 3 * 4 * 4 and e["fold->gather"]["count"] == 3 * 4 * 3
+    assert e["gather->d2h"]["count"] == 3 * 4 * 3 and e["fold->d2h"]["count"] == 3 * 4
+    assert e["fold->gather"]["min_slack_us"] == 10.0 and e["gather->d2h"]["min_slack_us"] == 10.0
+    bad = tmp_path / "bad"
+    write_host_call(str(bad), late=(1, 2))
+    r = subprocess.run([sys.executable, HOST_ORDER, str(bad), "--pidmap", str(bad / "pidmap.txt")],
+                       capture_output=True, text=True)
+    assert r.returncode == 1
+    v = json.loads(r.stdout)["edges"]["gather->d2h"]
+    assert v["nviolations"] == 3 and {x["rank"] for x in v["violations"]} == {1} and {x["piece"] for x in v["violations"]} == {2}

@@ -46,6 +46,12 @@ for s in "${steps[@]}"; do
     hostipc) run hostipc2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29538 tools/host_ipc_rate.py --sizes 24,26,28 --pieces 0,4194304 &&
              run hostipc4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29539 tools/host_ipc_rate.py --sizes 24,26 --topo 4 ;;
     hosttests) run pytest_host 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_host_transport.py tests/test_harness.py -m gpu ;;
+    hostcomm) run pytest_hostcomm 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider tests/test_gpu_full_size.py -k host_comm -m gpu ;;
+    # stress_<config>[@cycles]: tools/host_comm_stress.py under one of its configurations
+    stress_*) cfg=${s#stress_}; cyc=${cfg#*@}; [ "$cyc" = "$cfg" ] && cyc=${STRESS_CYCLES:-8}; cfg=${cfg%@*}
+              run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --out gpurun_out/stress.jsonl ;;
+    # one c4_host_read call on 8 processes, kernel + copy trace, for tools/host_order_check.py
+    hbtrace) rm -f gpurun_out/pidmap.txt; FTAR_STRESS_PIDMAP=gpurun_out/pidmap.txt run hbtrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hbtrace -- python3 tools/host_comm_stress.py --config "${HB_CONFIG:-current}" --cycles 1 --cases c4_host_read --timeout 500 ;;
     dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
   esac

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Diagnostic: the full-size host-comm cases (tests/host_comm_cases.py) for many cycles on eight processes of
+one GPU, each case on poisoned exchange buffers, every mapping compared page by page, every wrong result
+localised and classified -- under the current settings and under round 5's failing configuration.
+
+    python3 tools/host_comm_stress.py --config current --cycles 10 --out gpurun_out/stress.jsonl
+    python3 tools/host_comm_stress.py --config r5 --cycles 10 ...
+
+Configurations (environment of every rank; engine.cpp ensure_host_streams, engine_host.cpp): see CONFIGS.
+  current  the tree as it is
+  r5       the build of round 5's one c4_host_read mismatch: copy streams at the highest priority
+           (FTAR_DEBUG_HOST_COPY_PRIORITY=1), every H2D piece issued up front (FTAR_DEBUG_HOST_LOOKAHEAD=1000),
+           D2H on the host D2H stream (FTAR_DEBUG_HOST_D2H_STREAM=1); prio / upfront / d2hs one of those each
+  r5_*     r5 with a change at the gather -> D2H hand-off (FTAR_DEBUG_HOST_GATHER_FENCE): an empty kernel
+           after the gather (noop), a system-scope release ending every gather workgroup (fence), temporal
+           stores in the gather (temporal)
+Writes one JSON line per (rank, cycle, case) and prints a summary; exit status 1 if anything was wrong.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "allreduce-over-mpi_amd"), os.path.join(ROOT, "tests")]
+
+R5 = {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1", "FTAR_DEBUG_HOST_LOOKAHEAD": "1000", "FTAR_DEBUG_HOST_D2H_STREAM": "1"}
+CONFIGS = {
+    "current": {},
+    "r5": R5,
+    # one ingredient of r5 at a time
+    "prio": {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1"},
+    "upfront": {"FTAR_DEBUG_HOST_LOOKAHEAD": "1000"},
+    "d2hs": {"FTAR_DEBUG_HOST_D2H_STREAM": "1"},
+    # r5 with a change at the gather -> D2H hand-off (FTAR_DEBUG_HOST_GATHER_FENCE, engine_host.cpp)
+    "r5_noop": dict(R5, FTAR_DEBUG_HOST_GATHER_FENCE="1"),
+    "r5_fence": dict(R5, FTAR_DEBUG_HOST_GATHER_FENCE="2"),
+    "r5_temporal": dict(R5, FTAR_DEBUG_HOST_GATHER_FENCE="3"),
+    "fence": {"FTAR_DEBUG_HOST_GATHER_FENCE": "2"},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="current")
+    ap.add_argument("--cycles", type=int, default=5)
+    ap.add_argument("--cases", default="", help="comma-separated case names (default: the four default cases)")
+    ap.add_argument("--out", default="")
+    ap.add_argument("--timeout", type=int, default=600)
+    a = ap.parse_args()
+    import host_comm_cases as hc
+    cases = hc.CASES + hc.WIDE
+    if a.cases:
+        want = a.cases.split(",")
+        cases = [c for c in cases if c[0] in want]
+    t0 = time.time()
+    res = hc.run(cases, cycles=a.cycles, env=CONFIGS[a.config], timeout=a.timeout)
+    lines = hc.failures(res)
+    if a.out:
+        with open(a.out, "a") as f:
+            for r in sorted(res):
+                for x in res[r].get("results", []):
+                    f.write(json.dumps(dict(x, rank=r, config=a.config)) + "\n")
+                if "error" in res[r]:
+                    f.write(json.dumps({"rank": r, "config": a.config, "error": res[r]["error"]}) + "\n")
+    ms = {}
+    for r in res:
+        for x in res[r].get("results", []):
+            ms.setdefault(x["name"], []).append(x["ms"])
+    print(json.dumps({"config": a.config, "cycles": a.cycles, "cases": [c[0] for c in cases],
+                      "problems": len(lines), "seconds": round(time.time() - t0, 1),
+                      "median_ms": {k: sorted(v)[len(v) // 2] for k, v in ms.items()}}))
+    for ln in lines:
+        print(ln)
+    return 1 if lines else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
