@@ -2,6 +2,7 @@
 // exchange / D2H overlapped (the MPI drop-in's `ipc` transport).  Split out of engine.cpp (round 5); no
 // behaviour change.
 #include <algorithm>
+#include <cstring>
 
 #include "engine_state.h"
 
@@ -66,6 +67,10 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // waits on; 2 the gather's workgroups end with a system-scope release; 3 the gather with temporal stores
   static const int gather_fence =
       getenv("FTAR_DEBUG_HOST_GATHER_FENCE") ? atoi(getenv("FTAR_DEBUG_HOST_GATHER_FENCE")) : 0;
+  // FTAR_DEBUG_HOST_D2H_ORDER=host (diagnostic): the D2H of piece k is issued only once the host has seen
+  // the gather of piece k complete (after the next barrier) instead of waiting for its event on the device
+  static const bool d2h_host_order =
+      getenv("FTAR_DEBUG_HOST_D2H_ORDER") && !strcmp(getenv("FTAR_DEBUG_HOST_D2H_ORDER"), "host");
   // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
   // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
   // so all of them leave the call at the same barrier instead of some waiting in the next.
@@ -149,11 +154,12 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
             [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
       if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
       FTAR_RETURN_IF(issue_h2d(k + 1 + lookahead));  // after this fold's commands (see above)
-      if (k > 0) FTAR_RETURN_IF(issue_d2h(k - 1));            // likewise
+      if (k > 0 && !d2h_host_order) FTAR_RETURN_IF(issue_d2h(k - 1));  // likewise
       return FTAR_SUCCESS;
     });
     if (!sync()) return leave();  // piece k folded everywhere (and piece k+1 in)
     work([&]() -> ftar_status_t {
+      if (k > 0 && d2h_host_order) FTAR_RETURN_IF(issue_d2h(k - 1));
       segs.clear();
       for (const Transfer& x : ag.recvs)
         if (x.len > lo)
@@ -168,9 +174,14 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
         if (gather_fence == 1) FTAR_RETURN_IF(launch_noop(c->comm_s));
       }
       FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
-      return k + 1 == m ? issue_d2h(k) : FTAR_SUCCESS;  // the others after the next fold
+      return k + 1 == m && !d2h_host_order ? issue_d2h(k) : FTAR_SUCCESS;  // the others after the next fold
     });
   }
+  work([&]() -> ftar_status_t {
+    if (!d2h_host_order) return FTAR_SUCCESS;
+    FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
+    return issue_d2h(m - 1);
+  });
   work([&]() -> ftar_status_t {
     FTAR_RETURN_IF(mark(c, "pieces folded and gathered", c->comm_s));
     // the last barrier also waits for my D2H pieces: after it nothing of this call reads my X, my own

@@ -594,6 +594,29 @@ struct LocalHub {
     std::vector<std::shared_ptr<hipEvent_t>> ev;
   };
   void notify(int rank) { rcv[rank].notify_all(); }
+  // After any transport failure the group is unusable: messages of the failed call may still
+  // sit in `wire` and a failed sender's buffer may still be read by copies enqueued for it, so a later call
+  // could pair a receive with a stale message.  fail() records the first failure and wakes every waiter;
+  // every later operation of every rank is refused (destroy the group and create a new one).
+  void fail(const std::string& why) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (broken.empty()) broken = why.empty() ? std::string("a transport failure") : why;
+    }
+    for (int q = 0; q < nranks; ++q) rcv[q].notify_all();
+  }
+  ftar_status_t usable() {
+    std::string why;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      why = broken;
+    }
+    if (why.empty()) return FTAR_SUCCESS;
+    set_error("local transport: this group failed in an earlier call (" + why +
+                  "); destroy it and create a new one",
+              __FILE__, __LINE__);
+    return FTAR_ERR_INTERNAL;
+  }
   // whether kernels on device `dev` may read device `peer`'s memory (ftar_comm_init_local enables peer
   // access between every pair that supports it), cached per pair
   bool can_reach(int dev, int peer) {
@@ -625,9 +648,12 @@ struct LocalHub {
       arrived = 0;
       ++gen;
       for (int q = 0; q < nranks; ++q) rcv[q].notify_all();
-    } else if (!wait(g, rank, [&] { return gen != my_gen; })) {
+    } else if (!wait(g, rank, [&] { return gen != my_gen || !broken.empty(); })) {
       set_error("local transport: rendezvous timed out", __FILE__, __LINE__);
       return FTAR_ERR_TIMEOUT;
+    } else if (gen == my_gen) {
+      set_error("local transport: another rank failed during a rendezvous (" + broken + ")", __FILE__, __LINE__);
+      return FTAR_ERR_INTERNAL;
     }
     *out = done;
     return FTAR_SUCCESS;
@@ -639,6 +665,7 @@ struct LocalHub {
   std::shared_ptr<Round> pending, done;
   int arrived = 0;
   long gen = 0;
+  std::string broken;  // the first failure (under mu); non-empty: every later operation is refused
   std::mutex issue;  // capture of the group: one issuing thread at a time
   std::mutex pool_mu;
   std::vector<hipEvent_t> pool, retired;
@@ -689,11 +716,29 @@ class LocalTransport final : public Transport {
   }
   ftar_status_t before_join() override {
     if (!t_issue_held) return FTAR_SUCCESS;
-    std::shared_ptr<LocalHub::Round> r;
-    return hub_->rendezvous(rank_, nullptr, nullptr, &r);
+    return guarded([&] {
+      std::shared_ptr<LocalHub::Round> r;
+      return hub_->rendezvous(rank_, nullptr, nullptr, &r);
+    });
+  }
+  ftar_status_t barrier(hipStream_t s) override {
+    return guarded([&] { return barrier_impl(s); });
+  }
+  ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+    return guarded([&] { return map_peers_impl(mine, rank, nranks, peers); });
+  }
+
+ private:
+  // refused once the group failed; a failure here breaks the group for every rank
+  template <class F>
+  ftar_status_t guarded(F&& fn) {
+    FTAR_RETURN_IF(hub_->usable());
+    const ftar_status_t st = fn();
+    if (st != FTAR_SUCCESS) hub_->fail(last_error());
+    return st;
   }
   // each rank's stream waits for every other rank's event recorded at the barrier
-  ftar_status_t barrier(hipStream_t s) override {
+  ftar_status_t barrier_impl(hipStream_t s) {
     LocalHub* hub = hub_.get();
     auto e = std::shared_ptr<hipEvent_t>(new hipEvent_t(nullptr), [hub](hipEvent_t* p) {
       if (*p) hub->give_event(*p);
@@ -708,7 +753,7 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
   // one address space: the peers' allocations are usable as they are
-  ftar_status_t map_peers(void* mine, int rank, int nranks, std::vector<char*>* peers) override {
+  ftar_status_t map_peers_impl(void* mine, int rank, int nranks, std::vector<char*>* peers) {
     (void)rank;
     std::shared_ptr<LocalHub::Round> r;
     FTAR_RETURN_IF(hub_->rendezvous(rank_, mine, nullptr, &r));
@@ -717,11 +762,13 @@ class LocalTransport final : public Transport {
     return FTAR_SUCCESS;
   }
 
- private:
-
   ftar_status_t flush() {
     std::vector<Op> ops;
     ops.swap(ops_);
+    return guarded([&] { return flush_ops(ops); });
+  }
+
+  ftar_status_t flush_ops(std::vector<Op>& ops) {
     using Ev = LocalHub::Ev;
     // the event of a stream within this flush (sends: data ready; receives: copies done), recorded once
     auto per_stream = [](std::vector<std::pair<hipStream_t, Ev>>& v, hipStream_t st) -> Ev* {
@@ -797,10 +844,16 @@ class LocalTransport final : public Transport {
       {
         std::unique_lock<std::mutex> g(hub_->mu);
         auto& q = hub_->wire[{o.peer, rank_}];
-        if (!hub_->wait(g, rank_, [&] { return !q.empty(); })) {
+        if (!hub_->wait(g, rank_, [&] { return !q.empty() || !hub_->broken.empty(); })) {
           g.unlock();
           set_error("local transport: no matching send from rank " + std::to_string(o.peer), __FILE__, __LINE__);
           return publish(FTAR_ERR_TIMEOUT);
+        }
+        if (q.empty()) {
+          const std::string why = hub_->broken;
+          g.unlock();
+          set_error("local transport: another rank failed (" + why + ")", __FILE__, __LINE__);
+          return publish(FTAR_ERR_INTERNAL);
         }
         p = q.front();
         q.pop_front();
@@ -860,10 +913,15 @@ class LocalTransport final : public Transport {
       Ev d;
       {
         std::unique_lock<std::mutex> g(hub_->mu);
-        if (!hub_->wait(g, rank_, [&] { return p->taken; })) {
+        if (!hub_->wait(g, rank_, [&] { return p->taken || !hub_->broken.empty(); })) {
           set_error("local transport: send to rank " + std::to_string(o.peer) + " never received", __FILE__,
                     __LINE__);
           return FTAR_ERR_TIMEOUT;
+        }
+        if (!p->taken) {
+          set_error("local transport: another rank failed before receiving (" + hub_->broken + ")", __FILE__,
+                    __LINE__);
+          return FTAR_ERR_INTERNAL;
         }
         d = p->done;
       }

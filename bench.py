@@ -143,23 +143,33 @@ def host_cores():
 def cpu_baseline(k, n, seconds):
     """The reference's reduce_sum<float> (mpi_mod.hpp:812, 14 OpenMP threads, :820) on this host,
     built from the unmodified header into oracle/_ref/ref_golden; else the oracle port.  `cores` = the
-    threads it ran; `cores_available` = what this process may use (affinity, cgroup quota)."""
+    threads it ran; `cores_available` = what this process may use (affinity, cgroup quota).  Two legs of
+    half the time each: `value` is the warm leg (the same buffers every call, as the reference's own
+    harness reruns them) and its best call; `rotated` is the cold leg (2 disjoint buffer sets in turn, the
+    regime of the GPU line's rotated sets, bench_single), best and median."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_golden")
     hc = host_cores()
     if os.path.exists(ref):
         try:
-            out = subprocess.run([ref, "bench", "--k", str(k), "--n", str(n), "--seconds", str(seconds)],
-                                 capture_output=True, text=True, timeout=seconds * 6 + 120, check=True).stdout
-            d = json.loads(out.strip().splitlines()[-1])
+            def leg(sets, secs):
+                out = subprocess.run([ref, "bench", "--k", str(k), "--n", str(n), "--seconds", str(secs), "--sets",
+                                      str(sets)], capture_output=True, text=True, timeout=secs * 6 + 120,
+                                     check=True).stdout
+                return json.loads(out.strip().splitlines()[-1])
+            d = leg(1, seconds / 2)
+            r = leg(2, seconds / 2)
             return {"value": round(d["GBps_best"], 3), "unit": "GB/s", "cores": d["threads"], "kind": "reference",
+                    "buffers": "same every call (warm)", "statistic": "best",
                     "median": round(d["GBps_median"], 3), "mean": round(d["GBps_mean"], 3), "samples": d["iters"],
-                    "statistic": "value = the best call (the reference harness's min time, benchmark.cpp:229-240); "
-                                 "median and mean of the same calls beside it; the shared host spreads them widely",
+                    "rotated": {"buffers": "2 disjoint sets in turn (cold, as the GPU line)", "best": round(r["GBps_best"], 3),
+                                "median": round(r["GBps_median"], 3), "samples": r["iters"]},
                     "cores_available": hc,
-                    "sample": f"FlexTree::reduce_sum<float> k={k} n={n} fp32, best of {d['iters']} calls in ~{seconds:.0f}s "
-                              f"(mean {d['GBps_mean']:.2f} GB/s); {d['threads']} OpenMP threads (mpi_mod.hpp:820) on "
-                              f"{hc['available_cpus']} available CPUs (affinity {hc['affinity_cpus']}, cgroup quota "
-                              f"{hc['cgroup_quota_cpus']}, machine {hc['machine_cpus']})"}
+                    "sample": f"FlexTree::reduce_sum<float> k={k} n={n} fp32, the same buffers every call: best of "
+                              f"{d['iters']} calls in ~{seconds / 2:.0f}s (median {d['GBps_median']:.2f}); 2 rotated "
+                              f"sets: best {r['GBps_best']:.2f}, median {r['GBps_median']:.2f} of {r['iters']} calls; "
+                              f"{d['threads']} OpenMP threads (mpi_mod.hpp:820) on {hc['available_cpus']} available "
+                              f"CPUs (affinity {hc['affinity_cpus']}, cgroup quota {hc['cgroup_quota_cpus']}, "
+                              f"machine {hc['machine_cpus']})"}
         except Exception as e:  # fall through to the port
             sys.stderr.write(f"reference cpu baseline failed: {e}\n")
     import numpy as np
@@ -176,8 +186,8 @@ def cpu_baseline(k, n, seconds):
     times.sort()
     best, med, iters = times[0], times[len(times) // 2], len(times)
     return {"value": round((k + 1) * m * 4 / best / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "buffers": "same every call (warm)", "statistic": "best",
             "median": round((k + 1) * m * 4 / med / 1e9, 3), "samples": iters,
-            "statistic": "value = the best call; median beside it",
             "cores_available": hc,
             "sample": f"oracle reduce k={k} n={m} fp32 single thread, best of {iters}"}
 
@@ -706,6 +716,72 @@ def c4_ring_by_form(sweep, world, gpus, bucket, links_of):
                      "roofline": allreduce_roofline(world, gpus, bucket, b["ms"], links_of(b)),
                      "judged": form == "direct"}
     return out or None
+
+
+# The N > 1 line's stages after the default configuration, in the order they run: what the
+# line must carry first -- the ring and default-topology RCCL entries (c4_ring), the bounded xGMI probe and
+# the model's fit, C5 per width, the host-memory rate -- then the rest of the sweep, the model's refit and the
+# re-timed headline; the extras last.  (name, required, reserve_s): a required stage always runs; an optional
+# one runs only while the time left after it still covers every later required stage's reserve, and a
+# bounded stage (the sweeps, the probe) gets exactly that much time.  Reserves are generous for a node (the
+# loopback rehearsal's stages took 0.3-7 s each, its probe 40 s on one shared GPU).
+DIST_STAGES = [
+    ("sweep core", True, 30.0),
+    ("xgmi probe", False, 10.0),
+    ("C5 bf16", True, 40.0),
+    ("host e2e", True, 30.0),
+    ("sweep rest", False, 5.0),
+    ("cost model", True, 5.0),
+    ("headline", True, 15.0),
+    ("phase timing", False, 8.0),
+    ("rccl yardstick", False, 8.0),
+    ("256 MiB", False, 8.0),
+    ("reference cpu/mpi", False, 40.0),
+]
+
+
+class StageClock:
+    """Time accounting of DIST_STAGES against the run's budget (FTAR_BENCH_BUDGET_S, which the watchdog
+    enforces): `margin` seconds are kept for printing the line."""
+
+    def __init__(self, budget, t0, now=time.time, stages=DIST_STAGES, margin=10.0):
+        self.budget, self.t0, self.now, self.margin = budget, t0, now, margin
+        self.stages = list(stages)
+        self.names = [st[0] for st in self.stages]
+        self.skipped = {}
+
+    def left(self):
+        return self.budget - (self.now() - self.t0) - self.margin
+
+    def reserved_after(self, name):
+        i = self.names.index(name)
+        return sum(r for _, req, r in self.stages[i + 1:] if req)
+
+    def limit(self, name):
+        """seconds this stage may take and still leave every later required stage its reserve"""
+        return self.left() - self.reserved_after(name)
+
+    def may_run(self, name):
+        _, req, reserve = self.stages[self.names.index(name)]
+        if req:
+            return True
+        ok = self.limit(name) >= reserve
+        if not ok:
+            self.skipped[name] = round(self.limit(name), 1)
+        return ok
+
+
+def run_stage_plan(clock, work):
+    """Run DIST_STAGES with `work` = {name: fn(limit_s)} under `clock`: the order and the skipping rule of
+    bench_distributed, kept apart so tests/test_bench_helpers.py can drive it with synthetic stage times.
+    Returns the names run, in order."""
+    ran = []
+    for name in clock.names:
+        if name not in work or not clock.may_run(name):
+            continue
+        work[name](clock.limit(name))
+        ran.append(name)
+    return ran
 
 
 def sweep_form(form):
@@ -1604,7 +1680,7 @@ def bench_distributed(a):
                                             "stuck_stream_still_blocked": state["stuck_stream_still_blocked"]}
 
     # 2. the sweep: every factorization of P and the ring x chunk sizes x form, in tiers (below)
-    phase("sweep")
+    phase("sweep core")
     sweep = []
     cands = [str(default_topo)] + (["1"] if world > 1 else []) + [",".join(map(str, f)) for f in _factorizations(world)]
     seen, plan = set(), []
@@ -1633,38 +1709,47 @@ def bench_distributed(a):
                                                          "peer-read-reg:vec", "peer-write-reg:vec",
                                                          "peer-read-reg:dma", "peer-write-reg:dma", "peer-read:dma")]
     # stable sort into tiers, so the likeliest winners are timed before the budget can run out: the default
-    # topology's direct RCCL forms, then its peer forms (the xGMI probe runs before the first of them), then
-    # the other topologies' direct/collective forms, the reference's staged rounds, the other peer forms
+    # topology's direct RCCL forms and the ring's (c4_ring, BASELINE configs[3]), then the default topology's
+    # peer forms, the other topologies' direct/collective forms, the reference's staged rounds, the other peer
+    # forms.  Tier 0 is the required "sweep core" stage; the rest runs after C5 and the host-memory rate, in
+    # whatever time the budget leaves (DIST_STAGES, StageClock)
     def tier(p):
         t, _, form = p
         default = str(t) == str(default_topo)
         if form.startswith("peer-"):
             return 1 if default else 4
         if form.startswith("direct"):
-            return 0 if default else 2
+            return 0 if default or t.ring else 2
         return 2 if form == "collective" else 3
     plan.sort(key=tier)
-    sweep_t0 = time.time()
-    probed = False
-    i_plan = 0
-    while i_plan < len(plan):
-        t, chunk, form = plan[i_plan]
-        i_plan += 1
-        if form.startswith("peer-") and not probed and world > 1:
-            # xGMI calibration before the first peer configuration: link rates by copy kernels (read/write,
-            # one peer / all peers), every rank at once; min/max over ranks
-            probed = True
-            phase("xgmi probe")
-            try:
-                pr = comm.xgmi_probe(64 << 20, iters=10)
-                vals = torch.tensor(list(pr.values()), dtype=torch.float64)
-                lo, hi = vals.clone(), vals.clone()
-                dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-                dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-                state["line"]["xgmi_probe_GBps"] = {k: [round(lo[i].item(), 1), round(hi[i].item(), 1)]
-                                                    for i, k in enumerate(pr)}
-                state["line"]["xgmi_probe_GBps"]["note"] = ("[min, max] over ranks; 64 MiB per peer per copy, "
-                                                            "10 launches, all ranks at once")
+    clock = StageClock(budget, t_start)
+    state["clock"] = clock
+
+    def agreed(name):
+        """rank 0's decision whether the stage runs, and its time limit, on every rank (the ranks' clocks
+        differ by their start-up times; a stage some rank skipped would leave the others in its collectives)"""
+        v = torch.tensor([1.0 if clock.may_run(name) else 0.0, clock.limit(name)], dtype=torch.float64)
+        dist.broadcast(v, 0)
+        return bool(v[0].item()), v[1].item()
+
+    def xgmi_probe_stage(limit_s):
+        """xGMI calibration: link rates by copy kernels (read/write, one peer / all peers), every rank at once,
+        min/max over ranks; the workgroup-cap sweep only if the first pass left time for it (the loopback
+        rehearsal's probe took 40 s on one shared GPU); then the model's fit from it"""
+        t0 = time.time()
+        try:
+            pr = comm.xgmi_probe(64 << 20, iters=10)
+            vals = torch.tensor(list(pr.values()), dtype=torch.float64)
+            lo, hi = vals.clone(), vals.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            state["line"]["xgmi_probe_GBps"] = {k: [round(lo[i].item(), 1), round(hi[i].item(), 1)]
+                                                for i, k in enumerate(pr)}
+            state["line"]["xgmi_probe_GBps"]["note"] = ("[min, max] over ranks; 64 MiB per peer per copy, "
+                                                        "10 launches, all ranks at once")
+            first = torch.tensor([time.time() - t0], dtype=torch.float64)
+            dist.broadcast(first, 0)   # every rank takes the same decision
+            if 2.5 * first.item() < limit_s:
                 # how many CUs fill the links: the same copies capped at w workgroups (256 threads) per peer
                 by_cap = {}
                 for w in (4, 8, 16, 32, 64):
@@ -1674,32 +1759,74 @@ def bench_distributed(a):
                     by_cap[w] = {"read_all_peers": round(v[0].item(), 1), "write_all_peers": round(v[1].item(), 1)}
                 state["line"]["xgmi_probe_GBps"]["by_workgroups_per_peer"] = by_cap
                 # where a capped copy beat the uncapped one by > 10 % on every rank, the peer forms get a
-                # sweep entry with that cap next (the same decision on every rank: the rates are MIN-reduced)
+                # sweep entry with that cap (the same decision on every rank: the rates are MIN-reduced)
                 extra = probe_cap_entries(state["line"]["xgmi_probe_GBps"], by_cap)
-                plan[i_plan:i_plan] = [(t, 0, f) for f in extra]
-            except Exception as e:  # noqa: BLE001
-                state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
-            try:
-                state["line"]["cost_model_fit"] = fit_cost_model(state["line"].get("xgmi_probe_GBps"))
-            except Exception as e:  # noqa: BLE001
-                state["line"]["cost_model_fit"] = {"error": str(e)[:200]}
-        stop = torch.tensor([1 if time.time() - sweep_t0 > sweep_budget else 0], dtype=torch.int32)
-        dist.broadcast(stop, 0)  # every rank takes the same decision
-        if stop.item():
-            sweep.append({"skipped": f"sweep budget {sweep_budget:.0f}s reached ({len(plan) - len(sweep)} left)"})
-            break
-        key = str(t)
-        phase(f"sweep {key} {form} {chunk}", major=False)
+                rest[0:0] = [(default_topo, 0, f) for f in extra if not a.no_peer]
+            else:
+                state["line"]["xgmi_probe_GBps"]["by_workgroups_per_peer"] = {
+                    "skipped": f"first pass took {first.item():.1f}s of a {limit_s:.0f}s stage limit"}
+        except Exception as e:  # noqa: BLE001
+            state["line"]["xgmi_probe_GBps"] = {"error": str(e)[:200]}
         try:
-            fn = run_with(t, chunk, form)
-            ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
-            ok_, why_ = check_y(fn)   # every configuration's own output, before it may be chosen
-        except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
-            sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "error": str(e)[:200]})
-            continue
-        sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "ms": round(ms_, 4),
-                      "busbw_GBps": round(bws(ms_)[1], 2), "enqueue_ms": enq["ms"],
-                      "check": "ok" if ok_ else f"MISMATCH ({why_})"})
+            state["line"]["cost_model_fit"] = fit_cost_model(state["line"].get("xgmi_probe_GBps"))
+        except Exception as e:  # noqa: BLE001
+            state["line"]["cost_model_fit"] = {"error": str(e)[:200]}
+
+    def sweep_run(entries, limit_s, what):
+        """time `entries` in order until `limit_s` seconds have gone (rank 0's clock, broadcast)"""
+        t0 = time.time()
+        for i, (t, chunk, form) in enumerate(entries):
+            stop = torch.tensor([1 if time.time() - t0 > limit_s else 0], dtype=torch.int32)
+            dist.broadcast(stop, 0)  # every rank takes the same decision
+            if stop.item():
+                sweep.append({"skipped": f"{what}: its {limit_s:.0f}s reached ({len(entries) - i} entries left)"})
+                return
+            key = str(t)
+            phase(f"sweep {key} {form} {chunk}", major=False)
+            try:
+                fn = run_with(t, chunk, form)
+                ms_ = timed(fn, steps=min(5, a.steps), warmup=1)
+                ok_, why_ = check_y(fn)   # every configuration's own output, before it may be chosen
+            except Exception as e:  # noqa: BLE001  one bad configuration must not end the run
+                sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "error": str(e)[:200]})
+                continue
+            sweep.append({"topology": key, "chunk_bytes": chunk, "form": form, "ms": round(ms_, 4),
+                          "busbw_GBps": round(bws(ms_)[1], 2), "enqueue_ms": enq["ms"],
+                          "check": "ok" if ok_ else f"MISMATCH ({why_})"})
+
+    core = [p for p in plan if tier(p) == 0]
+    rest = [p for p in plan if tier(p) > 0]
+    state["line"]["sweep"] = sweep
+    sweep_run(core, min(sweep_budget, agreed("sweep core")[1]), "sweep core")
+    phase("xgmi probe")
+    go, lim = agreed("xgmi probe")
+    if world > 1 and go:
+        xgmi_probe_stage(lim)
+
+    # BASELINE configs[4] (C5): bf16 bucket of 2^29 elements (1 GiB) with the cost model's topology (fitted to
+    # the probe when it ran), the default data movement, and every other width; validated like the rest
+    phase("C5 bf16")
+    if a.dtype == "f32" and not a.no_c5:
+        try:
+            state["line"]["c5_bf16"] = measure_c5()
+        except Exception as e:  # noqa: BLE001
+            state["line"]["c5_bf16"] = {"error": str(e)[:200]}
+
+    # the host-memory end-to-end rate (DESIGN §6): PCIe in and out included, never the headline
+    phase("host e2e")
+    if not a.no_host:
+        try:
+            state["line"]["host_e2e"] = measure_host()
+        except Exception as e:  # noqa: BLE001
+            state["line"]["host_e2e"] = {"error": str(e)[:200]}
+
+    # the rest of the sweep, in the time the later required stages leave
+    phase("sweep rest")
+    go, lim = agreed("sweep rest")
+    if go:
+        sweep_run(rest, min(sweep_budget, lim), "sweep rest")
+    else:
+        sweep.append({"skipped": f"sweep rest: {len(rest)} entries, no time left in the budget"})
     state["line"]["sweep"] = sweep
 
     # the execution model against this run's own sweep (VERDICT r3 next #2): every entry's prediction under
@@ -1759,6 +1886,9 @@ def bench_distributed(a):
     # where a call's time goes (transfer rounds vs folds vs barriers), for the next round's tuning
     phase("phase timing")
     try:
+        go, lim = agreed("phase timing")
+        if not go:
+            raise RuntimeError(f"skipped: {lim:.0f}s left after the required stages")
         fam_best = {}
         for r in ok_runs:
             if r["form"] not in fam_best or r["ms"] < fam_best[r["form"]]["ms"]:
@@ -1781,6 +1911,9 @@ def bench_distributed(a):
     # 4. RCCL's own ncclAllReduce on the same communicator and bucket (yardstick)
     phase("rccl yardstick")
     try:
+        go, lim = agreed("rccl yardstick")
+        if not go:
+            raise RuntimeError(f"skipped: {lim:.0f}s left after the required stages")
         y2 = torch.empty_like(x)
         ms_rccl = timed(lambda: comm.rccl_allreduce(x, y2, n, a.dtype, "sum", stream=stream), min(a.steps, 10), 2)
         del y2
@@ -1794,7 +1927,10 @@ def bench_distributed(a):
     phase("256 MiB")
     try:
         n2 = min(n, 1 << 26)
-        if n2 < n:
+        go, lim = agreed("256 MiB")
+        if n2 < n and not go:
+            state["line"]["bucket_256MiB"] = {"skipped": f"{lim:.0f}s left"}
+        elif n2 < n:
             hb = state["line"]["config"]
             t2 = ftar.topo("1" if hb["topology"] == "ring" else hb["topology"])
             f2 = run_with(t2, hb["chunk_bytes"], hb["form"])
@@ -1809,33 +1945,19 @@ def bench_distributed(a):
     except Exception as e:  # noqa: BLE001
         state["line"]["bucket_256MiB"] = {"error": str(e)[:200]}
 
-    # 5. BASELINE configs[4] (C5): bf16 bucket of 2^29 elements (1 GiB) with the cost model's topology, the
-    # default data movement; one more line item, validated like the rest
-    phase("C5 bf16")
-    if a.dtype == "f32" and not a.no_c5:
-        try:
-            state["line"]["c5_bf16"] = measure_c5()
-        except Exception as e:  # noqa: BLE001
-            state["line"]["c5_bf16"] = {"error": str(e)[:200]}
-
-    # 6. the host-memory end-to-end rate: PCIe in and out included, never the headline
-    phase("host e2e")
-    if not a.no_host:
-        try:
-            state["line"]["host_e2e"] = measure_host()
-        except Exception as e:  # noqa: BLE001
-            state["line"]["host_e2e"] = {"error": str(e)[:200]}
-
     # 7. the reference's own CPU/MPI path on this node's host cores, in the same run (north_star): its ring
     # over MPICH with P ranks (oracle/_ref/ref_golden arbench: mpi_mod.hpp's MPI_Allreduce_FT, 14 OpenMP
     # threads per rank), on a bounded sample, rank 0 only while the other ranks wait
     phase("reference cpu/mpi")
-    if rank == 0 and not a.no_cpu_baseline:
+    go, _ = agreed("reference cpu/mpi")
+    if rank == 0 and not a.no_cpu_baseline and go:
         state["line"]["reference_cpu_mpi"] = reference_mpi_path(world)
     dist.barrier()
 
     phase("end")
     state["line"]["stage_wall_s"] = dict(stage_t)
+    state["line"]["stages_skipped_for_budget"] = dict(clock.skipped)
+    state["line"]["budget_s"] = budget
     state["line"]["wall_s"] = round(time.time() - t_start, 1)
     emit(state["line"])
     state["done"] = True

@@ -91,6 +91,8 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                     piece = HOST_PIECE_BYTES // (2 if dt == "bf16" else 4)
                     bad = whole_fold.explain(y, exp, xs, rank, "ring" if topo == "1" else "tree", piece,
                                              poison=POISON[dt])
+                    if host:   # what this rank's exchange buffer holds there now: did the gather land?
+                        bad["exchange_now"] = exchange_at(comm, bad, n, piece, tdt, exp, xs[rank], POISON[dt])
                     xs.clear()
                 del y, exp
                 torch.cuda.empty_cache()
@@ -116,6 +118,40 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
         import traceback
         out["error"] = traceback.format_exc()
     q.put((rank, out))
+
+
+def exchange_at(comm, bad, n, piece, tdt, exp, mine, poison):
+    """Classify what this rank's exchange buffer X holds, read afresh after the call, at the first bad cell's
+    wrong elements: the final value (the gather's data is in X, so the D2H read it too early or stale), this
+    rank's input (X still holds what the H2D put there), the poison, or other."""
+    import ctypes
+
+    import torch
+
+    import gpu_util
+    ptr, nbytes = comm.exchange_buffer(comm.rank)
+    fc = bad["first_cell"]
+    split = -(-n // comm.nranks)
+    lo = fc["block"] * split + fc["piece"] * piece
+    hi = min(n, fc["block"] * split + min(split, (fc["piece"] + 1) * piece))
+    esz = torch.tensor([], dtype=tdt).element_size()
+    if not ptr or hi * esz > nbytes:
+        return None
+    buf = torch.empty(hi - lo, dtype=tdt, device="cuda")
+    hip = gpu_util.hip_runtime()
+    assert hip.hipMemcpy(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(ptr + lo * esz),
+                         ctypes.c_size_t((hi - lo) * esz), 3) == 0
+    torch.cuda.synchronize()
+    iv = {torch.float32: torch.int32, torch.bfloat16: torch.int16}[tdt]
+    xb, eb, mb = buf.view(iv), exp[lo:hi].view(iv), mine[lo:hi].view(iv)
+    # the first cell's wrong elements: recompute them from the runs (explain keeps only counts)
+    want = torch.zeros(hi - lo, dtype=torch.bool, device="cuda")
+    for s0, ln in fc["runs"]:
+        want[s0 - lo:s0 - lo + ln] = True
+    pv = torch.tensor(poison, dtype=torch.int64).to(iv).to("cuda")
+    return {"checked": int(want.sum().item()), "final": int((want & (xb == eb)).sum().item()),
+            "own_input": int((want & (xb == mb) & (xb != eb)).sum().item()),
+            "poison": int((want & (xb == pv)).sum().item())}
 
 
 def run(cases, world=8, cycles=1, env=None, timeout=240):
@@ -155,7 +191,9 @@ def failures(res, world=8):
             if x["ran"] != "peer-" + form:
                 lines.append(f"{tag}: ran {x['ran']}")
             if x["bad"] is not None:
-                lines.append(f"{tag}: {whole_fold.describe(x['bad'])}")
+                lines.append(f"{tag}: {whole_fold.describe(x['bad'])}"
+                             + (f"; exchange buffer there now: {x['bad']['exchange_now']}"
+                                if x["bad"].get("exchange_now") else ""))
             for mm in x["maps"]:
                 lines.append(f"{tag}: mapping of rank {mm['owner']}'s exchange buffer differs from the owner's "
                              f"view in {mm['npages']} 2 MiB pages, first {mm['pages']}")

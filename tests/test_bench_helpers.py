@@ -428,3 +428,63 @@ def test_refit_of_the_round4_loopback_sweep_leaves_no_constant_on_a_bound(model_
     assert rates["coll_gbps"]["unidentified"] == "bound" and rates["coll_gbps"]["value"] == 0.0
     for r in rates.values():
         assert r["value"] == 0.0 or 1.01 < r["value"] < 5000 / 1.01
+
+
+def test_cpu_baseline_states_its_regime():
+    """the CPU leg says which buffers it ran on and which statistic `value` is -- the warm leg
+    (the same buffers every call, the reference harness's way) as the best call, the median beside it, and a
+    cold leg over 2 rotated buffer sets (the GPU line's regime) -- whichever of the reference build
+    (oracle/_ref/ref_golden) or the port ran."""
+    import bench
+    d = bench.cpu_baseline(2, 1 << 18, 1.0)
+    assert d["unit"] == "GB/s" and d["value"] > 0 and d["kind"] in ("reference", "port")
+    assert d["buffers"] == "same every call (warm)" and d["statistic"] == "best"
+    assert 0 < d["median"] <= d["value"] * 1.0001
+    if d["kind"] == "reference":
+        r = d["rotated"]
+        assert r["buffers"].startswith("2 disjoint sets") and 0 < r["median"] <= r["best"] * 1.0001 and r["samples"] > 0
+        assert d["cores"] == 14   # PARALLEL_THREAD, mpi_mod.hpp:820
+
+
+class _FakeTime:
+    def __init__(self):
+        self.t = 0.0
+
+    def __call__(self):
+        return self.t
+
+
+def test_n_gt_1_stage_order_and_budget_with_synthetic_stage_times():
+    """the N > 1 line's required stages (c4_ring's sweep entries, C5 per width, the host-memory
+    rate, the model's refit, the re-timed headline) run first and inside FTAR_BENCH_BUDGET_S even when the
+    optional ones are slow (the loopback rehearsal's probe took 40 s); bounded stages get only the time the
+    later required stages leave; the extras are skipped, not the required stages."""
+    import bench
+    req = [n for n, r, _ in bench.DIST_STAGES if r]
+    assert req == ["sweep core", "C5 bf16", "host e2e", "cost model", "headline"]
+    names = [n for n, _, _ in bench.DIST_STAGES]
+    assert names.index("sweep core") < names.index("xgmi probe") < names.index("C5 bf16") < names.index("sweep rest")
+    for budget, times in ((300.0, {}), (300.0, {"xgmi probe": 40.0, "sweep rest": 1e9, "reference cpu/mpi": 60}),
+                          (150.0, {"sweep core": 25.0, "C5 bf16": 35.0, "host e2e": 20.0})):
+        clk = _FakeTime()
+        clock = bench.StageClock(budget, 0.0, now=clk)
+        used = {}
+
+        def stage(name):
+            def fn(limit):
+                want = times.get(name, 3.0)
+                took = min(want, max(0.0, limit)) if name in ("sweep core", "sweep rest", "xgmi probe") else want
+                used[name] = (took, limit)
+                clk.t += took
+            return fn
+        ran = bench.run_stage_plan(clock, {n: stage(n) for n in names})
+        assert [n for n in ran if n in req] == req, (budget, ran)       # every required stage, in order
+        assert clk.t <= budget - clock.margin + 1e-9, (budget, clk.t, used)
+        if times.get("sweep rest") == 1e9:                              # an endless sweep is cut at its limit
+            assert used["sweep rest"][0] == used["sweep rest"][1]
+            assert "reference cpu/mpi" not in ran and "reference cpu/mpi" in clock.skipped
+    # a budget too small for the probe: skipped, and the required stages still all run
+    clk = _FakeTime()
+    clock = bench.StageClock(100.0, 0.0, now=clk)
+    ran = bench.run_stage_plan(clock, {n: (lambda lim: None) for n in names})
+    assert "xgmi probe" not in ran and set(req) <= set(ran)

@@ -743,5 +743,23 @@ def test_local_transport_size_mismatch_fails_both_ranks_at_once():
         assert all(e is not None for e in errs), errs
         assert any("size mismatch" in str(e) for e in errs), errs
         torch.cuda.synchronize()
+        # the failed call's messages may still be queued: the group refuses every later call
+        # rather than pairing a receive with a stale message
+        errs = [None, None]
+        bufs = [torch.ones(n, device="cuda") for _ in range(2)]
+
+        def run2(r):
+            try:
+                g[r].allreduce(None, bufs[r], n, "f32", "sum", topo_="2")
+            except ftar.FtarError as e:
+                errs[r] = e
+        th = [threading.Thread(target=run2, args=(r,)) for r in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        assert not any(t.is_alive() for t in th)
+        assert all(e is not None and "failed in an earlier call" in str(e) for e in errs), errs
+        torch.cuda.synchronize()
     finally:
         g.destroy()

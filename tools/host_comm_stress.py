@@ -38,6 +38,10 @@ CONFIGS = {
     "r5_fence": dict(R5, FTAR_DEBUG_HOST_GATHER_FENCE="2"),
     "r5_temporal": dict(R5, FTAR_DEBUG_HOST_GATHER_FENCE="3"),
     "fence": {"FTAR_DEBUG_HOST_GATHER_FENCE": "2"},
+    # pairs of r5's ingredients, and r5 with the D2H ordered by the host instead of an event
+    "prio_d2hs": {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1", "FTAR_DEBUG_HOST_D2H_STREAM": "1"},
+    "prio_upfront": {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1", "FTAR_DEBUG_HOST_LOOKAHEAD": "1000"},
+    "r5_hostorder": dict(R5, FTAR_DEBUG_HOST_D2H_ORDER="host"),
 }
 
 
