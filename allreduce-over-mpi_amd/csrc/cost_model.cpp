@@ -46,9 +46,9 @@ std::atomic<uint64_t> g_generation{0};  // bumped by every set: communicators re
 //   alpha   one p2p group's launch and handshake (assumed, 20 us)
 //   link    an RCCL p2p stream to one peer: the xGMI link spec, 76.8 GB/s per direction, times an ASSUMED
 //           RCCL p2p efficiency of 0.7 (protocol and FIFO staging; never measured on xGMI here -- the first
-//           N > 1 run's probe and sweep replace it, DESIGN §7)
+//           N > 1 run's probe and sweep replace it, DESIGN §8)
 //   hbm     the measured k = 2..8 fold (profiles/r01/kbench3)
-//   issue   the host enqueue of one piece of one round at P = 8 (DESIGN §6, enqueue cost)
+//   issue   the host enqueue of one piece of one round at P = 8 (DESIGN §9, enqueue cost)
 //   barrier a 4-byte ncclAllReduce (assumed)
 //   copy    the LDS-staged copy (profiles/r03/kbench_copy.log)
 //   peer read / write, coll: unmeasured (0), so those forms are never chosen until a run measures them

@@ -82,7 +82,7 @@ ftar_status_t grow_events(ftar_comm* c, size_t n) {
 // the legacy NULL stream) on a hardware queue of its own, the price of the knob.
 // Refused on RCCL communicators (Transport::masked_reduce_stream_ok): two runs
 // of the RCCL stress driver stalled ranks inside the first call after the knob
-// moved from 0 to a CU share (DESIGN §4, profiles/r04/stress_soak/).
+// moved from 0 to a CU share (DESIGN §5.1, profiles/r04/stress_soak/).
 ftar_status_t set_reduce_cus(ftar_comm* c, int cus) {
   int total = 0;
   FTAR_CHECK_HIP(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, c->device));
@@ -90,7 +90,7 @@ ftar_status_t set_reduce_cus(ftar_comm* c, int cus) {
   if (cus && c->tp && !c->tp->masked_reduce_stream_ok()) {
     set_error("the reduce stream cannot be CU-masked on a " + std::string(c->tp->name()) +
                   " communicator (ftar_comm_set_reduce_cus / FTAR_REDUCE_CUS): a masked stream is a blocking "
-                  "stream on a hardware queue of its own, and over RCCL it stalled ranks (DESIGN §4); "
+                  "stream on a hardware queue of its own, and over RCCL it stalled ranks (DESIGN §5.1); "
                   "0 (every CU) is the only value accepted there",
               __FILE__, __LINE__);
     return FTAR_ERR_UNSUPPORTED;
@@ -318,7 +318,7 @@ ftar_status_t first_contact(ftar_comm* c) {
 // The topology of a call with topo == NULL, from the environment AT THIS CALL
 // (get_stages, mpi_mod.hpp:1419-1486, re-run by every MPI_Allreduce_FT call,
 // :1732).  FT_TOPO and FT_LONELY both unset (or FT_LONELY "0"): *is_auto, the
-// cost model chooses (DESIGN §9 #1: the reference exit(1)s here for P > 1).
+// cost model chooses (DESIGN §11 #1: the reference exit(1)s here for P > 1).
 // Anything else must parse for this communicator's size, or the call fails
 // with FTAR_ERR_INVALID_TOPO before it enqueues anything (the reference:
 // "invalid FT_TOPO" and exit(1), :1471-1475) -- on every rank alike, since
@@ -579,7 +579,7 @@ ftar_status_t allreduce_locked(const void* sendbuf, void* recvbuf, size_t count,
 // Serial capture: a captured call issues everything on the caller's stream (FTAR_CAPTURE_SERIAL=1 / 0;
 // default on when the loaded HIP runtime is older than 7.2).  torch 2.10 bundles HIP 7.0, whose
 // hipStreamEndCapture dies (SIGSEGV, unbounded recursion) on the graph the forked comm/reduce streams and
-// their per-piece cross waits leave, while 7.2 captures it (DESIGN §4); a chain in issue order keeps every
+// their per-piece cross waits leave, while 7.2 captures it (DESIGN §5.5); a chain in issue order keeps every
 // dependency and gives up only the comm/reduce overlap inside the graph.
 bool serial_capture() {
   static const bool on = [] {

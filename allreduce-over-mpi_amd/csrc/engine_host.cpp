@@ -86,7 +86,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     return FTAR_SUCCESS;
   };
   // Order matters when the copy streams share a hardware queue with the comm stream (HIP's 4 queues
-  // per process; DESIGN §6): commands of a shared queue run in issue order, and a barrier waits for the
+  // per process; DESIGN §6.2): commands of a shared queue run in issue order, and a barrier waits for the
   // comm stream.  So every H2D piece is issued after the fold commands of an earlier piece (never all
   // up front: the first barrier then waited for the whole bucket), and the D2H of piece k after the
   // fold of piece k + 1 (else that fold, and the barrier after it, waited for the D2H).

@@ -174,10 +174,10 @@ struct Segment {
 // nt: nontemporal loads and stores (the default: cold copies, data not
 // re-read soon); false keeps both in the caches.  release_system: every
 // workgroup ends with a system-scope release fence, so its stores are in
-// memory before it retires (the host path's gather -> D2H hand-off, DESIGN §4).
+// memory before it retires (the host path's gather -> D2H hand-off, DESIGN §6.4).
 ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true,
                             size_t max_wg_per_seg = 0, bool release_system = false);
-// An empty kernel: a stream-order point after the kernel before it (diagnostics, DESIGN §4).
+// An empty kernel: a stream-order point after the kernel before it (diagnostics, DESIGN §6.4).
 ftar_status_t launch_noop(hipStream_t stream);
 // One local device copy (k = 1 reduces, the P = 1 AllReduce, the peer forms' local copy-in/out): the
 // LDS-staged kernel when source and destination share their 16-byte alignment, else the copy kernel.
@@ -271,7 +271,7 @@ class Transport {
   virtual bool capture_serially() const { return false; }
   // The reduce stream may be a CU-masked one (ftar_comm_set_reduce_cus).  Not where the transport's kernels
   // wait on other processes on the device (RCCL): a masked stream takes a hardware queue of its own out of the
-  // process's four and is a blocking stream, and over RCCL that stalled ranks in a call (DESIGN §4).
+  // process's four and is a blocking stream, and over RCCL that stalled ranks in a call (DESIGN §5.1).
   virtual bool masked_reduce_stream_ok() const { return true; }
   // Called by every rank before it joins its internal streams back into the
   // caller's stream.  Under capture the local transport makes the ranks meet

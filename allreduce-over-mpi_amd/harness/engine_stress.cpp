@@ -277,7 +277,7 @@ bool skip(const char* knob) {
   return e && strstr(e, knob);
 }
 // On an RCCL communicator the CU share is refused (FTAR_ERR_UNSUPPORTED, the reduce stream stays on every CU:
-// DESIGN §4); the draw still happens, so the call sequence of a seed is the same as before the rule.
+// DESIGN §5.1); the draw still happens, so the call sequence of a seed is the same as before the rule.
 void apply_knobs(ftar_comm_t c, const Case& k, bool rccl) {
   const int nt = skip("tune") ? 1 : k.tune & 1, lds = skip("tune") ? 1 : (k.tune >> 1) & 1;
   const int dma = skip("dma") ? 0 : (k.tune >> 2) & 1;
@@ -311,7 +311,7 @@ int fail(const std::string& what) {
 
 // The call just made, captured into a HIP graph (relaxed mode; every rank's call on the capture stream, the
 // form the HIP runtime ends: a stream forked per rank from the capture stream makes hipStreamEndCapture recurse
-// without end, DESIGN §4 and profiles/r03/capture) and replayed twice on fresh inputs in the same buffers; the
+// without end, DESIGN §5.5 and profiles/r03/capture) and replayed twice on fresh inputs in the same buffers; the
 // uncaptured call before it grew every buffer the plan needs
 void capture_replay(int P, std::vector<ftar_comm_t>& comms, std::vector<void*>& send, std::vector<void*>& recv,
                     size_t n, const Dt& d, ftar_op_t op, bool band, const ftar_topo_t* topo, bool oop,

@@ -313,7 +313,7 @@ def bench_single(a):
                      "kernel": kern, "traffic": tr, **pv}
         if kk == 8 and not a.sweep:
             # in place (destination = source 0): the width-8 tree's fold in an MPI_IN_PLACE AllReduce, whose own
-            # block is operand and result (DESIGN §3); same bytes, (k+1) x n x 4 (the values grow; timing only)
+            # block is operand and result (DESIGN §4); same bytes, (k+1) x n x 4 (the values grow; timing only)
             ti = timed_k(lambda i: pp[i][0])
             bwi = (kk + 1) * n * esz / (ti * 1e-3) / 1e9
             sweep[kk]["in_place"] = {"ms": round(ti, 4), "GBps": round(bwi, 1), "frac": round(bwi / HBM_PEAK_GBPS, 4)}
@@ -700,7 +700,7 @@ def form_label(topology, form):
 def c4_ring_by_form(sweep, world, gpus, bucket, links_of):
     """BASELINE configs[3] (ring AllReduce, chunk size swept): the fastest validated ring entry of each RCCL
     p2p form, with its label, the pieces swept and its roofline.  `judged` marks the form the >= 70 % xGMI
-    busBW target is judged on (DESIGN §6): direct -- the reference ring's association order, tree(P)'s data
+    busBW target is judged on (DESIGN §9): direct -- the reference ring's association order, tree(P)'s data
     movement on every link; the staged ring is single-link bound by construction (its roofline is 1 link)."""
     out = {}
     for form in RCCL_P2P_FORMS:
@@ -918,7 +918,7 @@ def _identify(f, x, fx, lo, hi, n, grid=None):
 
 
 def refit_cost_model(ftar, sweep, world, bucket, fixed=None):
-    """The execution model's p2p constants re-fitted to this run's own sweep (DESIGN §7): alpha (one p2p
+    """The execution model's p2p constants re-fitted to this run's own sweep (DESIGN §8): alpha (one p2p
     group), link (one peer, one direction) and issue (host enqueue of one piece) minimise the squared log
     error of the model's prediction over the validated RCCL p2p entries (forms direct / stages, no tuning
     suffix; several topologies and piece sizes): a log grid, then a pattern search.  `fixed` names constants
@@ -1278,7 +1278,7 @@ def bench_distributed(a):
         # ":dma" = the cross-GPU copies by the DMA engines
         form, _, tune = form.partition(":")
         comm.peer_tuning(nt=tune != "plain", lds=tune != "vec", dma=tune == "dma")
-        # (no ":cusN": a CU-masked reduce stream is refused on RCCL communicators, DESIGN §4)
+        # (no ":cusN": a CU-masked reduce stream is refused on RCCL communicators, DESIGN §5.1)
         # ":ncclreg": RCCL p2p between buffers registered with RCCL (ncclCommRegister): the comm's scratch
         # and registered copies of x and y, so RCCL may skip its staging copies where it supports that
         comm.rccl_register = tune == "ncclreg"
@@ -1311,7 +1311,7 @@ def bench_distributed(a):
         return reg["x"], reg["y"]
 
     def fit_cost_model(probe):
-        """The execution model's constants from this node's probe (DESIGN §7), before the sweep prices
+        """The execution model's constants from this node's probe (DESIGN §8), before the sweep prices
         anything: link = the probe's per-link, per-direction copy rate; peer read / write = the probe's
         read / write from all peers per link (so the peer forms become candidates); alpha = half a 4 KiB
         direct-form AllReduce (two p2p rounds, no bandwidth term to speak of); barrier = a third of a 4 KiB
@@ -1603,7 +1603,7 @@ def bench_distributed(a):
 
     # 1. the default configuration: FT_TOPO/FT_LONELY (or --topo), else the re-fitted cost model
     phase("default")
-    # the default configuration is the execution model's (DESIGN §7): FT_TOPO / --topo fix the topology,
+    # the default configuration is the execution model's (DESIGN §8): FT_TOPO / --topo fix the topology,
     # --chunk-bytes the piece; the rest -- topology, form, piece -- comes from the model under its default
     # constants (no rate of this node is known yet, so the peer forms are not candidates)
     if a.topo:
@@ -1835,7 +1835,7 @@ def bench_distributed(a):
     phase("cost model")
     try:
         state["line"]["cost_model"] = validate_model(sweep)
-        if a.save_cost and rank == 0:   # the node's calibration, for FTAR_COST_FILE (DESIGN §7)
+        if a.save_cost and rank == 0:   # the node's calibration, for FTAR_COST_FILE (DESIGN §8)
             ftar.cost_save(a.save_cost)
             state["line"]["cost_model"]["saved_to"] = a.save_cost
     except Exception as e:  # noqa: BLE001  the model's report must not cost the run its line
@@ -1877,7 +1877,7 @@ def bench_distributed(a):
             hl["rccl_p2p_best"]["is_headline"] = all(hl["config"][f] == hl["rccl_p2p_best"][f]
                                                      for f in ("form", "topology", "chunk_bytes"))
         # BASELINE configs[3] says "ring AllReduce ... chunk size swept": the ring topology's best entry in
-        # each RCCL form, labelled, so nobody reads the gather as a ring (DESIGN §6 names the one the >= 70 %
+        # each RCCL form, labelled, so nobody reads the gather as a ring (DESIGN §9 names the one the >= 70 %
         # xGMI target is judged on: the direct form, the reference ring's bits over all links)
         hl["c4_ring"] = c4_ring_by_form(sweep, world, torch.cuda.device_count(), bucket,
                                         lambda r: links_driven(world, r["topology"], r["form"]))

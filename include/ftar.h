@@ -143,7 +143,7 @@ ftar_status_t ftar_cost_get_params(double* alpha_us, double* link_gbps, double* 
  * The role of the reference's CostModel (cost_model/CostModel.h:82-120: a
  * width list chosen for a chunk size), re-derived for one MI355X node.  With
  * the one-round forms every topology moves tree(P)'s bytes, so what varies on
- * a node is the form and the piece size; the model prices both (DESIGN §7):
+ * a node is the form and the piece size; the model prices both (DESIGN §8):
  *   per piece of a round: r(x) = max(alpha + x / link, issue)  (x = bytes per
  *   link), a fold of k sources (k + 1) * c / hbm on the reduce stream, the
  *   fill / drain of that two-stream pipeline simulated piece by piece; peer

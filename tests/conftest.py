@@ -15,7 +15,7 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
     config.addinivalue_line("markers", "capture_runtime_limit: a graph-capture shape the HIP runtime crashes on "
-                                       "(SIGSEGV in hipStreamEndCapture, DESIGN §4); runs only with "
+                                       "(SIGSEGV in hipStreamEndCapture, DESIGN §5.5); runs only with "
                                        "FTAR_RUN_CAPTURE_LIMITS=1")
     config.addinivalue_line("markers", "wide: further world sizes / dtypes of the multi-process RCCL rehearsals "
                                        "(several minutes together); the default GPU suite keeps one or two per "

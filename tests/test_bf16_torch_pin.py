@@ -10,7 +10,7 @@ own fp32 adds and float -> bfloat16 conversion, written out as the fold each sch
 
 The GPU kernels are pinned to the same definition by tests/test_gpu_reduce.py (flat fold against torch) and
 by the oracle comparisons of tests/test_gpu_allreduce.py.  NaN: NaN exactly where torch has NaN (which NaN
-is outside the contract, DESIGN §5)."""
+is outside the contract, DESIGN §7)."""
 import numpy as np
 import pytest
 

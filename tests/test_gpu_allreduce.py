@@ -178,7 +178,7 @@ def test_rccl_single_rank_comm():
 
 
 def test_rccl_comm_refuses_a_cu_masked_reduce_stream(monkeypatch):
-    """The rule of DESIGN §4: on an RCCL communicator the reduce stream stays on every CU -- a CU share is
+    """The rule of DESIGN §5.1: on an RCCL communicator the reduce stream stays on every CU -- a CU share is
     refused with FTAR_ERR_UNSUPPORTED (the setter, and FTAR_REDUCE_CUS at bring-up), 0 is accepted, and the
     communicator still runs; an in-process group keeps the knob."""
     import ftar
@@ -572,7 +572,7 @@ def test_allreduce_group_captures_on_the_torch_runtime(tmp_path, P, topo, rs, ag
 @pytest.mark.capture_runtime_limit
 @pytest.mark.xfail(reason="HIP 7.0 runtime (torch): hipStreamEndCapture recurses without end once the caller "
                           "forks one stream per rank from the capture stream; a single-threaded event-only "
-                          "reproducer is in profiles/r03/capture/ (tools/capture/replay.cpp), DESIGN §4",
+                          "reproducer is in profiles/r03/capture/ (tools/capture/replay.cpp), DESIGN §5.5",
                    strict=False)
 @pytest.mark.parametrize("P,topo,rs,ag,chunk,shared", [(2, "1", "direct", "direct", 4096, False)])
 def test_allreduce_group_capture_runtime_limits(tmp_path, P, topo, rs, ag, chunk, shared):

@@ -22,12 +22,15 @@ def _run(args, timeout, **extra_env):
     return p
 
 
-@pytest.mark.parametrize("calls", [200, pytest.param(1500, marks=pytest.mark.wide)])
+@pytest.mark.parametrize("calls", [500, pytest.param(1500, marks=pytest.mark.wide)])
 def test_in_process_groups(calls):
+    # 500 calls of seed 5 bring up and tear down at least 8 groups (the bar round 5 lowered to 3),
+    # so the in-process transport's pooled threads, batched events and broken-group state see several
+    # lifecycles in the default suite
     p = _run([calls, 5], 240)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
     stats = json.loads(p.stdout.strip().splitlines()[-1])
-    assert stats["checked"] == stats["calls"] >= calls and stats["groups"] >= 3 and stats["captured"] > 0, stats
+    assert stats["checked"] == stats["calls"] >= calls and stats["groups"] >= 8 and stats["captured"] > 0, stats
 
 
 def test_in_process_groups_multi_segment_receives():

@@ -59,7 +59,7 @@ def test_rccl_p2p_between_ranks_matches_reference(world):
     assert len({r["golden"] for r in res}) == 1
 
 
-@pytest.mark.parametrize("world", [pytest.param(2, marks=WIDE), pytest.param(4, marks=WIDE)])
+@pytest.mark.parametrize("world", [2, pytest.param(4, marks=WIDE)])   # one default case
 def test_rccl_p2p_allreduce_captures_into_a_hip_graph(world):
     """One rank per process over RCCL (the product's process model), P > 1, under torch.cuda.graph: the
     ring and the width-P tree in the direct form and the ring in the reference's staged rounds, each captured
@@ -84,7 +84,7 @@ def test_rccl_p2p_random_soak(world):
         assert not r["fail"] and r["soak"] == 40, r
 
 
-@pytest.mark.parametrize("world,dtype", [pytest.param(2, "bf16", marks=WIDE), pytest.param(2, "f32", marks=WIDE),
+@pytest.mark.parametrize("world,dtype", [pytest.param(2, "bf16", marks=WIDE), (2, "f32"),   # one default
                                          pytest.param(4, "f32", marks=WIDE), pytest.param(4, "bf16", marks=WIDE)])
 def test_ddp_comm_hook_over_rccl(world, dtype):
     """torch DistributedDataParallel with ftar as the gradient AllReduce (ftar.ddp.allreduce_hook, one rank

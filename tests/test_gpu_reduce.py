@@ -141,7 +141,7 @@ def test_reduce_bf16_is_torch_fp32_fold_rounded_once(k):
     ref = acc.to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
     nan_g = (got & 0x7FFF) > 0x7F80
     nan_r = (ref & 0x7FFF) > 0x7F80
-    assert np.array_equal(nan_g, nan_r)                     # NaN exactly where torch has NaN (DESIGN §5)
+    assert np.array_equal(nan_g, nan_r)                     # NaN exactly where torch has NaN (DESIGN §7)
     assert np.array_equal(got[~nan_r], ref[~nan_r])
 
 

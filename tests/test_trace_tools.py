@@ -1,4 +1,4 @@
-"""The trace analyser behind DESIGN §6's engine_local numbers (tools/engine_local_trace.py), on a small synthetic
+"""The trace analyser behind DESIGN §9's engine_local numbers (tools/engine_local_trace.py), on a small synthetic
 rocprofv3 kernel trace whose answers are known: calls split at the marker kernels, span / busy / idle, fold
 time overlapped by transfers, per-stream gaps, the lead from a marker's end to the call's first kernel, and
 the HBM rate over the span."""

@@ -1,5 +1,5 @@
 // capture_probe — which multi-stream / multi-thread stream-capture patterns the
-// HIP runtime accepts (diagnostic for the in-process group capture, DESIGN §4).
+// HIP runtime accepts (diagnostic for the in-process group capture, DESIGN §5.5).
 // Each case runs in its own process (argv[1] = case), captures into one graph
 // from stream s0 (relaxed mode), instantiates, replays twice and checks the
 // data.  Prints "case N ok" or dies.

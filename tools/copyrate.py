@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""PCIe piece rates for the host path (DESIGN §6, next step #3): a 256 MiB bucket moved in pieces of
+"""PCIe piece rates for the host path (DESIGN §6): a 256 MiB bucket moved in pieces of
 1..64 MiB, one stream, by the runtime's copies (hipMemcpyAsync: SDMA for H2D, blit kernels for D2H on this
 image) and by ftar's own streaming copy kernel (ftar_reduce with k = 1) reading or writing the pinned host
 buffer directly over PCIe; then both directions at once on two streams.  Prints one JSON line per case."""

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Co-scheduling of the fold with the transport on one GPU (DESIGN §4): P in-process ranks on cuda:0, a
+"""Co-scheduling of the fold with the transport on one GPU (DESIGN §5.1): P in-process ranks on cuda:0, a
 width-P tree in the direct forms, the reduce stream limited to `reduce_cus` CUs (ftar_comm_set_reduce_cus)
 so the transport's copy kernels on the comm stream keep free CUs while a piece's fold runs.
 

@@ -52,6 +52,9 @@ for s in "${steps[@]}"; do
               run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --out gpurun_out/stress.jsonl ;;
     # one c4_host_read call on 8 processes, kernel + copy trace, for tools/host_order_check.py
     hbtrace) rm -f gpurun_out/pidmap.txt; FTAR_STRESS_PIDMAP=gpurun_out/pidmap.txt run hbtrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hbtrace -- python3 tools/host_comm_stress.py --config "${HB_CONFIG:-current}" --cycles 1 --cases c4_host_read --timeout 500 ;;
+    # engine_local under a kernel + copy trace, summarised per call (span, idle, fold time overlapped by transfers)
+    eltrace) run eltrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/eltrace -o el -- python3 bench.py --engine-local-only --steps 5 --warmup 2 &&
+             python3 tools/engine_local_trace.py gpurun_out/eltrace/el_kernel_trace.csv gpurun_out/eltrace/el_memory_copy_trace.csv --calls 7 --keep 5 --hbm-bytes 39728447488 > gpurun_out/eltrace_summary.json ;;
     dist1) run dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --force-dist --steps 5 --warmup 2 ;;
     *) echo "unknown step $s" ;;
   esac

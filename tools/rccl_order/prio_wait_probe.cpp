@@ -1,5 +1,5 @@
 // prio_wait_probe — does a stream wait on an event recorded after an H2D copy on a HIGH-PRIORITY stream
-// hold the waiting stream until the copy has landed?  (DESIGN §6, the host path's copy streams.)
+// hold the waiting stream until the copy has landed?  (DESIGN §6.4, the host path's copy streams.)
 //
 // Each iteration copies a pinned host buffer holding pattern i % 2 into one device buffer on the copy stream
 // (high priority, or plain for the control), records an event there, makes a plain stream wait on it and

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise bench.py N > 1 lines (a driver SCALE_rNN.json, or log files holding the JSON lines) into the
-calibration facts DESIGN §11 #1 asks for: per N the headline (form, topology, chunk, busBW, frac of the xGMI
+calibration facts DESIGN §13 #1 asks for: per N the headline (form, topology, chunk, busBW, frac of the xGMI
 spec and of the probe), the best RCCL p2p configuration beside it, the best validated entry of every form,
 the xGMI probe's link rates, the fitted cost model and C5's widths, host_e2e, and any RCCL failure or
 watchdog cut with the stage times.

@@ -11,7 +11,7 @@ spot check, so the stats average mixes them.  bench.py's launch order is fixed (
     k = 8:  2 untimed, 20 timed out of place, 20 timed in place
 
 This tool takes the dispatches of each kernel in start order and averages each phase, so the headline's
-kernel duration can be compared with the bench line's per-step time (DESIGN §6)."""
+kernel duration can be compared with the bench line's per-step time (DESIGN §9)."""
 import argparse
 import csv
 import json
