@@ -99,15 +99,18 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
         return FTAR_SUCCESS;
       }));
       FTAR_CHECK_HIP(hipEventRecord(ev_h(k), c->h2d_s));
+      FTAR_RETURN_IF(mark(c, "h2d " + std::to_string(k) + " done", c->h2d_s));
     }
     return FTAR_SUCCESS;
   };
   auto issue_d2h = [&](size_t k) -> ftar_status_t {  // piece k of the whole bucket, once it is final here
     FTAR_CHECK_HIP(hipStreamWaitEvent(d2h, ev_g(k), 0));
-    return for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
+    FTAR_RETURN_IF(mark(c, "d2h " + std::to_string(k) + " start", d2h));
+    FTAR_RETURN_IF(for_piece(k, [&](size_t lo2, size_t n) -> ftar_status_t {
       FTAR_CHECK_HIP(hipMemcpyAsync(io.dst + lo2 * esz, X + lo2 * esz, n * esz, hipMemcpyDeviceToHost, d2h));
       return FTAR_SUCCESS;
-    });
+    }));
+    return mark(c, "d2h " + std::to_string(k) + " done", d2h);
   };
   auto work = [&](auto&& fn) {
     if (st == FTAR_SUCCESS) st = fn();
@@ -148,10 +151,14 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   for (size_t k = 0; k < m; ++k) {
     const size_t lo = k * chunk;
     work([&]() -> ftar_status_t {
+      // phase timing (ftar_comm_set_phase_timing): every hand-off of the piece has a mark on its stream, the
+      // happens-before check of tools/host_order_check.py --marks
+      FTAR_RETURN_IF(mark(c, "fold " + std::to_string(k) + " start", c->comm_s));
       for (const ReduceItem& r : rs.reduces)
         FTAR_RETURN_IF(peer_fold(
             r, plan, dt, op, X + (r.off + lo) * esz, c->comm_s, c->peer_lds,
             [&](int q, size_t off) -> const void* { return (q < 0 ? X : Xq[q]) + off * esz; }, lo, chunk));
+      FTAR_RETURN_IF(mark(c, "fold " + std::to_string(k) + " done", c->comm_s));
       if (k + 1 < m) FTAR_CHECK_HIP(hipStreamWaitEvent(c->comm_s, ev_h(k + 1), 0));
       FTAR_RETURN_IF(issue_h2d(k + 1 + lookahead));  // after this fold's commands (see above)
       if (k > 0 && !d2h_host_order) FTAR_RETURN_IF(issue_d2h(k - 1));  // likewise
@@ -160,6 +167,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
     if (!sync()) return leave();  // piece k folded everywhere (and piece k+1 in)
     work([&]() -> ftar_status_t {
       if (k > 0 && d2h_host_order) FTAR_RETURN_IF(issue_d2h(k - 1));
+      FTAR_RETURN_IF(mark(c, "gather " + std::to_string(k) + " start", c->comm_s));
       segs.clear();
       for (const Transfer& x : ag.recvs)
         if (x.len > lo)
@@ -173,6 +181,7 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
           FTAR_RETURN_IF(peer_copy(c, segs));
         if (gather_fence == 1) FTAR_RETURN_IF(launch_noop(c->comm_s));
       }
+      FTAR_RETURN_IF(mark(c, "gather " + std::to_string(k) + " done", c->comm_s));
       FTAR_CHECK_HIP(hipEventRecord(ev_g(k), c->comm_s));
       return k + 1 == m && !d2h_host_order ? issue_d2h(k) : FTAR_SUCCESS;  // the others after the next fold
     });

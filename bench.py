@@ -1851,8 +1851,8 @@ def bench_distributed(a):
         ms = timed(fn_best, a.steps, a.warmup)
         ok, _ = check_y(fn_best)
         if ok and ms < ms_default:
-            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps", "cost_model_fit", "cost_model", "fallback_stream")
-                     if k in state["line"]}
+            carry = {k: state["line"][k] for k in ("xgmi_probe_GBps", "cost_model_fit", "cost_model", "fallback_stream",
+                                                   "c5_bf16", "host_e2e") if k in state["line"]}
             state["line"] = make_result(ms, best_topo, best["chunk_bytes"], best["form"], ok, a.steps, a.warmup,
                                         {"config_selection": "best validated configuration of the sweep",
                                          "default_config": default_info, "sweep": sweep, **carry})

@@ -69,6 +69,8 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                 x = xs[rank]
                 xs.clear()
                 comm.peer_direct = form
+                marks = host and os.environ.get("FTAR_STRESS_MARKS") == "1"
+                comm.phase_timing(marks)   # tools/host_order_check.py --marks: every hand-off's time
                 t0 = time.perf_counter()
                 if host:
                     h = x.cpu().pin_memory()
@@ -85,6 +87,7 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                     ms = (time.perf_counter() - t0) * 1e3
                     del x
                 ran = comm.last_exec()["form"]
+                phases = comm.last_phases() if marks else None
                 bad = None
                 if whole_fold.first_mismatch(y, exp) is not None:
                     xs = inputs(world, n, tdt, seed, dev)
@@ -108,7 +111,7 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                     if pages or len(fps[owner]) != len(allfp[owner][owner]):
                         maps.append({"owner": owner, "pages": pages[:16], "npages": len(pages)})
                 out["results"].append({"name": name, "cycle": cyc, "ran": ran, "bad": bad, "maps": maps,
-                                       "ms": round(ms, 2)})
+                                       "ms": round(ms, 2), **({"phases": phases} if phases else {})})
                 if rank == 0 and cycles > 1:
                     print(f"cycle {cyc} {name}: {ms:.1f} ms, {'BAD' if bad else 'ok'}", flush=True)
         dist.barrier()

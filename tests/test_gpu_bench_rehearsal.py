@@ -44,7 +44,8 @@ def test_bench_n_gt_1_rehearsal(ranks, extra):
     assert d["c5_bf16"]["check"] == "ok", d["c5_bf16"]
     assert "ms" in d["bucket_256MiB"], d["bucket_256MiB"]
     assert d["xgmi_probe_GBps"]["read_all_peers"][0] > 0
-    assert set(d["stage_wall_s"]) >= {"init", "default", "sweep", "headline", "C5 bf16", "host e2e"}, d["stage_wall_s"]
+    assert set(d["stage_wall_s"]) >= {"init", "default", "sweep core", "headline", "C5 bf16", "host e2e"}, d["stage_wall_s"]
+    assert "stages_skipped_for_budget" in d and d["budget_s"] > 0, d.get("stages_skipped_for_budget")
     if not extra:   # RCCL refused the shared GPU on every rank and every rank fell back
         assert "rccl_init_error" in d
         assert [e["rank"] for e in d["rccl_error_by_rank"]] == list(range(ranks)), d["rccl_error_by_rank"]

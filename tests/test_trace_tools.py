@@ -118,3 +118,27 @@ def test_host_order_check_on_known_calls(tmp_path):
     assert r.returncode == 1
     v = json.loads(r.stdout)["edges"]["gather->d2h"]
     assert v["nviolations"] == 3 and {x["rank"] for x in v["violations"]} == {1} and {x["piece"] for x in v["violations"]} == {2}
+
+
+def test_host_order_check_from_the_engines_marks(tmp_path):
+    """--marks: the local hand-off edges of peer_allreduce_host from its phase-timing marks (ms since the call's
+    start), one JSON line per rank-call as tools/host_comm_stress.py writes them; one late D2H is found."""
+    def phases(late=None):
+        ph = [["start", 0.0]]
+        for k in range(3):
+            t = 10.0 * k
+            ph += [[f"h2d {k} done", t + 1], [f"fold {k} start", t + 2], [f"fold {k} done", t + 3],
+                   [f"gather {k} start", t + 4], [f"gather {k} done", t + 5],
+                   [f"d2h {k} start", t + (4.5 if late == k else 6)], [f"d2h {k} done", t + 7]]
+        return ph + [["barrier", 40.0]]
+    good = tmp_path / "good.jsonl"
+    good.write_text("\n".join(json.dumps({"rank": r, "name": "c4_host_read", "phases": phases()}) for r in range(4)) + "\n")
+    r = subprocess.run([sys.executable, HOST_ORDER, "--marks", str(good)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout)
+    assert d["ok"] and d["calls"] == 4
+    assert d["edges"]["gather->d2h"]["count"] == 12 and d["edges"]["gather->d2h"]["min_slack_us"] == 1000.0
+    bad = tmp_path / "bad.jsonl"
+    bad.write_text(json.dumps({"rank": 0, "phases": phases(late=1)}) + "\n")
+    r = subprocess.run([sys.executable, HOST_ORDER, "--marks", str(bad)], capture_output=True, text=True)
+    assert r.returncode == 1 and json.loads(r.stdout)["edges"]["gather->d2h"]["nviolations"] == 1

@@ -21,6 +21,11 @@ Edges (reader start - writer end = slack; a negative slack is a violation):
   fold->d2h        fold(r,k) -> D2H(r,k)[o(r)]                     (D2H of r's own block)
   d2h->next_h2d    none: a later piece's H2D never touches piece k
 Prints a JSON summary (per edge: count, min slack in us, violations) and exits 1 on any violation.
+
+    python3 tools/host_order_check.py --marks gpurun_out/stress.jsonl
+
+checks the local edges of every rank-call from the engine's own hand-off marks instead (phase timing, recorded
+by tools/host_comm_stress.py under FTAR_STRESS_MARKS=1), with no profiler.
 """
 import argparse
 import csv
@@ -117,7 +122,67 @@ def check(ranks, topo):
     return edges
 
 
+def check_marks(phases):
+    """The same edges inside one rank from the engine's own hand-off marks (phase timing: each mark is the time its
+    stream reached it, in ms since the call's start on the same device): H2D(k) done before my fold(k) starts, my
+    fold(k) done before my gather(k) starts, my gather(k) done before my D2H(k) starts, every D2H done before the
+    call's last barrier.  The cross-process edges are host barriers and need no clock."""
+    t = {}
+    for name, ms in phases:
+        t[name] = ms
+    ks = sorted(int(n.split()[1]) for n in t if n.startswith("gather ") and n.endswith(" done"))
+    edges = {}
+
+    def edge(name, w, r, k):
+        if w not in t or r not in t:
+            return
+        sl = (t[r] - t[w]) * 1e3   # us
+        e = edges.setdefault(name, {"count": 0, "min_slack_us": None, "violations": []})
+        e["count"] += 1
+        e["min_slack_us"] = sl if e["min_slack_us"] is None else min(e["min_slack_us"], sl)
+        if sl < 0:
+            e["violations"].append({"piece": k, "slack_us": round(sl, 3)})
+    for k in ks:
+        edge("h2d->fold", f"h2d {k} done", f"fold {k} start", k)
+        edge("fold->gather", f"fold {k} done", f"gather {k} start", k)
+        edge("gather->d2h", f"gather {k} done", f"d2h {k} start", k)
+        edge("d2h->last barrier", f"d2h {k} done", "barrier", k)
+    for e in edges.values():
+        e["min_slack_us"] = round(e["min_slack_us"], 3)
+        e["nviolations"] = len(e["violations"])
+    return {"pieces": len(ks), "edges": edges, "ok": bool(ks) and all(e["nviolations"] == 0 for e in edges.values())}
+
+
+def main_marks(path, out):
+    """every rank-call of a host_comm_stress.py --out file run with FTAR_STRESS_MARKS=1"""
+    res = {"calls": 0, "ok": True, "edges": {}}
+    with open(path) as f:
+        for ln in f:
+            d = json.loads(ln)
+            if not d.get("phases"):
+                continue
+            c = check_marks(d["phases"])
+            res["calls"] += 1
+            res["ok"] = res["ok"] and c["ok"]
+            for name, e in c["edges"].items():
+                a = res["edges"].setdefault(name, {"count": 0, "min_slack_us": None, "nviolations": 0})
+                a["count"] += e["count"]
+                a["nviolations"] += e["nviolations"]
+                a["min_slack_us"] = e["min_slack_us"] if a["min_slack_us"] is None else min(a["min_slack_us"], e["min_slack_us"])
+    res["ok"] = res["ok"] and res["calls"] > 0
+    s = json.dumps(res, indent=1)
+    print(s)
+    if out:
+        with open(out, "w") as f:
+            f.write(s + "\n")
+    return 0 if res["ok"] else 1
+
+
 def main():
+    if "--marks" in sys.argv:   # host_order_check.py --marks stress.jsonl [--out f]
+        i = sys.argv.index("--marks")
+        out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else ""
+        return main_marks(sys.argv[i + 1], out)
     ap = argparse.ArgumentParser()
     ap.add_argument("trace_dir")
     ap.add_argument("--pidmap", required=True, help="lines 'rank pid' (FTAR_STRESS_PIDMAP)")
