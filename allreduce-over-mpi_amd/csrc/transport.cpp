@@ -819,6 +819,18 @@ class LocalTransport final : public Transport {
     // hand every message taken so far back to its sender: with its stream's copies-done event, or none if
     // this rank failed (the sender then fails too, at once, instead of waiting out the timeout)
     auto publish = [&](ftar_status_t st) -> ftar_status_t {
+      if (st != FTAR_SUCCESS) {
+        // a failed flush hands the senders their messages back only once the copies it already enqueued from
+        // them have finished, so a failed sender that returns at once may free or reuse its buffer;
+        // the receiving streams wait only on the senders' data-ready events, recorded before the senders wait
+        // for anything of this flush, so these synchronisations end
+        std::vector<hipStream_t> seen;
+        for (auto& x : got)
+          if (std::find(seen.begin(), seen.end(), x.second) == seen.end()) {
+            seen.push_back(x.second);
+            hip_ignore(hipStreamSynchronize(x.second));
+          }
+      }
       for (auto& x : got) {
         Ev* e = per_stream(done, x.second);
         if (st != FTAR_SUCCESS || *e) continue;

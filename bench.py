@@ -742,11 +742,13 @@ DIST_STAGES = [
 
 class StageClock:
     """Time accounting of DIST_STAGES against the run's budget (FTAR_BENCH_BUDGET_S, which the watchdog
-    enforces): `margin` seconds are kept for printing the line."""
+    enforces): `margin` seconds are kept for printing the line; the reserves, sized for the default 300 s, shrink
+    with a smaller budget (a rehearsal's 100 s keeps every stage)."""
 
-    def __init__(self, budget, t0, now=time.time, stages=DIST_STAGES, margin=10.0):
+    def __init__(self, budget, t0, now=time.time, stages=DIST_STAGES, margin=10.0, budget_ref=300.0):
         self.budget, self.t0, self.now, self.margin = budget, t0, now, margin
-        self.stages = list(stages)
+        f = min(1.0, budget / budget_ref)
+        self.stages = [(n, req, r * f) for n, req, r in stages]
         self.names = [st[0] for st in self.stages]
         self.skipped = {}
 

@@ -483,8 +483,13 @@ def test_n_gt_1_stage_order_and_budget_with_synthetic_stage_times():
         if times.get("sweep rest") == 1e9:                              # an endless sweep is cut at its limit
             assert used["sweep rest"][0] == used["sweep rest"][1]
             assert "reference cpu/mpi" not in ran and "reference cpu/mpi" in clock.skipped
-    # a budget too small for the probe: skipped, and the required stages still all run
+    # a run that reaches the probe with 60 s of its 300 left: the probe is skipped (C5, host e2e, the refit and
+    # the headline need its time), the required stages all run, and what they leave goes to the sweep's rest
     clk = _FakeTime()
-    clock = bench.StageClock(100.0, 0.0, now=clk)
+    clock = bench.StageClock(300.0, 0.0, now=clk)
+    clk.t = 230.0
     ran = bench.run_stage_plan(clock, {n: (lambda lim: None) for n in names})
-    assert "xgmi probe" not in ran and set(req) <= set(ran)
+    assert "xgmi probe" not in ran and "xgmi probe" in clock.skipped and set(req) <= set(ran) and "sweep rest" in ran
+    # a rehearsal's small budget scales the reserves down: at its start every stage still fits
+    clock = bench.StageClock(100.0, 0.0, now=_FakeTime())
+    assert bench.run_stage_plan(clock, {n: (lambda lim: None) for n in names}) == names

@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--calls", type=int, default=7)
     ap.add_argument("--keep", type=int, default=5)
     ap.add_argument("--hbm-bytes", type=float, default=0.0)
+    ap.add_argument("--first", action="store_true",
+                    help="the calls follow the FIRST `calls` markers (engine_local's default configuration, before "
+                         "its whole-block and peer-read sub-runs add markers of their own), not the last")
     a = ap.parse_args()
     # the engine's own work only: ftar's kernels (folds, copies) and the runtime's copies (the input setup
     # and the sample check around the timed calls are torch kernels)
@@ -84,7 +87,10 @@ def main():
         ops += load(a.copy_csv, "copy")
     ops.sort(key=lambda o: o["s"])
     if len(marks) >= a.calls:   # the calls lie between consecutive markers (the last one: up to the next torch op)
-        bounds = marks[-a.calls:] + [max(o["e"] for o in ops) + 1]
+        if a.first:
+            bounds = marks[:a.calls] + [marks[a.calls] if len(marks) > a.calls else max(o["e"] for o in ops) + 1]
+        else:
+            bounds = marks[-a.calls:] + [max(o["e"] for o in ops) + 1]
         calls = [[o for o in ops if lo <= o["s"] < hi] for lo, hi in zip(bounds, bounds[1:])]
         # the last call ends where its ops stop: drop anything after a gap wider than the call itself
         last = calls[-1]

@@ -57,7 +57,7 @@ for s in "${steps[@]}"; do
     hbtrace) rm -f gpurun_out/pidmap.txt; FTAR_STRESS_PIDMAP=gpurun_out/pidmap.txt run hbtrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/hbtrace -- python3 tools/host_comm_stress.py --config "${HB_CONFIG:-current}" --cycles 1 --cases c4_host_read --timeout 500 ;;
     # engine_local under a kernel + copy trace, summarised per call (span, idle, fold time overlapped by transfers)
     eltrace) run eltrace 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/eltrace -o el -- python3 bench.py --engine-local-only --steps 5 --warmup 2 &&
-             python3 tools/engine_local_trace.py gpurun_out/eltrace/el_kernel_trace.csv gpurun_out/eltrace/el_memory_copy_trace.csv --calls 7 --keep 5 --hbm-bytes 39728447488 > gpurun_out/eltrace_summary.json ;;
+             python3 tools/engine_local_trace.py gpurun_out/eltrace/el_kernel_trace.csv $(ls gpurun_out/eltrace/el_memory_copy_trace.csv 2>/dev/null) --first --calls 7 --keep 5 --hbm-bytes 39728447488 > gpurun_out/eltrace_summary.json ;;
     # the N > 1 line at P = 8 over RCCL loopback sockets on one GPU, at the driver's default budget (300 s)
     dist8lb) run dist8lb 420 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29561 bench.py --rccl-loopback --steps 3 --warmup 1 --elements 4194304 --elements-c5 4194304 --no-cpu-baseline --save-cost gpurun_out/node.cost &&
              grep '^{' gpurun_out/dist8lb.log > gpurun_out/dist8.json && python3 tools/scale_report.py gpurun_out/dist8.json > gpurun_out/dist8_report.txt ;;
