@@ -396,6 +396,8 @@ bool comm_teardown(ftar_comm* c) {
   for (auto e : c->tev) hip_ignore(hipEventDestroy(e));
   if (c->scratch) hip_ignore(hipFree(c->scratch));
   if (c->staging) hip_ignore(hipFree(c->staging));
+  if (c->glog.host) hip_ignore(hipHostFree(c->glog.host));
+  if (c->glog.dev) hip_ignore(hipFree(c->glog.dev));
   for (hipStream_t st : {c->comm_s, c->red_s, c->h2d_s, c->d2h_s})
     if (st) hip_ignore(hipStreamDestroy(st));
   return true;

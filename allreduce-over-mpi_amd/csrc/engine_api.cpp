@@ -3,6 +3,7 @@
 // behaviour change.
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -371,6 +372,34 @@ ftar_status_t ftar_debug_exchange_buffer(ftar_comm_t comm, int peer, void** ptr,
   if (!comm->xbuf || comm->xpeers.size() != (size_t)comm->nranks) return FTAR_SUCCESS;
   *ptr = peer == comm->rank ? comm->xbuf : comm->xpeers[(size_t)peer];
   *bytes = comm->xbuf_bytes;
+  return FTAR_SUCCESS;
+}
+
+// Test hook (not in ftar.h): the gather records of piece `piece` of the last host-path call made
+// under FTAR_DEBUG_HOST_GATHER_LOG=1 -- host_rec: 4 words per workgroup in host memory, dev_rec: 1 word per
+// workgroup in device memory (reduce_impl.h gather_logged_kernel) -- and info[4 + 2 * FTAR_MAX_K] = {pieces
+// logged, grid, segments, tile bytes, each segment's destination offset in the exchange buffer, its bytes}.
+// Read them only after the call completed.
+ftar_status_t ftar_debug_gather_log(ftar_comm_t comm, size_t piece, const unsigned** host_rec,
+                                    const unsigned** dev_rec, size_t* info) {
+  if (!comm || !host_rec || !dev_rec || !info) return FTAR_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> g(comm->mu);
+  const auto& L = comm->glog;
+  std::fill(info, info + 4 + 2 * FTAR_MAX_K, size_t(0));
+  info[0] = L.pieces.size();
+  *host_rec = nullptr;
+  *dev_rec = nullptr;
+  if (piece >= L.pieces.size()) return FTAR_SUCCESS;
+  const auto& p = L.pieces[piece];
+  *host_rec = L.host + 4 * p.first;
+  *dev_rec = L.dev + p.first;
+  info[1] = p.geom.grid;
+  info[2] = p.geom.nsegs;
+  info[3] = p.geom.tile_bytes;
+  for (unsigned j = 0; j < p.geom.nsegs; ++j) {
+    info[4 + j] = p.off[j];
+    info[4 + FTAR_MAX_K + j] = p.bytes[j];
+  }
   return FTAR_SUCCESS;
 }
 

@@ -25,6 +25,47 @@ size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
   return std::max<size_t>({64, (chunk_bytes / esz) & ~size_t(63), (floor_elems + 63) & ~size_t(63)});
 }
 
+// FTAR_DEBUG_HOST_GATHER_LOG (diagnostic): the gather of piece k with one record per workgroup
+// (launch_gather_logged), read back by ftar_debug_gather_log.  The call's records are cleared at its piece 0,
+// after the host waited for the comm stream (no gather of an earlier call still writes them); room for m
+// pieces of piece 0's grid.  Always the copy kernel (peer_dma is not consulted).
+static ftar_status_t log_gather(ftar_comm* c, const std::vector<Segment>& segs, const char* X, size_t k, size_t m) {
+  ftar_comm::GatherLog& L = c->glog;
+  const GatherGeom g = gather_geometry(segs.data(), (int)segs.size(), c->peer_wg_cap);
+  if (k == 0) {
+    FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
+    const size_t need = m * (size_t)g.grid;
+    if (need > L.cap) {
+      if (L.host) FTAR_CHECK_HIP(hipHostFree(L.host));
+      if (L.dev) FTAR_CHECK_HIP(hipFree(L.dev));
+      L.host = nullptr;
+      L.dev = nullptr;
+      L.cap = 0;
+      FTAR_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&L.host), need * 4 * sizeof(unsigned),
+                                   hipHostMallocCoherent));
+      FTAR_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&L.dev), need * sizeof(unsigned)));
+      L.cap = need;
+    }
+    memset(L.host, 0, L.cap * 4 * sizeof(unsigned));
+    FTAR_CHECK_HIP(hipMemsetAsync(L.dev, 0, L.cap * sizeof(unsigned), c->comm_s));
+    L.pieces.clear();
+  }
+  ftar_comm::GatherLog::Piece p{};
+  p.first = L.pieces.empty() ? 0 : L.pieces.back().first + L.pieces.back().geom.grid;
+  p.geom = g;
+  if (p.first + g.grid > L.cap) return FTAR_ERR_INTERNAL;
+  size_t j = 0;
+  for (const Segment& s : segs)
+    if (s.bytes) {
+      p.off[j] = (size_t)(static_cast<const char*>(s.dst) - X);
+      p.bytes[j++] = s.bytes;
+    }
+  FTAR_RETURN_IF(launch_gather_logged(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt, c->peer_wg_cap,
+                                      L.host + 4 * p.first, L.dev + p.first, L.cap - p.first));
+  L.pieces.push_back(p);
+  return FTAR_SUCCESS;
+}
+
 // Host buffers on a communicator without point-to-point transfers (ftar_comm_init_host: the MPI
 // drop-in's `ipc` transport), the read form piece by piece, as the p2p host path pipelines its
 // stages.  Piece k is elements [k*chunk, (k+1)*chunk) of every block.
@@ -71,6 +112,9 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   // the gather of piece k complete (after the next barrier) instead of waiting for its event on the device
   static const bool d2h_host_order =
       getenv("FTAR_DEBUG_HOST_D2H_ORDER") && !strcmp(getenv("FTAR_DEBUG_HOST_D2H_ORDER"), "host");
+  // FTAR_DEBUG_HOST_GATHER_LOG=1 (diagnostic): each gather workgroup leaves a record of where and when it
+  // ran (launch_gather_logged; ftar_debug_gather_log reads them after the call)
+  static const bool gather_log = getenv("FTAR_DEBUG_HOST_GATHER_LOG") && atoi(getenv("FTAR_DEBUG_HOST_GATHER_LOG"));
   // Every rank goes through all m + 2 barriers whatever fails locally: `st` keeps this rank's first
   // failure, the work after it is skipped, and each barrier tells every rank whether any rank failed,
   // so all of them leave the call at the same barrier instead of some waiting in the next.
@@ -174,7 +218,9 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
           segs.push_back(
               {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
       if (!segs.empty()) {
-        if (gather_fence == 2 || gather_fence == 3)
+        if (gather_log)
+          FTAR_RETURN_IF(log_gather(c, segs, X, k, m));
+        else if (gather_fence == 2 || gather_fence == 3)
           FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, gather_fence == 2 && c->peer_nt,
                                        c->peer_wg_cap, gather_fence == 2));
         else

@@ -96,6 +96,19 @@ struct ftar_comm {
   std::vector<hipEvent_t> tev;
   std::vector<std::string> tnames;
   size_t nmarks = 0;
+  // FTAR_DEBUG_HOST_GATHER_LOG (diagnostic, engine_host.cpp): one record per gather workgroup of
+  // the last host-path call (launch_gather_logged), and each piece's launch geometry
+  struct GatherLog {
+    unsigned* host = nullptr;  // pinned host memory, 4 words per workgroup
+    unsigned* dev = nullptr;   // device memory, 1 word per workgroup
+    size_t cap = 0;            // workgroups both hold
+    struct Piece {
+      size_t first;            // the piece's first record
+      ftar::GatherGeom geom;
+      size_t off[FTAR_MAX_K], bytes[FTAR_MAX_K];  // each segment's destination, bytes from the exchange buffer
+    };
+    std::vector<Piece> pieces;
+  } glog;
   // completion marker of the previous call, recorded on that call's stream after it joined every internal
   // stream: a call on a different stream waits for it (scratch, staging and exchange buffers are shared)
   hipEvent_t done_ev = nullptr;

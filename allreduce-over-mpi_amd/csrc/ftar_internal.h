@@ -177,6 +177,17 @@ struct Segment {
 // memory before it retires (the host path's gather -> D2H hand-off).
 ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt = true,
                             size_t max_wg_per_seg = 0, bool release_system = false);
+// launch_gather's launch for these segments: its workgroups, the segments with bytes (packed in order) and
+// the bytes one workgroup copies per pass over a segment (workgroup w copies tiles w / nsegs + j * grid /
+// nsegs of segment w % nsegs)
+struct GatherGeom {
+  unsigned grid = 0, nsegs = 0, tile_bytes = 0;
+};
+GatherGeom gather_geometry(const Segment* segs, int nsegs, size_t max_wg_per_seg);
+// Diagnostic: launch_gather (no release) whose workgroups each leave a record when they end --
+// 4 words in host_log, 1 in dev_log (reduce_impl.h gather_logged_kernel); cap_wg: records that fit
+ftar_status_t launch_gather_logged(const Segment* segs, int nsegs, hipStream_t stream, bool nt,
+                                   size_t max_wg_per_seg, unsigned* host_log, unsigned* dev_log, size_t cap_wg);
 // An empty kernel: a stream-order point after the kernel before it (diagnostics).
 ftar_status_t launch_noop(hipStream_t stream);
 // One local device copy (k = 1 reduces, the P = 1 AllReduce, the peer forms' local copy-in/out): the

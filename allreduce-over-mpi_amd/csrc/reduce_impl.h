@@ -676,8 +676,8 @@ struct SegArgs {
   size_t bytes[FTAR_MAX_K];
 };
 
-template <bool NT, bool REL = false>
-__global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
+template <bool NT>
+__device__ __forceinline__ void gather_body(const SegArgs& a, int m) {
   const int sgi = (int)(blockIdx.x % (unsigned)m);
   const size_t bid = blockIdx.x / (unsigned)m, nb = gridDim.x / (unsigned)m;
   const char* src = a.src[sgi];
@@ -687,7 +687,6 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
   const uintptr_t ms = reinterpret_cast<uintptr_t>(src) & 15, md = reinterpret_cast<uintptr_t>(dst) & 15;
   if (ms != md) {
     for (size_t i = tid; i < n; i += nthr) dst[i] = src[i];
-    if constexpr (REL) __threadfence_system();
     return;
   }
   size_t head = ms ? 16 - ms : 0;
@@ -705,7 +704,38 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
     st16<NT>(d4 + v + kThreads, x1);
   }
   if (v < nvec) st16<NT>(d4 + v, ld16<NT>(s4 + v));
+}
+
+template <bool NT, bool REL = false>
+__global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
+  gather_body<NT>(a, m);
   if constexpr (REL) __threadfence_system();  // this workgroup's stores reach memory before it retires
+}
+
+// Diagnostic (engine_host.cpp FTAR_DEBUG_HOST_GATHER_LOG): the gather, and when every wave of
+// the workgroup has issued its stores, one record of where and when it ran -- in host memory (fine-grained:
+// the store goes past the GPU caches) {0x80000000 | XCD, HW_ID (CU, SIMD, queue, pipe), wall clock at start,
+// at end} and one word {0x80000000 | XCD} in device memory through the caches like the data.  A tile whose
+// data is missing while its workgroup's host record is present ran to its end; a missing device word beside
+// a present host record is a store of that workgroup lost after it issued.
+template <bool NT>
+__global__ void __launch_bounds__(kThreads) gather_logged_kernel(SegArgs a, int m, unsigned* host_log,
+                                                                 unsigned* dev_log) {
+  const unsigned t0 = (unsigned)wall_clock64();
+  gather_body<NT>(a, m);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // s_getreg: HW_REG_XCC_ID (20) bits [3:0], HW_REG_HW_ID (4) whole
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11)) & 15u;
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));
+    const unsigned t1 = (unsigned)wall_clock64();
+    unsigned* h = host_log + 4 * (size_t)blockIdx.x;
+    h[0] = 0x80000000u | xcc;
+    h[1] = hw;
+    h[2] = t0;
+    h[3] = t1;
+    dev_log[blockIdx.x] = 0x80000000u | xcc;
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -29,25 +29,44 @@ bool dtype_op_supported(ftar_dtype_t dt, ftar_op_t op) {
   return false;
 }
 
+namespace {
+// the segments with bytes, packed, and the grid: workgroups per segment to cover the largest in one pass
+// (at most 65535, then grid-stride; max_wg_per_seg caps it), times the segments
+GatherGeom pack_segments(const Segment* segs, int nsegs, size_t max_wg_per_seg, SegArgs* a) {
+  GatherGeom g;
+  size_t most = 0;
+  for (int i = 0; i < nsegs; ++i) {
+    if (!segs[i].bytes) continue;
+    a->src[g.nsegs] = static_cast<const char*>(segs[i].src);
+    a->dst[g.nsegs] = static_cast<char*>(segs[i].dst);
+    a->bytes[g.nsegs] = segs[i].bytes;
+    most = std::max(most, segs[i].bytes);
+    ++g.nsegs;
+  }
+  if (!g.nsegs) return g;
+  size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
+  bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
+  if (max_wg_per_seg) bx = std::min(bx, max_wg_per_seg);
+  g.grid = (unsigned)(bx * (size_t)g.nsegs);
+  g.tile_bytes = 2 * kThreads * 16;
+  return g;
+}
+}  // namespace
+
+GatherGeom gather_geometry(const Segment* segs, int nsegs, size_t max_wg_per_seg) {
+  if (nsegs < 0 || nsegs > FTAR_MAX_K) return GatherGeom{};
+  SegArgs a{};
+  return pack_segments(segs, nsegs, max_wg_per_seg, &a);
+}
+
 ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, bool nt, size_t max_wg_per_seg,
                             bool release_system) {
   if (nsegs < 0 || nsegs > FTAR_MAX_K) return FTAR_ERR_INVALID_ARG;
   SegArgs a{};
-  int m = 0;
-  size_t most = 0;
-  for (int i = 0; i < nsegs; ++i) {
-    if (!segs[i].bytes) continue;
-    a.src[m] = static_cast<const char*>(segs[i].src);
-    a.dst[m] = static_cast<char*>(segs[i].dst);
-    a.bytes[m] = segs[i].bytes;
-    most = std::max(most, segs[i].bytes);
-    ++m;
-  }
-  if (!m) return FTAR_SUCCESS;
-  size_t bx = (most / 16 + 2 * kThreads - 1) / (2 * kThreads);
-  bx = std::max<size_t>(1, std::min<size_t>(bx, 65535));  // per segment; grid-stride beyond
-  if (max_wg_per_seg) bx = std::min(bx, max_wg_per_seg);
-  const dim3 grid((unsigned)(bx * (size_t)m));
+  const GatherGeom g = pack_segments(segs, nsegs, max_wg_per_seg, &a);
+  if (!g.nsegs) return FTAR_SUCCESS;
+  const int m = (int)g.nsegs;
+  const dim3 grid(g.grid);
   if (release_system && nt)
     FTAR_LAUNCH((gather_kernel<true, true>), grid, dim3(kThreads), 0, stream, a, m);
   else if (release_system)
@@ -56,6 +75,22 @@ ftar_status_t launch_gather(const Segment* segs, int nsegs, hipStream_t stream, 
     FTAR_LAUNCH(gather_kernel<true>, grid, dim3(kThreads), 0, stream, a, m);
   else
     FTAR_LAUNCH(gather_kernel<false>, grid, dim3(kThreads), 0, stream, a, m);
+  FTAR_CHECK_HIP(hipGetLastError());
+  return FTAR_SUCCESS;
+}
+
+ftar_status_t launch_gather_logged(const Segment* segs, int nsegs, hipStream_t stream, bool nt,
+                                   size_t max_wg_per_seg, unsigned* host_log, unsigned* dev_log, size_t cap_wg) {
+  if (nsegs < 0 || nsegs > FTAR_MAX_K || !host_log || !dev_log) return FTAR_ERR_INVALID_ARG;
+  SegArgs a{};
+  const GatherGeom g = pack_segments(segs, nsegs, max_wg_per_seg, &a);
+  if (!g.nsegs) return FTAR_SUCCESS;
+  if (g.grid > cap_wg) return FTAR_ERR_INVALID_ARG;  // one record per workgroup must fit
+  const int m = (int)g.nsegs;
+  if (nt)
+    FTAR_LAUNCH(gather_logged_kernel<true>, dim3(g.grid), dim3(kThreads), 0, stream, a, m, host_log, dev_log);
+  else
+    FTAR_LAUNCH(gather_logged_kernel<false>, dim3(g.grid), dim3(kThreads), 0, stream, a, m, host_log, dev_log);
   FTAR_CHECK_HIP(hipGetLastError());
   return FTAR_SUCCESS;
 }

@@ -53,6 +53,7 @@ STATUS = {0: "success", 1: "invalid argument", 2: "unsupported", 3: "invalid FT_
           4: "HIP error", 5: "RCCL error", 6: "internal error", 7: "timeout",
           8: "out of device memory"}
 MAX_STAGES = 16
+MAX_K = 64          # FTAR_MAX_K (ftar.h): sources of one reduce, segments of one gather
 _TORCH_DTYPE_NAMES = {"torch.float32": "f32", "torch.float64": "f64", "torch.bfloat16": "bf16", "torch.int32": "i32",
                       "torch.int64": "i64", "torch.int16": "i16", "torch.int8": "i8", "torch.uint8": "u8",
                       "torch.bool": "bool", "torch.uint16": "u16"}
@@ -162,6 +163,7 @@ _lib.ftar_debug_set_peer_dma.argtypes = [_vp, _int]
 _lib.ftar_debug_set_rccl_register.argtypes = [_vp, _int]
 _lib.ftar_debug_set_peer_wg_cap.argtypes = [_vp, _sz]
 _lib.ftar_debug_exchange_buffer.argtypes = [_vp, _int, ctypes.POINTER(_vp), ctypes.POINTER(_sz)]
+_lib.ftar_debug_gather_log.argtypes = [_vp, _sz, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_sz)]
 _lib.ftar_comm_get_peer_direct.argtypes = [_vp, ctypes.POINTER(_int)]
 _lib.ftar_xgmi_probe.argtypes = [_vp, _sz, _int, ctypes.POINTER(ctypes.c_double), _int]
 _lib.ftar_debug_xgmi_probe_cap.argtypes = [_vp, _sz, _int, _sz, ctypes.POINTER(ctypes.c_double), _int]
@@ -646,6 +648,25 @@ class Comm:
         _check(_lib.ftar_debug_exchange_buffer(self.handle, int(peer), ctypes.byref(p), ctypes.byref(n)),
                "exchange_buffer")
         return (p.value or 0), n.value
+
+    def gather_log(self, piece):
+        """Test hook (ftar_debug_gather_log): the gather records of piece `piece` of the last host
+        call made under FTAR_DEBUG_HOST_GATHER_LOG=1, or None past the pieces logged.  A dict: pieces (logged),
+        grid, nsegs, tile_bytes, off / bytes (each segment's destination in the exchange buffer), host (a
+        numpy uint32 [grid, 4]: 0x80000000 | XCD, HW_ID, wall clock at start, at end; all 0 if the workgroup
+        left no record) and dev_ptr (device address of grid uint32 words, 0x80000000 | XCD)."""
+        import numpy as np
+        h, d = _vp(), _vp()
+        info = (_sz * (4 + 2 * MAX_K))()
+        _check(_lib.ftar_debug_gather_log(self.handle, int(piece), ctypes.byref(h), ctypes.byref(d), info),
+               "gather_log")
+        if not h.value:
+            return None
+        grid, nsegs = int(info[1]), int(info[2])
+        host = np.frombuffer(ctypes.string_at(h.value, grid * 16), dtype=np.uint32).reshape(grid, 4).copy()
+        return {"pieces": int(info[0]), "grid": grid, "nsegs": nsegs, "tile_bytes": int(info[3]),
+                "off": [int(info[4 + j]) for j in range(nsegs)],
+                "bytes": [int(info[4 + MAX_K + j]) for j in range(nsegs)], "host": host, "dev_ptr": d.value}
 
     @property
     def reduce_cus(self):

@@ -86,6 +86,8 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                     torch.cuda.synchronize()
                     ms = (time.perf_counter() - t0) * 1e3
                     del x
+                glog = gather_forensics(comm, y, exp, tdt) if host and os.environ.get(
+                    "FTAR_DEBUG_HOST_GATHER_LOG") == "1" else None
                 ran = comm.last_exec()["form"]
                 phases = comm.last_phases() if marks else None
                 bad = None
@@ -111,7 +113,8 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
                     if pages or len(fps[owner]) != len(allfp[owner][owner]):
                         maps.append({"owner": owner, "pages": pages[:16], "npages": len(pages)})
                 out["results"].append({"name": name, "cycle": cyc, "ran": ran, "bad": bad, "maps": maps,
-                                       "ms": round(ms, 2), **({"phases": phases} if phases else {})})
+                                       "ms": round(ms, 2), **({"phases": phases} if phases else {}),
+                                       **({"gather_log": glog} if glog else {})})
                 if rank == 0 and cycles > 1:
                     print(f"cycle {cyc} {name}: {ms:.1f} ms, {'BAD' if bad else 'ok'}", flush=True)
         dist.barrier()
@@ -121,6 +124,90 @@ def worker(rank, world, port, q, cases, cycles=1, seed=6161, env=None):
         import traceback
         out["error"] = traceback.format_exc()
     q.put((rank, out))
+
+
+def hw_fields(hw):
+    """HW_REG_HW_ID (gfx9 layout) -> the fields that say where a wave ran."""
+    return {"me": (hw >> 30) & 3, "pipe": (hw >> 6) & 3, "queue": (hw >> 24) & 7, "se": (hw >> 13) & 7,
+            "cu": (hw >> 8) & 15}
+
+
+def gather_forensics(comm, y, exp, tdt, read_dev=None):
+    """The gather records of the last host call (FTAR_DEBUG_HOST_GATHER_LOG=1, engine_host.cpp log_gather):
+    which workgroups left a record in host memory (past the GPU caches) and in device memory (through them),
+    on which XCD and hardware queue they ran, and -- when the result is wrong -- the same for the workgroups
+    that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
+    Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
+    -> numpy uint32 reads the device records (default: hipMemcpy)."""
+    import collections
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    iv = {torch.float32: torch.int32, torch.bfloat16: torch.int16}[tdt]
+    esz = torch.tensor([], dtype=tdt).element_size()
+    ne = y.view(iv) != exp.view(iv)
+    if read_dev is None:
+        import gpu_util
+        hip = gpu_util.hip_runtime()
+
+        def read_dev(ptr, words):
+            buf = np.zeros(words, dtype=np.uint32)
+            assert hip.hipMemcpy(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(ptr),
+                                 ctypes.c_size_t(words * 4), 2) == 0
+            return buf
+    out = {"pieces": 0, "wgs": 0, "host_missing": 0, "dev_missing": 0, "xcc_is_w_mod_8": 0, "queues": {},
+           "bad": []}
+    k = 0
+    while True:
+        g = comm.gather_log(k)
+        if g is None:
+            break
+        out["pieces"] = g["pieces"]
+        grid, m, tile = g["grid"], g["nsegs"], g["tile_bytes"]
+        dev = read_dev(g["dev_ptr"], grid)
+        h = g["host"]
+        present_h = (h[:, 0] & 0x80000000) != 0
+        present_d = (dev & 0x80000000) != 0
+        xcc = h[:, 0] & 15
+        w = np.arange(grid)
+        out["wgs"] += grid
+        out["host_missing"] += int((~present_h).sum())
+        out["dev_missing"] += int((~present_d).sum())
+        out["xcc_is_w_mod_8"] += int((present_h & (xcc == w % 8)).sum())
+        for hw in h[present_h, 1]:
+            f = hw_fields(int(hw))
+            key = f"me{f['me']}.pipe{f['pipe']}.q{f['queue']}"
+            out["queues"][key] = out["queues"].get(key, 0) + 1
+        # the workgroups that own wrong tiles
+        nb = grid // m
+        te = tile // esz
+        bad_w = collections.Counter()
+        for j in range(m):
+            lo, cnt = g["off"][j] // esz, g["bytes"][j] // esz
+            seg = ne[lo:lo + cnt]
+            nt = -(-cnt // te)
+            pad = torch.zeros(nt * te, dtype=torch.bool, device=ne.device)
+            pad[:cnt] = seg
+            for t in torch.nonzero(pad.view(nt, te).any(1)).flatten().tolist():
+                bad_w[(t % nb) * m + j] += 1
+        if bad_w:
+            ws = np.array(sorted(bad_w))
+            t0 = int(h[present_h, 2].min()) if present_h.any() else 0
+            span = (int(h[present_h, 3].max()) - t0) if present_h.any() else 0
+            ends = [(int(h[x, 3]) - t0) for x in ws if present_h[x]]
+            out["bad"].append({
+                "piece": k, "grid": grid, "nsegs": m, "bad_wgs": int(len(ws)), "bad_tiles": int(sum(bad_w.values())),
+                "host_present": int(present_h[ws].sum()), "dev_present": int(present_d[ws].sum()),
+                "xcc": dict(collections.Counter(int(x) for x in xcc[ws][present_h[ws]])),
+                "w_mod_8": dict(collections.Counter(int(x) % 8 for x in ws)),
+                "queues": dict(collections.Counter(
+                    "me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(x))) for x in h[ws, 1][present_h[ws]])),
+                "end_ticks_of_bad": [min(ends), max(ends)] if ends else None, "piece_span_ticks": span,
+                "first_wgs": [int(x) for x in ws[:8]]})
+        k += 1
+    return out
 
 
 def exchange_at(comm, bad, n, piece, tdt, exp, mine, poison):
@@ -196,7 +283,9 @@ def failures(res, world=8):
             if x["bad"] is not None:
                 lines.append(f"{tag}: {whole_fold.describe(x['bad'])}"
                              + (f"; exchange buffer there now: {x['bad']['exchange_now']}"
-                                if x["bad"].get("exchange_now") else ""))
+                                if x["bad"].get("exchange_now") else "")
+                             + (f"; gather records of the bad pieces: {x['gather_log']['bad']}"
+                                if x.get("gather_log") else ""))
             for mm in x["maps"]:
                 lines.append(f"{tag}: mapping of rank {mm['owner']}'s exchange buffer differs from the owner's "
                              f"view in {mm['npages']} 2 MiB pages, first {mm['pages']}")

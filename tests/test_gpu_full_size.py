@@ -177,6 +177,23 @@ def test_host_comm_peer_forms_full_size_whole_bucket():
         assert [x["name"] for x in res[r]["results"]] == [c[0] for c in cases], r
 
 
+def test_host_comm_gather_records():
+    """The diagnostic gather of the host path (FTAR_DEBUG_HOST_GATHER_LOG=1) gives the same result
+    and leaves one record per workgroup in host and in device memory, naming an XCD 0-7."""
+    import host_comm_cases as hc
+    res = hc.run([("c4_host_read", 1 << 24, "f32", "1", "read", True)], world=2,
+                 env={"FTAR_DEBUG_HOST_GATHER_LOG": "1"})
+    bad = hc.failures(res, world=2)
+    assert not bad, "\n".join(bad)
+    for r in range(2):
+        g = res[r]["results"][0]["gather_log"]
+        print(r, {k: v for k, v in g.items() if k != "bad"})
+        # 64 MiB, 2 ranks: 32 MiB blocks in 4 MiB pieces, each piece one 4 MiB segment of 512 workgroups
+        assert g["pieces"] == 8 and g["wgs"] == 8 * 512, g
+        assert g["host_missing"] == 0 and g["dev_missing"] == 0 and g["bad"] == [], g
+        assert sum(g["queues"].values()) == g["wgs"], g
+
+
 @pytest.mark.parametrize("topo", ["1", "2"])
 def test_allreduce_at_mpi_max_count_fp32(topo):
     """The largest bucket MPI_Allreduce_FT's `int count` can name (mpi_mod.hpp:1724): 2^31 - 1 fp32 elements

@@ -47,6 +47,8 @@ for s in "${steps[@]}"; do
              run hostipc4 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29539 tools/host_ipc_rate.py --sizes 24,26 --topo 4 ;;
     hosttests) run pytest_host 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_host_transport.py tests/test_harness.py -m gpu ;;
     hostcomm) run pytest_hostcomm 600 python -u -m pytest -x -v --timeout 400 --timeout-method thread -p no:cacheprovider tests/test_gpu_full_size.py -k host_comm -m gpu ;;
+    # the diagnostic gather's records on 2 ranks, and the IPC host pipeline's timing test
+    glogtests) run pytest_glog 400 python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_full_size.py::test_host_comm_gather_records tests/test_harness.py::test_harness_ipc_host_pipeline_beats_whole_bucket_copies -m gpu ;;
     # stress_<config>[@cycles]: tools/host_comm_stress.py under one of its configurations
     stress_*) cfg=${s#stress_}; cyc=${cfg#*@}; [ "$cyc" = "$cfg" ] && cyc=${STRESS_CYCLES:-8}; cfg=${cfg%@*}
               run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --out gpurun_out/stress.jsonl ;;

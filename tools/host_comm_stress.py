@@ -13,7 +13,7 @@ Configurations (environment of every rank; engine.cpp ensure_host_streams, engin
            D2H on the host D2H stream (FTAR_DEBUG_HOST_D2H_STREAM=1); prio / upfront / d2hs one of those each
   r5_*     r5 with a change at the gather -> D2H hand-off (FTAR_DEBUG_HOST_GATHER_FENCE): an empty kernel
            after the gather (noop), a system-scope release ending every gather workgroup (fence), temporal
-           stores in the gather (temporal)
+           stores in the gather (temporal); r5_log / log: a record per gather workgroup (gather_forensics)
 Writes one JSON line per (rank, cycle, case) and prints a summary; exit status 1 if anything was wrong.
 """
 import argparse
@@ -42,6 +42,10 @@ CONFIGS = {
     "prio_d2hs": {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1", "FTAR_DEBUG_HOST_D2H_STREAM": "1"},
     "prio_upfront": {"FTAR_DEBUG_HOST_COPY_PRIORITY": "1", "FTAR_DEBUG_HOST_LOOKAHEAD": "1000"},
     "r5_hostorder": dict(R5, FTAR_DEBUG_HOST_D2H_ORDER="host"),
+    # a record per gather workgroup (FTAR_DEBUG_HOST_GATHER_LOG): where and when each ran, and whether its
+    # last store reached host memory (past the caches) and device memory (through them)
+    "log": {"FTAR_DEBUG_HOST_GATHER_LOG": "1"},
+    "r5_log": dict(R5, FTAR_DEBUG_HOST_GATHER_LOG="1"),
 }
 
 
@@ -72,9 +76,19 @@ def main():
     for r in res:
         for x in res[r].get("results", []):
             ms.setdefault(x["name"], []).append(x["ms"])
+    glog = {}
+    for r in res:
+        for x in res[r].get("results", []):
+            for key, v in x.get("gather_log", {}).items():
+                if key in ("wgs", "host_missing", "dev_missing", "xcc_is_w_mod_8"):
+                    glog[key] = glog.get(key, 0) + v
+                elif key == "queues":
+                    for q, c in v.items():
+                        glog.setdefault("queues", {})[q] = glog.get("queues", {}).get(q, 0) + c
     print(json.dumps({"config": a.config, "cycles": a.cycles, "cases": [c[0] for c in cases],
                       "problems": len(lines), "seconds": round(time.time() - t0, 1),
-                      "median_ms": {k: sorted(v)[len(v) // 2] for k, v in ms.items()}}))
+                      "median_ms": {k: sorted(v)[len(v) // 2] for k, v in ms.items()},
+                      **({"gather_log": glog} if glog else {})}))
     for ln in lines:
         print(ln)
     return 1 if lines else 0
