@@ -158,7 +158,7 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
                                  ctypes.c_size_t(words * 4), 2) == 0
             return buf
     out = {"pieces": 0, "wgs": 0, "host_missing": 0, "dev_missing": 0, "xcc_is_w_mod_8": 0, "queues": {},
-           "bad": []}
+           "split_pieces": 0, "bad": []}
     k = 0
     while True:
         g = comm.gather_log(k)
@@ -176,10 +176,12 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
         out["host_missing"] += int((~present_h).sum())
         out["dev_missing"] += int((~present_d).sum())
         out["xcc_is_w_mod_8"] += int((present_h & (xcc == w % 8)).sum())
-        for hw in h[present_h, 1]:
-            f = hw_fields(int(hw))
-            key = f"me{f['me']}.pipe{f['pipe']}.q{f['queue']}"
-            out["queues"][key] = out["queues"].get(key, 0) + 1
+        pq = collections.Counter("me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(hw))) for hw in h[present_h, 1])
+        for key, c in pq.items():
+            out["queues"][key] = out["queues"].get(key, 0) + c
+        # one dispatch whose workgroups ran from more than one hardware queue slot: the queue was unmapped
+        # (preempted) and mapped again part-way through the launch
+        out["split_pieces"] += len(pq) > 1
         # the workgroups that own wrong tiles
         nb = grid // m
         te = tile // esz
@@ -197,6 +199,9 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
             t0 = int(h[present_h, 2].min()) if present_h.any() else 0
             span = (int(h[present_h, 3].max()) - t0) if present_h.any() else 0
             ends = [(int(h[x, 3]) - t0) for x in ws if present_h[x]]
+            ph = np.nonzero(present_h)[0]
+            starts = np.sort(h[ph, 2].astype(np.int64) - t0)
+            gaps = np.diff(starts)
             out["bad"].append({
                 "piece": k, "grid": grid, "nsegs": m, "bad_wgs": int(len(ws)), "bad_tiles": int(sum(bad_w.values())),
                 "host_present": int(present_h[ws].sum()), "dev_present": int(present_d[ws].sum()),
@@ -205,7 +210,15 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
                 "queues": dict(collections.Counter(
                     "me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(x))) for x in h[ws, 1][present_h[ws]])),
                 "end_ticks_of_bad": [min(ends), max(ends)] if ends else None, "piece_span_ticks": span,
-                "first_wgs": [int(x) for x in ws[:8]]})
+                "first_wgs": [int(x) for x in ws[:8]],
+                # the piece's workgroups that did run: their queue slots, XCD - w mod 8 (the dispatch's
+                # rotation over the XCDs), end times (percentiles 0/50/90/99/100) and the largest pause
+                # between two consecutive workgroup starts, in wall-clock ticks (100 MHz)
+                "piece_queues": dict(pq),
+                "rotation": dict(collections.Counter(int(x) for x in (xcc[ph].astype(np.int64) - ph) % 8)),
+                "end_pct": [int(v) for v in np.percentile(h[ph, 3].astype(np.int64) - t0, [0, 50, 90, 99, 100])]
+                if len(ph) else None,
+                "largest_start_gap": int(gaps.max()) if len(gaps) else None})
         k += 1
     return out
 

@@ -58,6 +58,8 @@ def test_wrong_tiles_name_their_workgroups_and_xcd():
     assert b["piece"] == 1 and b["first_wgs"] == [4] and b["bad_tiles"] == 2
     assert b["xcc"] == {4: 1} and b["w_mod_8"] == {4: 1} and b["host_present"] == 1 and b["dev_present"] == 0
     assert b["end_ticks_of_bad"] == [104, 104] and b["piece_span_ticks"] == 105
+    assert b["piece_queues"] == {"me1.pipe0.q2": 6} and b["rotation"] == {0: 6} and b["largest_start_gap"] == 1
+    assert b["end_pct"][0] == 100 and b["end_pct"][-1] == 105 and out["split_pieces"] == 0
 
 
 def test_right_result_lists_no_bad_piece():
@@ -66,4 +68,8 @@ def test_right_result_lists_no_bad_piece():
     exp = torch.arange(n, dtype=torch.float32)
     out = hc.gather_forensics(comm, exp.clone(), exp, torch.float32,
                               read_dev=lambda ptr, words: comm.records[ptr]["dev"])
-    assert out["bad"] == [] and out["host_missing"] == 0 and out["dev_missing"] == 0
+    assert out["bad"] == [] and out["host_missing"] == 0 and out["dev_missing"] == 0 and out["split_pieces"] == 0
+    comm.records[0]["host"][5, 1] = (1 << 30) | (5 << 24) | 64     # one workgroup ran from another queue slot
+    out = hc.gather_forensics(comm, exp.clone(), exp, torch.float32,
+                              read_dev=lambda ptr, words: comm.records[ptr]["dev"])
+    assert out["split_pieces"] == 1 and out["queues"] == {"me1.pipe0.q2": 11, "me1.pipe1.q5": 1}
