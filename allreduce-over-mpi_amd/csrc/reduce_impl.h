@@ -713,11 +713,10 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
 }
 
 // Diagnostic (engine_host.cpp FTAR_DEBUG_HOST_GATHER_LOG): the gather, and when every wave of
-// the workgroup has issued its stores, one record of where and when it ran -- in host memory (fine-grained:
-// the store goes past the GPU caches) {0x80000000 | XCD, HW_ID (CU, SIMD, queue, pipe), wall clock at start,
-// at end} and one word {0x80000000 | XCD} in device memory through the caches like the data.  A tile whose
-// data is missing while its workgroup's host record is present ran to its end; a missing device word beside
-// a present host record is a store of that workgroup lost after it issued.
+// the workgroup has issued its stores, one record of where and when it ran in host memory (fine-grained, not
+// held in the GPU caches) {0x80000000 | XCD, HW_ID (CU, SIMD, queue, pipe), wall clock at start, at end}, and
+// a device-scope atomic increment of its workgroup id's word in device memory: that word counts how many
+// times a workgroup with this id ran (0: never; 2: an id handed out twice).
 template <bool NT>
 __global__ void __launch_bounds__(kThreads) gather_logged_kernel(SegArgs a, int m, unsigned* host_log,
                                                                  unsigned* dev_log) {
@@ -734,7 +733,7 @@ __global__ void __launch_bounds__(kThreads) gather_logged_kernel(SegArgs a, int 
     h[1] = hw;
     h[2] = t0;
     h[3] = t1;
-    dev_log[blockIdx.x] = 0x80000000u | xcc;
+    atomicAdd(dev_log + blockIdx.x, 1u);
   }
 }
 

@@ -134,9 +134,9 @@ def hw_fields(hw):
 
 def gather_forensics(comm, y, exp, tdt, read_dev=None):
     """The gather records of the last host call (FTAR_DEBUG_HOST_GATHER_LOG=1, engine_host.cpp log_gather):
-    which workgroups left a record in host memory (past the GPU caches) and in device memory (through them),
-    on which XCD and hardware queue they ran, and -- when the result is wrong -- the same for the workgroups
-    that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
+    which workgroups left a record in host memory (not held in the GPU caches), how many times each workgroup
+    id ran (a device-scope counter per id: 0 never, 2 handed out twice), on which XCD and hardware queue they
+    ran, and -- when the result is wrong -- the same for the workgroups that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
     Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
     -> numpy uint32 reads the device records (default: hipMemcpy)."""
     import collections
@@ -157,8 +157,8 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
             assert hip.hipMemcpy(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(ptr),
                                  ctypes.c_size_t(words * 4), 2) == 0
             return buf
-    out = {"pieces": 0, "wgs": 0, "host_missing": 0, "dev_missing": 0, "xcc_is_w_mod_8": 0, "queues": {},
-           "split_pieces": 0, "bad": []}
+    out = {"pieces": 0, "wgs": 0, "host_missing": 0, "dev_missing": 0, "runs": 0, "ids_run_twice": 0,
+           "xcc_is_w_mod_8": 0, "queues": {}, "split_pieces": 0, "bad": []}
     k = 0
     while True:
         g = comm.gather_log(k)
@@ -169,12 +169,14 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
         dev = read_dev(g["dev_ptr"], grid)
         h = g["host"]
         present_h = (h[:, 0] & 0x80000000) != 0
-        present_d = (dev & 0x80000000) != 0
+        present_d = dev != 0
         xcc = h[:, 0] & 15
         w = np.arange(grid)
         out["wgs"] += grid
         out["host_missing"] += int((~present_h).sum())
         out["dev_missing"] += int((~present_d).sum())
+        out["runs"] += int(dev.astype(np.int64).sum())
+        out["ids_run_twice"] += int((dev > 1).sum())
         out["xcc_is_w_mod_8"] += int((present_h & (xcc == w % 8)).sum())
         pq = collections.Counter("me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(hw))) for hw in h[present_h, 1])
         for key, c in pq.items():
@@ -205,6 +207,9 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
             out["bad"].append({
                 "piece": k, "grid": grid, "nsegs": m, "bad_wgs": int(len(ws)), "bad_tiles": int(sum(bad_w.values())),
                 "host_present": int(present_h[ws].sum()), "dev_present": int(present_d[ws].sum()),
+                # workgroups that ran in this launch, counted by id: grid - bad_wgs if the missing ones never
+                # ran, grid if their ids went to other workgroups (then some ids ran twice)
+                "piece_runs": int(dev.astype(np.int64).sum()), "piece_ids_run_twice": int((dev > 1).sum()),
                 "xcc": dict(collections.Counter(int(x) for x in xcc[ws][present_h[ws]])),
                 "w_mod_8": dict(collections.Counter(int(x) % 8 for x in ws)),
                 "queues": dict(collections.Counter(

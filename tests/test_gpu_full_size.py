@@ -179,7 +179,7 @@ def test_host_comm_peer_forms_full_size_whole_bucket():
 
 def test_host_comm_gather_records():
     """The diagnostic gather of the host path (FTAR_DEBUG_HOST_GATHER_LOG=1) gives the same result
-    and leaves one record per workgroup in host and in device memory, naming an XCD 0-7."""
+    and leaves one record per workgroup in host memory, and every workgroup id ran exactly once."""
     import host_comm_cases as hc
     res = hc.run([("c4_host_read", 1 << 24, "f32", "1", "read", True)], world=2,
                  env={"FTAR_DEBUG_HOST_GATHER_LOG": "1"})
@@ -191,6 +191,7 @@ def test_host_comm_gather_records():
         # 64 MiB, 2 ranks: 32 MiB blocks in 4 MiB pieces, each piece one 4 MiB segment of 512 workgroups
         assert g["pieces"] == 8 and g["wgs"] == 8 * 512, g
         assert g["host_missing"] == 0 and g["dev_missing"] == 0 and g["bad"] == [], g
+        assert g["runs"] == g["wgs"] and g["ids_run_twice"] == 0, g
         assert sum(g["queues"].values()) == g["wgs"], g
 
 

@@ -80,7 +80,8 @@ def main():
     for r in res:
         for x in res[r].get("results", []):
             for key, v in x.get("gather_log", {}).items():
-                if key in ("wgs", "host_missing", "dev_missing", "xcc_is_w_mod_8", "split_pieces"):
+                if key in ("wgs", "host_missing", "dev_missing", "runs", "ids_run_twice", "xcc_is_w_mod_8",
+                           "split_pieces"):
                     glog[key] = glog.get(key, 0) + v
                 elif key == "queues":
                     for q, c in v.items():
