@@ -377,7 +377,8 @@ ftar_status_t ftar_debug_exchange_buffer(ftar_comm_t comm, int peer, void** ptr,
 
 // Test hook (not in ftar.h): the gather records of piece `piece` of the last host-path call made
 // under FTAR_DEBUG_HOST_GATHER_LOG=1 -- host_rec: 4 words per workgroup in host memory, dev_rec: per workgroup
-// id the number of times it ran, in device memory (reduce_impl.h gather_logged_kernel) -- and info[4 + 2 * FTAR_MAX_K] = {pieces
+// id the number of times it ran and the XCDs it ran on, 2 words in device memory (reduce_impl.h
+// gather_logged_kernel) -- and info[4 + 2 * FTAR_MAX_K] = {pieces
 // logged, grid, segments, tile bytes, each segment's destination offset in the exchange buffer, its bytes}.
 // Read them only after the call completed.
 ftar_status_t ftar_debug_gather_log(ftar_comm_t comm, size_t piece, const unsigned** host_rec,
@@ -392,7 +393,7 @@ ftar_status_t ftar_debug_gather_log(ftar_comm_t comm, size_t piece, const unsign
   if (piece >= L.pieces.size()) return FTAR_SUCCESS;
   const auto& p = L.pieces[piece];
   *host_rec = L.host + 4 * p.first;
-  *dev_rec = L.dev + p.first;
+  *dev_rec = L.dev + 2 * p.first;
   info[1] = p.geom.grid;
   info[2] = p.geom.nsegs;
   info[3] = p.geom.tile_bytes;

@@ -43,11 +43,11 @@ static ftar_status_t log_gather(ftar_comm* c, const std::vector<Segment>& segs, 
       L.cap = 0;
       FTAR_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(&L.host), need * 4 * sizeof(unsigned),
                                    hipHostMallocCoherent));
-      FTAR_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&L.dev), need * sizeof(unsigned)));
+      FTAR_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&L.dev), need * 2 * sizeof(unsigned)));
       L.cap = need;
     }
     memset(L.host, 0, L.cap * 4 * sizeof(unsigned));
-    FTAR_CHECK_HIP(hipMemsetAsync(L.dev, 0, L.cap * sizeof(unsigned), c->comm_s));
+    FTAR_CHECK_HIP(hipMemsetAsync(L.dev, 0, L.cap * 2 * sizeof(unsigned), c->comm_s));
     L.pieces.clear();
   }
   ftar_comm::GatherLog::Piece p{};
@@ -61,7 +61,7 @@ static ftar_status_t log_gather(ftar_comm* c, const std::vector<Segment>& segs, 
       p.bytes[j++] = s.bytes;
     }
   FTAR_RETURN_IF(launch_gather_logged(segs.data(), (int)segs.size(), c->comm_s, c->peer_nt, c->peer_wg_cap,
-                                      L.host + 4 * p.first, L.dev + p.first, L.cap - p.first));
+                                      L.host + 4 * p.first, L.dev + 2 * p.first, L.cap - p.first));
   L.pieces.push_back(p);
   return FTAR_SUCCESS;
 }

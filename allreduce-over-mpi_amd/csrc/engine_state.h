@@ -100,7 +100,7 @@ struct ftar_comm {
   // the last host-path call (launch_gather_logged), and each piece's launch geometry
   struct GatherLog {
     unsigned* host = nullptr;  // pinned host memory, 4 words per workgroup
-    unsigned* dev = nullptr;   // device memory, 1 word per workgroup: how many times it ran
+    unsigned* dev = nullptr;   // device memory, 2 words per workgroup: how many times it ran, on which XCDs
     size_t cap = 0;            // workgroups both hold
     struct Piece {
       size_t first;            // the piece's first record

@@ -185,8 +185,8 @@ struct GatherGeom {
 };
 GatherGeom gather_geometry(const Segment* segs, int nsegs, size_t max_wg_per_seg);
 // Diagnostic: launch_gather (no release) whose workgroups each leave a record when they end --
-// 4 words in host_log, and a count of its runs in dev_log (reduce_impl.h gather_logged_kernel); cap_wg: records
-// that fit
+// 4 words in host_log, and a count of its runs and the XCDs they ran on in dev_log (2 words; reduce_impl.h
+// gather_logged_kernel); cap_wg: records that fit
 ftar_status_t launch_gather_logged(const Segment* segs, int nsegs, hipStream_t stream, bool nt,
                                    size_t max_wg_per_seg, unsigned* host_log, unsigned* dev_log, size_t cap_wg);
 // An empty kernel: a stream-order point after the kernel before it (diagnostics).

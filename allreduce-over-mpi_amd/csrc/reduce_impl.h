@@ -715,8 +715,8 @@ __global__ void __launch_bounds__(kThreads) gather_kernel(SegArgs a, int m) {
 // Diagnostic (engine_host.cpp FTAR_DEBUG_HOST_GATHER_LOG): the gather, and when every wave of
 // the workgroup has issued its stores, one record of where and when it ran in host memory (fine-grained, not
 // held in the GPU caches) {0x80000000 | XCD, HW_ID (CU, SIMD, queue, pipe), wall clock at start, at end}, and
-// a device-scope atomic increment of its workgroup id's word in device memory: that word counts how many
-// times a workgroup with this id ran (0: never; 2: an id handed out twice).
+// two device-scope atomics on its workgroup id's pair of words in device memory: how many times a workgroup
+// with this id ran (0: never; 2: the id handed out twice) and the set of XCDs it ran on (bit x: XCD x).
 template <bool NT>
 __global__ void __launch_bounds__(kThreads) gather_logged_kernel(SegArgs a, int m, unsigned* host_log,
                                                                  unsigned* dev_log) {
@@ -733,7 +733,8 @@ __global__ void __launch_bounds__(kThreads) gather_logged_kernel(SegArgs a, int 
     h[1] = hw;
     h[2] = t0;
     h[3] = t1;
-    atomicAdd(dev_log + blockIdx.x, 1u);
+    atomicAdd(dev_log + 2 * (size_t)blockIdx.x, 1u);
+    atomicOr(dev_log + 2 * (size_t)blockIdx.x + 1, 1u << xcc);
   }
 }
 

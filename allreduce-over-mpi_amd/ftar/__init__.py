@@ -654,7 +654,8 @@ class Comm:
         call made under FTAR_DEBUG_HOST_GATHER_LOG=1, or None past the pieces logged.  A dict: pieces (logged),
         grid, nsegs, tile_bytes, off / bytes (each segment's destination in the exchange buffer), host (a
         numpy uint32 [grid, 4]: 0x80000000 | XCD, HW_ID, wall clock at start, at end; all 0 if the workgroup
-        left no record) and dev_ptr (device address of grid uint32 words: how many times each workgroup id ran)."""
+        left no record) and dev_ptr (device address of grid x 2 uint32 words: how many times each workgroup id ran,
+        and the XCDs it ran on as a bit set)."""
         import numpy as np
         h, d = _vp(), _vp()
         info = (_sz * (4 + 2 * MAX_K))()

@@ -135,10 +135,10 @@ def hw_fields(hw):
 def gather_forensics(comm, y, exp, tdt, read_dev=None):
     """The gather records of the last host call (FTAR_DEBUG_HOST_GATHER_LOG=1, engine_host.cpp log_gather):
     which workgroups left a record in host memory (not held in the GPU caches), how many times each workgroup
-    id ran (a device-scope counter per id: 0 never, 2 handed out twice), on which XCD and hardware queue they
-    ran, and -- when the result is wrong -- the same for the workgroups that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
+    id ran and on which XCDs (device-scope counters per id: 0 never, 2 handed out twice), on which XCD and
+    hardware queue they ran, and -- when the result is wrong -- the same for the workgroups that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
     Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
-    -> numpy uint32 reads the device records (default: hipMemcpy)."""
+    -> numpy uint32 reads the device records (2 words per workgroup; default: hipMemcpy)."""
     import collections
     import ctypes
 
@@ -166,7 +166,8 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
             break
         out["pieces"] = g["pieces"]
         grid, m, tile = g["grid"], g["nsegs"], g["tile_bytes"]
-        dev = read_dev(g["dev_ptr"], grid)
+        devw = read_dev(g["dev_ptr"], 2 * grid)
+        dev, dmask = devw[0::2], devw[1::2]
         h = g["host"]
         present_h = (h[:, 0] & 0x80000000) != 0
         present_d = dev != 0
@@ -210,6 +211,10 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
                 # workgroups that ran in this launch, counted by id: grid - bad_wgs if the missing ones never
                 # ran, grid if their ids went to other workgroups (then some ids ran twice)
                 "piece_runs": int(dev.astype(np.int64).sum()), "piece_ids_run_twice": int((dev > 1).sum()),
+                # the ids that ran twice: their classes mod 8, and the XCD sets they ran on
+                "twice_w_mod_8": dict(collections.Counter(int(x) % 8 for x in np.nonzero(dev > 1)[0])),
+                "twice_xcds": dict(collections.Counter(
+                    ",".join(str(b) for b in range(8) if int(mk) >> b & 1) for mk in dmask[dev > 1])),
                 "xcc": dict(collections.Counter(int(x) for x in xcc[ws][present_h[ws]])),
                 "w_mod_8": dict(collections.Counter(int(x) % 8 for x in ws)),
                 "queues": dict(collections.Counter(

@@ -25,9 +25,14 @@ class FakeComm:
             host = np.zeros((grid, 4), dtype=np.uint32)
             for w in range(grid):
                 host[w] = [0x80000000 | (w % 8), (1 << 30) | (2 << 24) | (w % 4), 100 + w, 200 + w]
-            dev = np.ones(grid, dtype=np.uint32)          # how many times each workgroup id ran
-            if dev_lost and p == 1:
-                dev[[w for w in range(grid) if w % 8 == lost_xcc]] = 0
+            dev = np.zeros(2 * grid, dtype=np.uint32)     # per id: how many times it ran, on which XCDs
+            dev[0::2] = 1
+            dev[1::2] = [1 << (w % 8) for w in range(grid)]
+            if dev_lost and p == 1:   # id lost_xcc never ran; id lost_xcc - 4's workgroups ran it a second time
+                dev[2 * lost_xcc] = 0
+                dev[2 * lost_xcc + 1] = 0
+                dev[2 * (lost_xcc - 4)] = 2
+                dev[2 * (lost_xcc - 4) + 1] |= 1 << lost_xcc
             self.records.append({"pieces": 2, "grid": grid, "nsegs": m, "tile_bytes": TILE,
                                  "off": [(s * 10 + p * 4) * TILE for s in range(m)], "bytes": [4 * TILE] * m,
                                  "host": host, "dev_ptr": p, "dev": dev})
@@ -57,7 +62,8 @@ def test_wrong_tiles_name_their_workgroups_and_xcd():
     [b] = out["bad"]
     assert b["piece"] == 1 and b["first_wgs"] == [4] and b["bad_tiles"] == 2
     assert b["xcc"] == {4: 1} and b["w_mod_8"] == {4: 1} and b["host_present"] == 1 and b["dev_present"] == 0
-    assert b["piece_runs"] == 5 and b["piece_ids_run_twice"] == 0 and out["runs"] == 11
+    assert b["piece_runs"] == 6 and b["piece_ids_run_twice"] == 1 and out["runs"] == 12
+    assert b["twice_w_mod_8"] == {0: 1} and b["twice_xcds"] == {"0,4": 1}
     assert b["end_ticks_of_bad"] == [104, 104] and b["piece_span_ticks"] == 105
     assert b["piece_queues"] == {"me1.pipe0.q2": 6} and b["rotation"] == {0: 6} and b["largest_start_gap"] == 1
     assert b["end_pct"][0] == 100 and b["end_pct"][-1] == 105 and out["split_pieces"] == 0
