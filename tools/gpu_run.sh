@@ -50,8 +50,10 @@ for s in "${steps[@]}"; do
     # the diagnostic gather's records on 2 ranks, and the IPC host pipeline's timing test
     glogtests) run pytest_glog 400 python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_full_size.py::test_host_comm_gather_records tests/test_harness.py::test_harness_ipc_host_pipeline_beats_whole_bucket_copies -m gpu ;;
     # the ftar-free reproducer of DESIGN §6.4: 8 worker processes, copy streams at the highest priority, then plain
-    xcdprobe) run xcdprobe 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --timeout 280 --out gpurun_out/xcd_probe.jsonl &&
-              run xcdprobe_plain 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --plain --timeout 280 --out gpurun_out/xcd_probe.jsonl ;;
+    xcdprobe) run xcdprobe 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --timeout 280 --out gpurun_out/xcd_probe.jsonl ${XCD_ARGS:-} &&
+              run xcdprobe_plain 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --plain --timeout 280 --out gpurun_out/xcd_probe.jsonl ${XCD_ARGS:-} ;;
+    # the same with the highest priority only, under the settings in XCD_ARGS (no plain control)
+    xcdhi) run xcdhi 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --timeout 280 --out gpurun_out/xcd_probe.jsonl ${XCD_ARGS:-} ;;
     # stress_<config>[@cycles]: tools/host_comm_stress.py under one of its configurations
     stress_*) cfg=${s#stress_}; cyc=${cfg#*@}; [ "$cyc" = "$cfg" ] && cyc=${STRESS_CYCLES:-8}; cfg=${cfg%@*}
               run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --out gpurun_out/stress.jsonl ;;
