@@ -26,13 +26,13 @@ size_t host_peer_piece(const ftar_comm* c, size_t split, size_t esz) {
 }
 
 // FTAR_DEBUG_HOST_GATHER_LOG (diagnostic): the gather of piece k with one record per workgroup
-// (launch_gather_logged), read back by ftar_debug_gather_log.  The call's records are cleared at its piece 0,
-// after the host waited for the comm stream (no gather of an earlier call still writes them); room for m
-// pieces of piece 0's grid.  Always the copy kernel (peer_dma is not consulted).
-static ftar_status_t log_gather(ftar_comm* c, const std::vector<Segment>& segs, const char* X, size_t k, size_t m) {
+// (launch_gather_logged), read back by ftar_debug_gather_log.  The records are cleared at the call's first
+// logged gather (`first`), after the host waited for the comm stream (no gather of an earlier call still
+// writes them); room for m pieces of that gather's grid.  Always the copy kernel (peer_dma is not consulted).
+static ftar_status_t log_gather(ftar_comm* c, const std::vector<Segment>& segs, const char* X, bool first, size_t m) {
   ftar_comm::GatherLog& L = c->glog;
   const GatherGeom g = gather_geometry(segs.data(), (int)segs.size(), c->peer_wg_cap);
-  if (k == 0) {
+  if (first) {
     FTAR_CHECK_HIP(hipStreamSynchronize(c->comm_s));
     const size_t need = m * (size_t)g.grid;
     if (need > L.cap) {
@@ -192,6 +192,8 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
   if (!sync()) return leave();  // piece 0 is in everywhere
   work([&] { return mark(c, "piece 0 in", c->comm_s); });
   std::vector<Segment> segs;
+  bool logged = false;                    // FTAR_DEBUG_HOST_GATHER_LOG: this call logged a gather
+  if (gather_log) c->glog.pieces.clear();  // no records of an earlier call stay readable
   for (size_t k = 0; k < m; ++k) {
     const size_t lo = k * chunk;
     work([&]() -> ftar_status_t {
@@ -218,13 +220,15 @@ ftar_status_t peer_allreduce_host(const HostIO& io, size_t count, ftar_dtype_t d
           segs.push_back(
               {Xq[x.peer] + (x.off + lo) * esz, X + (x.off + lo) * esz, std::min(chunk, x.len - lo) * esz});
       if (!segs.empty()) {
-        if (gather_log)
-          FTAR_RETURN_IF(log_gather(c, segs, X, k, m));
-        else if (gather_fence == 2 || gather_fence == 3)
+        if (gather_log) {
+          FTAR_RETURN_IF(log_gather(c, segs, X, !logged, m));
+          logged = true;
+        } else if (gather_fence == 2 || gather_fence == 3) {
           FTAR_RETURN_IF(launch_gather(segs.data(), (int)segs.size(), c->comm_s, gather_fence == 2 && c->peer_nt,
                                        c->peer_wg_cap, gather_fence == 2));
-        else
+        } else {
           FTAR_RETURN_IF(peer_copy(c, segs));
+        }
         if (gather_fence == 1) FTAR_RETURN_IF(launch_noop(c->comm_s));
       }
       FTAR_RETURN_IF(mark(c, "gather " + std::to_string(k) + " done", c->comm_s));
