@@ -56,7 +56,7 @@ for s in "${steps[@]}"; do
     xcdhi) run xcdhi 300 python3 -u tools/xcd_id_probe.py --procs 8 --iters ${XCD_ITERS:-400} --timeout 280 --out gpurun_out/xcd_probe.jsonl ${XCD_ARGS:-} ;;
     # stress_<config>[@cycles]: tools/host_comm_stress.py under one of its configurations
     stress_*) cfg=${s#stress_}; cyc=${cfg#*@}; [ "$cyc" = "$cfg" ] && cyc=${STRESS_CYCLES:-8}; cfg=${cfg%@*}
-              run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --out gpurun_out/stress.jsonl ;;
+              run "stress_$cfg" 900 python -u tools/host_comm_stress.py --config "$cfg" --cycles "$cyc" --cases "${STRESS_CASES:-c4_read,c5_write,c4_host_read,c5_host_write}" --timeout 840 --world "${STRESS_WORLD:-8}" --out gpurun_out/stress.jsonl ;;
     # c4_host_read on 8 processes with the engine's hand-off marks, checked by tools/host_order_check.py --marks
     hbmarks) rm -f gpurun_out/marks.jsonl; FTAR_STRESS_MARKS=1 run hbmarks 600 python -u tools/host_comm_stress.py --config "${HB_CONFIG:-current}" --cycles "${STRESS_CYCLES:-4}" --cases c4_host_read --timeout 500 --out gpurun_out/marks.jsonl &&
              python3 tools/host_order_check.py --marks gpurun_out/marks.jsonl --out gpurun_out/marks_check.json ;;

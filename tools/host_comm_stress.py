@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--cases", default="", help="comma-separated case names (default: the four default cases)")
     ap.add_argument("--out", default="")
     ap.add_argument("--timeout", type=int, default=600)
+    ap.add_argument("--world", type=int, default=8, help="processes (ranks) on the one GPU, 2..8")
     a = ap.parse_args()
     import host_comm_cases as hc
     cases = hc.CASES + hc.WIDE
@@ -63,13 +64,15 @@ def main():
         want = a.cases.split(",")
         cases = [c for c in cases if c[0] in want]
     t0 = time.time()
-    res = hc.run(cases, cycles=a.cycles, env=CONFIGS[a.config], timeout=a.timeout)
-    lines = hc.failures(res)
+    if not 2 <= a.world <= 8:
+        sys.exit("--world must be 2..8")
+    res = hc.run(cases, world=a.world, cycles=a.cycles, env=CONFIGS[a.config], timeout=a.timeout)
+    lines = hc.failures(res, world=a.world)
     if a.out:
         with open(a.out, "a") as f:
             for r in sorted(res):
                 for x in res[r].get("results", []):
-                    f.write(json.dumps(dict(x, rank=r, config=a.config)) + "\n")
+                    f.write(json.dumps(dict(x, rank=r, config=a.config, world=a.world)) + "\n")
                 if "error" in res[r]:
                     f.write(json.dumps({"rank": r, "config": a.config, "error": res[r]["error"]}) + "\n")
     ms = {}
@@ -86,7 +89,7 @@ def main():
                 elif key == "queues":
                     for q, c in v.items():
                         glog.setdefault("queues", {})[q] = glog.get("queues", {}).get(q, 0) + c
-    print(json.dumps({"config": a.config, "cycles": a.cycles, "cases": [c[0] for c in cases],
+    print(json.dumps({"config": a.config, "world": a.world, "cycles": a.cycles, "cases": [c[0] for c in cases],
                       "problems": len(lines), "seconds": round(time.time() - t0, 1),
                       "median_ms": {k: sorted(v)[len(v) // 2] for k, v in ms.items()},
                       **({"gather_log": glog} if glog else {})}))
