@@ -136,8 +136,8 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
     """The gather records of the last host call (FTAR_DEBUG_HOST_GATHER_LOG=1, engine_host.cpp log_gather):
     which workgroups left a record in host memory (not held in the GPU caches), how many times each workgroup
     id ran and on which XCDs (device-scope counters per id: 0 never, 2 handed out twice), on which XCD and
-    hardware queue they ran, and -- when the result is wrong -- the same for the workgroups that own the wrong tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).
-    Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
+    hardware queue they ran, and -- when the result is wrong -- the same for the workgroups that own the wrong
+    tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).  Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
     -> numpy uint32 reads the device records (2 words per workgroup; default: hipMemcpy)."""
     import collections
     import ctypes
@@ -179,7 +179,8 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
         out["runs"] += int(dev.astype(np.int64).sum())
         out["ids_run_twice"] += int((dev > 1).sum())
         out["xcc_is_w_mod_8"] += int((present_h & (xcc == w % 8)).sum())
-        pq = collections.Counter("me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(hw))) for hw in h[present_h, 1])
+        pq = collections.Counter("me{me}.pipe{pipe}.q{queue}".format(**hw_fields(int(hw)))
+                                 for hw in h[present_h, 1])
         for key, c in pq.items():
             out["queues"][key] = out["queues"].get(key, 0) + c
         # one dispatch whose workgroups ran from more than one hardware queue slot: the queue was unmapped
