@@ -137,8 +137,9 @@ def gather_forensics(comm, y, exp, tdt, read_dev=None):
     which workgroups left a record in host memory (not held in the GPU caches), how many times each workgroup
     id ran and on which XCDs (device-scope counters per id: 0 never, 2 handed out twice), on which XCD and
     hardware queue they ran, and -- when the result is wrong -- the same for the workgroups that own the wrong
-    tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).  Every piece is summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words)
-    -> numpy uint32 reads the device records (2 words per workgroup; default: hipMemcpy)."""
+    tiles (workgroup w copies tiles w / nsegs + j * grid / nsegs of segment w % nsegs).  Every piece is
+    summarised; the bad ones are listed with their workgroups' records.  read_dev(ptr, words) -> numpy uint32
+    reads the device records (2 words per workgroup; default: hipMemcpy)."""
     import collections
     import ctypes
 
